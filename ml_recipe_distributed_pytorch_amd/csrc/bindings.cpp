@@ -1,0 +1,283 @@
+// PyTorch bindings of the gfx950 kernels + RCCL reducer.  The only translation unit that includes
+// torch headers.  Every entry point validates device/dtype/contiguity/shape before launching — a
+// hand-written kernel must never see an operand whose shape its grid does not assume.
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include <limits>
+
+#include "hq_kernels.h"
+#include "hq_reducer.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(const Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_opt(const c10::optional<Tensor>& t, at::ScalarType dt, const char* name) {
+  if (t.has_value() && t->defined()) check(*t, dt, name);
+}
+template <typename T>
+T* ptr(const Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()); }
+template <typename T>
+T* optr(const c10::optional<Tensor>& t) { return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr; }
+
+const auto BF16 = at::kBFloat16;
+const auto F32 = at::kFloat;
+const auto I64 = at::kLong;
+
+HqOuts outs4(float* a, float* b = nullptr, float* c = nullptr, float* d = nullptr) { return HqOuts{{a, b, c, d}}; }
+
+uint32_t u32(int64_t v) { return (uint32_t)(v & 0xFFFFFFFFll); }
+
+// ------------------------------------------------------------------------------------ embedding
+std::vector<Tensor> embed_fwd(Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tensor wp, Tensor wt, Tensor gamma,
+                              Tensor beta, double eps, double p, int64_t seed, int64_t opid) {
+  check(ids, I64, "ids"); check(pids, I64, "pos_ids"); check(tids, I64, "type_ids");
+  check(ww, BF16, "w_word"); check(wp, BF16, "w_pos"); check(wt, BF16, "w_type");
+  check(gamma, F32, "gamma"); check(beta, F32, "beta");
+  const int64_t T = ids.numel(), H = ww.size(1);
+  TORCH_CHECK(pids.numel() == T && tids.numel() == T, "id length mismatch");
+  TORCH_CHECK(wp.size(1) == H && wt.size(1) == H && gamma.numel() == H && beta.numel() == H, "hidden mismatch");
+  TORCH_CHECK(H % 4 == 0 && H <= 2048, "hidden size must be a multiple of 4 and <= 2048");
+  TORCH_CHECK(T * H < (int64_t)std::numeric_limits<uint32_t>::max(), "T*H exceeds 32-bit dropout index");
+  c10::DeviceGuard g(ids.device());
+  auto y = at::empty({T, H}, ww.options());
+  auto mean = at::empty({T}, gamma.options());
+  auto rstd = at::empty({T}, gamma.options());
+  hq_embed_fwd(ptr<int64_t>(ids), ptr<int64_t>(pids), ptr<int64_t>(tids), ptr<uint16_t>(ww), ptr<uint16_t>(wp),
+               ptr<uint16_t>(wt), ptr<float>(gamma), ptr<float>(beta), ptr<uint16_t>(y), ptr<float>(mean), ptr<float>(rstd),
+               (int)T, (int)H, (float)eps, (float)p, u32(seed), u32(opid), cur_stream());
+  return {y, mean, rstd};
+}
+
+void embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tensor wp, Tensor wt, Tensor gamma, Tensor mean,
+               Tensor rstd, double p, int64_t seed, int64_t opid, Tensor g_word, Tensor g_pos, Tensor g_type, Tensor g_gamma,
+               Tensor g_beta, bool accumulate, int64_t pad_word, int64_t pad_pos) {
+  check(dy, BF16, "dy"); check(ids, I64, "ids"); check(pids, I64, "pos_ids"); check(tids, I64, "type_ids");
+  check(ww, BF16, "w_word"); check(wp, BF16, "w_pos"); check(wt, BF16, "w_type"); check(gamma, F32, "gamma");
+  check(mean, F32, "mean"); check(rstd, F32, "rstd");
+  check(g_word, F32, "g_word"); check(g_pos, F32, "g_pos"); check(g_type, F32, "g_type");
+  check(g_gamma, F32, "g_gamma"); check(g_beta, F32, "g_beta");
+  const int64_t T = ids.numel(), H = ww.size(1);
+  TORCH_CHECK(dy.size(0) == T && dy.size(1) == H, "dy shape");
+  TORCH_CHECK(g_word.sizes() == ww.sizes() && g_pos.sizes() == wp.sizes() && g_type.sizes() == wt.sizes(), "grad shapes");
+  const int n_types = (int)wt.size(0);
+  c10::DeviceGuard g(dy.device());
+  auto s = cur_stream();
+  if (!accumulate) {
+    hipMemsetAsync(g_word.data_ptr(), 0, g_word.numel() * 4, s);
+    hipMemsetAsync(g_pos.data_ptr(), 0, g_pos.numel() * 4, s);
+    if (n_types > 2) hipMemsetAsync(g_type.data_ptr(), 0, g_type.numel() * 4, s);
+  }
+  const int nb = hq_ln_bwd_partials((int)T);
+  auto part = at::empty({nb, 4 * H}, gamma.options());
+  float* t0 = ptr<float>(g_type);
+  HqOuts o = outs4(ptr<float>(g_gamma), ptr<float>(g_beta), n_types <= 2 ? t0 : nullptr,
+                   n_types == 2 ? t0 + H : nullptr);
+  hq_embed_bwd(ptr<uint16_t>(dy), ptr<int64_t>(ids), ptr<int64_t>(pids), ptr<int64_t>(tids), ptr<uint16_t>(ww),
+               ptr<uint16_t>(wp), ptr<uint16_t>(wt), ptr<float>(gamma), ptr<float>(mean), ptr<float>(rstd),
+               ptr<float>(g_word), ptr<float>(g_pos), t0, ptr<float>(part), o, (int)T, (int)H, n_types, (int)pad_word,
+               (int)pad_pos, (float)p, u32(seed), u32(opid), accumulate, s);
+}
+
+// ------------------------------------------------------------------ residual + dropout + LayerNorm
+std::vector<Tensor> ln_fwd(Tensor a, Tensor resid, Tensor gamma, Tensor beta, double eps, double p, int64_t seed, int64_t opid) {
+  check(a, BF16, "a"); check(resid, BF16, "resid"); check(gamma, F32, "gamma"); check(beta, F32, "beta");
+  TORCH_CHECK(a.dim() == 2 && a.sizes() == resid.sizes(), "a/resid shape");
+  const int64_t T = a.size(0), H = a.size(1);
+  TORCH_CHECK(gamma.numel() == H && beta.numel() == H && H % 4 == 0 && H <= 2048, "hidden size");
+  TORCH_CHECK(T * H < (int64_t)std::numeric_limits<uint32_t>::max(), "T*H exceeds 32-bit dropout index");
+  c10::DeviceGuard g(a.device());
+  auto y = at::empty_like(a), z = at::empty_like(a);
+  auto mean = at::empty({T}, gamma.options()), rstd = at::empty({T}, gamma.options());
+  hq_ln_fwd(ptr<uint16_t>(a), ptr<uint16_t>(resid), ptr<float>(gamma), ptr<float>(beta), ptr<uint16_t>(y), ptr<uint16_t>(z),
+            ptr<float>(mean), ptr<float>(rstd), (int)T, (int)H, (float)eps, (float)p, u32(seed), u32(opid), cur_stream());
+  return {y, z, mean, rstd};
+}
+
+std::vector<Tensor> ln_bwd(Tensor dy, c10::optional<Tensor> dy2, Tensor z, Tensor gamma, Tensor mean, Tensor rstd, double p,
+                           int64_t seed, int64_t opid, c10::optional<Tensor> g_gamma, c10::optional<Tensor> g_beta,
+                           c10::optional<Tensor> g_bias, bool accumulate) {
+  check(dy, BF16, "dy"); check_opt(dy2, BF16, "dy2"); check(z, BF16, "z"); check(gamma, F32, "gamma");
+  check(mean, F32, "mean"); check(rstd, F32, "rstd");
+  check_opt(g_gamma, F32, "g_gamma"); check_opt(g_beta, F32, "g_beta"); check_opt(g_bias, F32, "g_bias");
+  TORCH_CHECK(dy.sizes() == z.sizes(), "dy/z shape");
+  if (dy2.has_value() && dy2->defined()) TORCH_CHECK(dy2->sizes() == dy.sizes(), "dy2 shape");
+  const int64_t T = dy.size(0), H = dy.size(1);
+  TORCH_CHECK(gamma.numel() == H && mean.numel() == T && rstd.numel() == T, "stat shapes");
+  c10::DeviceGuard g(dy.device());
+  auto dz = at::empty_like(dy), da = at::empty_like(dy);
+  const int nb = hq_ln_bwd_partials((int)T);
+  auto part = at::empty({nb, 3 * H}, gamma.options());
+  hq_ln_bwd(ptr<uint16_t>(dy), optr<uint16_t>(dy2), ptr<uint16_t>(z), ptr<float>(gamma), ptr<float>(mean), ptr<float>(rstd),
+            ptr<uint16_t>(dz), ptr<uint16_t>(da), ptr<float>(part),
+            outs4(optr<float>(g_gamma), optr<float>(g_beta), optr<float>(g_bias)), (int)T, (int)H, (float)p, u32(seed),
+            u32(opid), accumulate, cur_stream());
+  return {dz, da};
+}
+
+// ------------------------------------------------------------------------------------------ GELU
+Tensor gelu_fwd(Tensor pre) {
+  check(pre, BF16, "pre");
+  TORCH_CHECK(pre.numel() % 8 == 0, "numel must be a multiple of 8");
+  c10::DeviceGuard g(pre.device());
+  auto out = at::empty_like(pre);
+  hq_gelu_fwd(ptr<uint16_t>(pre), ptr<uint16_t>(out), pre.numel(), cur_stream());
+  return out;
+}
+
+Tensor gelu_bwd(Tensor dout, Tensor pre, c10::optional<Tensor> g_bias, bool accumulate) {
+  check(dout, BF16, "dout"); check(pre, BF16, "pre"); check_opt(g_bias, F32, "g_bias");
+  TORCH_CHECK(dout.sizes() == pre.sizes() && dout.dim() == 2, "shape");
+  const int64_t T = dout.size(0), N = dout.size(1);
+  TORCH_CHECK(N % 8 == 0, "N must be a multiple of 8");
+  if (g_bias.has_value() && g_bias->defined()) TORCH_CHECK(g_bias->numel() == N, "g_bias shape");
+  c10::DeviceGuard g(dout.device());
+  auto dpre = at::empty_like(dout);
+  auto part = at::empty({hq_rowblock_partials((int)T), N}, dout.options().dtype(F32));
+  hq_gelu_bwd(ptr<uint16_t>(dout), ptr<uint16_t>(pre), ptr<uint16_t>(dpre), ptr<float>(part), outs4(optr<float>(g_bias)),
+              (int)T, (int)N, accumulate, cur_stream());
+  return dpre;
+}
+
+void bias_grad(Tensor dy, Tensor g_b, bool accumulate) {
+  check(dy, BF16, "dy"); check(g_b, F32, "g_b");
+  TORCH_CHECK(dy.dim() == 2 && g_b.numel() == dy.size(1) && dy.size(1) % 8 == 0, "shape");
+  const int64_t T = dy.size(0), N = dy.size(1);
+  c10::DeviceGuard g(dy.device());
+  auto part = at::empty({hq_rowblock_partials((int)T), N}, g_b.options());
+  hq_bias_grad(ptr<uint16_t>(dy), ptr<float>(part), outs4(ptr<float>(g_b)), (int)T, (int)N, accumulate, cur_stream());
+}
+
+// ------------------------------------------------------------------------------------- attention
+void check_attn(const Tensor& qkv, const Tensor& kb, int64_t B, int64_t L, int64_t nh) {
+  check(qkv, BF16, "qkv"); check(kb, F32, "key_bias");
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(0) == B * L, "qkv rows must be B*L");
+  TORCH_CHECK(qkv.size(1) % (3 * nh) == 0 && qkv.size(1) / (3 * nh) == 64, "head_dim must be 64");
+  TORCH_CHECK(kb.numel() == B * L, "key_bias must be [B, L]");
+  TORCH_CHECK(L >= 1 && B * nh < 65536, "grid limits");
+  TORCH_CHECK(B * nh * L * L < (int64_t)std::numeric_limits<uint32_t>::max(), "B*nh*L*L exceeds 32-bit dropout index");
+}
+
+std::vector<Tensor> attn_fwd(Tensor qkv, Tensor key_bias, int64_t B, int64_t L, int64_t nh, double p, int64_t seed,
+                             int64_t opid, double scale) {
+  check_attn(qkv, key_bias, B, L, nh);
+  const int64_t H = qkv.size(1) / 3;
+  c10::DeviceGuard g(qkv.device());
+  auto ctx = at::empty({B * L, H}, qkv.options());
+  auto lse = at::empty({B, nh, L}, key_bias.options());
+  hq_attn_fwd(ptr<uint16_t>(qkv), ptr<float>(key_bias), ptr<uint16_t>(ctx), ptr<float>(lse), (int)B, (int)L, (int)nh, 64,
+              (float)p, u32(seed), u32(opid), (float)scale, cur_stream());
+  return {ctx, lse};
+}
+
+Tensor attn_bwd(Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, int64_t B, int64_t L, int64_t nh, double p,
+                int64_t seed, int64_t opid, double scale) {
+  check_attn(qkv, key_bias, B, L, nh);
+  check(dctx, BF16, "dctx"); check(ctx, BF16, "ctx"); check(lse, F32, "lse");
+  const int64_t H = qkv.size(1) / 3;
+  TORCH_CHECK(dctx.size(0) == B * L && dctx.size(1) == H && ctx.sizes() == dctx.sizes(), "ctx shapes");
+  TORCH_CHECK(lse.numel() == B * nh * L, "lse shape");
+  c10::DeviceGuard g(qkv.device());
+  auto dqkv = at::empty_like(qkv);
+  auto delta = at::empty({B, nh, L}, lse.options());
+  hq_attn_bwd(ptr<uint16_t>(dctx), ptr<uint16_t>(qkv), ptr<uint16_t>(ctx), ptr<float>(lse), ptr<float>(key_bias),
+              ptr<uint16_t>(dqkv), ptr<float>(delta), (int)B, (int)L, (int)nh, 64, (float)p, u32(seed), u32(opid),
+              (float)scale, cur_stream());
+  return dqkv;
+}
+
+// ------------------------------------------------------------------------------------ optimizer
+std::vector<Tensor> grad_norm(Tensor grad, double max_norm) {
+  check(grad, F32, "grad");
+  c10::DeviceGuard g(grad.device());
+  const int nparts = 1024;
+  auto part = at::empty({nparts}, grad.options());
+  auto norm = at::empty({1}, grad.options());
+  auto coef = at::empty({1}, grad.options());
+  auto s = cur_stream();
+  hq_sq_norm_partials(ptr<float>(grad), grad.numel(), ptr<float>(part), nparts, s);
+  hq_clip_coef(ptr<float>(part), nparts, (float)max_norm, ptr<float>(norm), ptr<float>(coef), s);
+  return {norm, coef};
+}
+
+HqOptGroups groups_of(const std::vector<double>& lr, const std::vector<double>& wd) {
+  TORCH_CHECK(lr.size() == wd.size() && lr.size() <= (size_t)kOptMaxGroups, "at most 8 param groups");
+  HqOptGroups gr{};
+  for (size_t i = 0; i < lr.size(); ++i) { gr.lr[i] = (float)lr[i]; gr.wd[i] = (float)wd[i]; }
+  return gr;
+}
+
+void adamw(Tensor master, c10::optional<Tensor> compute, Tensor grad, Tensor m, Tensor v, Tensor chunks,
+           std::vector<double> lr, std::vector<double> wd, double beta1, double beta2, double eps, double step_mult,
+           c10::optional<Tensor> clip_coef) {
+  check(master, F32, "master"); check_opt(compute, BF16, "compute"); check(grad, F32, "grad");
+  check(m, F32, "exp_avg"); check(v, F32, "exp_avg_sq"); check(chunks, I64, "chunks"); check_opt(clip_coef, F32, "clip");
+  TORCH_CHECK(grad.numel() == master.numel() && m.numel() == master.numel() && v.numel() == master.numel(), "arena sizes");
+  if (compute.has_value() && compute->defined()) TORCH_CHECK(compute->numel() == master.numel(), "compute size");
+  TORCH_CHECK(chunks.dim() == 2 && chunks.size(1) == 2, "chunks must be [n,2] int64");
+  c10::DeviceGuard g(master.device());
+  hq_adamw(ptr<float>(master), optr<uint16_t>(compute), ptr<float>(grad), ptr<float>(m), ptr<float>(v),
+           reinterpret_cast<const HqOptChunk*>(chunks.data_ptr()), (int)chunks.size(0), groups_of(lr, wd), (float)beta1,
+           (float)beta2, (float)eps, (float)step_mult, optr<float>(clip_coef), cur_stream());
+}
+
+void adamod(Tensor master, c10::optional<Tensor> compute, Tensor grad, Tensor m, Tensor v, Tensor n, Tensor chunks,
+            std::vector<double> lr, std::vector<double> wd, double beta1, double beta2, double beta3, double eps,
+            double bias_corr, c10::optional<Tensor> clip_coef) {
+  check(master, F32, "master"); check_opt(compute, BF16, "compute"); check(grad, F32, "grad");
+  check(m, F32, "exp_avg"); check(v, F32, "exp_avg_sq"); check(n, F32, "exp_avg_lr"); check(chunks, I64, "chunks");
+  check_opt(clip_coef, F32, "clip");
+  TORCH_CHECK(grad.numel() == master.numel() && m.numel() == master.numel() && v.numel() == master.numel() &&
+                  n.numel() == master.numel(), "arena sizes");
+  c10::DeviceGuard g(master.device());
+  hq_adamod(ptr<float>(master), optr<uint16_t>(compute), ptr<float>(grad), ptr<float>(m), ptr<float>(v), ptr<float>(n),
+            reinterpret_cast<const HqOptChunk*>(chunks.data_ptr()), (int)chunks.size(0), groups_of(lr, wd), (float)beta1,
+            (float)beta2, (float)beta3, (float)eps, (float)bias_corr, optr<float>(clip_coef), cur_stream());
+}
+
+void cast_f32_bf16(Tensor src, Tensor dst, double scale) {
+  check(src, F32, "src"); check(dst, BF16, "dst");
+  TORCH_CHECK(src.numel() == dst.numel(), "size");
+  c10::DeviceGuard g(src.device());
+  hq_cast_f32_bf16(ptr<float>(src), ptr<uint16_t>(dst), src.numel(), (float)scale, cur_stream());
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_hq_kernels, m) {
+  m.doc() = "gfx950 HIP kernels + RCCL reducer for ml_recipe_distributed_pytorch_amd";
+  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_bwd", &embed_bwd);
+  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_bwd", &ln_bwd);
+  m.def("gelu_fwd", &gelu_fwd);
+  m.def("gelu_bwd", &gelu_bwd);
+  m.def("bias_grad", &bias_grad);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("grad_norm", &grad_norm);
+  m.def("adamw", &adamw);
+  m.def("adamod", &adamod);
+  m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("rccl_unique_id", []() { return py::bytes(hq_rccl_unique_id()); });
+  py::class_<HqReducer>(m, "Reducer")
+      .def(py::init([](int rank, int world, py::bytes uid, int device) {
+             return new HqReducer(rank, world, std::string(uid), device);
+           }))
+      .def("allreduce_f32", &HqReducer::allreduce_f32, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_bf16", &HqReducer::allreduce_bf16, py::call_guard<py::gil_scoped_release>())
+      .def("broadcast", &HqReducer::broadcast, py::call_guard<py::gil_scoped_release>())
+      .def("wait", &HqReducer::wait)
+      .def("synchronize", &HqReducer::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("comm_stream", &HqReducer::comm_stream)
+      .def_property_readonly("rank", &HqReducer::rank)
+      .def_property_readonly("world", &HqReducer::world);
+}

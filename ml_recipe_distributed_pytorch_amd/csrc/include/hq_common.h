@@ -1,0 +1,98 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels.
+// - wave64 reductions (never 32-wide warp idioms)
+// - bf16 <-> f32 packing for 8/16-byte vector access
+// - the counter-hash dropout RNG, bit-identical to ml_recipe_distributed_pytorch_amd/ops/rng.py
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define HQ_WAVE 64
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // MFMA A/B fragment (4 VGPRs)
+typedef __attribute__((ext_vector_type(4))) short bf16x4_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;  // 32x32 MFMA accumulator
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+// ------------------------------------------------------------------------------ bf16 helpers
+__device__ __forceinline__ float hq_bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+__device__ __forceinline__ uint16_t hq_f2bf(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);   // RNE; hipcc emits v_cvt_pk_bf16_f32 on gfx950
+  return *reinterpret_cast<uint16_t*>(&b);
+}
+__device__ __forceinline__ uint32_t hq_pack2(float lo, float hi) {
+  return (uint32_t)hq_f2bf(lo) | ((uint32_t)hq_f2bf(hi) << 16);
+}
+__device__ __forceinline__ void hq_unpack8(const uint4& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xFFFF0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xFFFF0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xFFFF0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xFFFF0000u);
+}
+__device__ __forceinline__ uint4 hq_pack8(const float* f) {
+  return make_uint4(hq_pack2(f[0], f[1]), hq_pack2(f[2], f[3]), hq_pack2(f[4], f[5]), hq_pack2(f[6], f[7]));
+}
+__device__ __forceinline__ void hq_unpack4(const uint2& v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xFFFF0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xFFFF0000u);
+}
+__device__ __forceinline__ uint2 hq_pack4(const float* f) {
+  return make_uint2(hq_pack2(f[0], f[1]), hq_pack2(f[2], f[3]));
+}
+
+// ------------------------------------------------------------------------------ reductions
+__device__ __forceinline__ float hq_wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float hq_wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ------------------------------------------------------------------------------ dropout RNG
+// key = fmix32(seed ^ opid*0x9E3779B9) is computed on the host (hq_op_key) once per op.
+__host__ __device__ __forceinline__ uint32_t hq_fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16; return h;
+}
+static inline uint32_t hq_op_key(uint32_t seed, uint32_t opid) { return hq_fmix32(seed ^ (opid * 0x9E3779B9u)); }
+static inline uint32_t hq_threshold(float p) { return (uint32_t)__builtin_rintf(p * 65536.0f); }
+static inline float hq_keep_scale(uint32_t thr) { return thr < 65536u ? 65536.0f / (float)(65536u - thr) : 0.f; }
+
+// 32-bit hash covering the element pair (2i, 2i+1)
+__device__ __forceinline__ uint32_t hq_pair_hash(uint32_t idx_even, uint32_t key) {
+  return hq_fmix32(((idx_even >> 1) * 0x9E3779B1u) ^ key);
+}
+__device__ __forceinline__ bool hq_keep(uint32_t idx, uint32_t key, uint32_t thr) {
+  uint32_t h = hq_pair_hash(idx, key);
+  uint32_t u = (h >> ((idx & 1u) * 16u)) & 0xFFFFu;
+  return u >= thr;
+}
+// keep-multipliers (0 or scale) for 8 consecutive elements starting at an even index
+__device__ __forceinline__ void hq_keep8(uint32_t idx0, uint32_t key, uint32_t thr, float scale, float* m) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint32_t h = hq_pair_hash(idx0 + 2 * i, key);
+    m[2 * i] = ((h & 0xFFFFu) >= thr) ? scale : 0.f;
+    m[2 * i + 1] = ((h >> 16) >= thr) ? scale : 0.f;
+  }
+}
+__device__ __forceinline__ void hq_keep4(uint32_t idx0, uint32_t key, uint32_t thr, float scale, float* m) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    uint32_t h = hq_pair_hash(idx0 + 2 * i, key);
+    m[2 * i] = ((h & 0xFFFFu) >= thr) ? scale : 0.f;
+    m[2 * i + 1] = ((h >> 16) >= thr) ? scale : 0.f;
+  }
+}
+
+#define HQ_CHECK(x)                                                                       \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess) {                                                               \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); \
+      abort();                                                                            \
+    }                                                                                     \
+  } while (0)

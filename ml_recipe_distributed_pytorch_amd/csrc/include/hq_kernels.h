@@ -1,0 +1,62 @@
+// Host-side launch interface of the gfx950 kernels (raw pointers + hipStream_t; no torch headers,
+// so each .hip translation unit compiles in seconds).  bindings.cpp wraps these for PyTorch.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <algorithm>
+#include <type_traits>
+
+struct HqOuts {  // up to 4 fp32 column-sum destinations (null = skip), passed by value
+  float* p[4];
+};
+
+// ---- norm.hip --------------------------------------------------------------------------------
+int hq_ln_bwd_partials(int T);
+int hq_rowblock_partials(int T);
+void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, const float* beta, uint16_t* y, uint16_t* z,
+               float* mean, float* rstd, int T, int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s);
+void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const float* gamma, const float* mean,
+               const float* rstd, uint16_t* dz, uint16_t* da, float* part, HqOuts outs, int T, int H, float p,
+               uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s);
+void hq_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww, const uint16_t* wp,
+                  const uint16_t* wt, const float* gamma, const float* beta, uint16_t* y, float* mean, float* rstd, int T,
+                  int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s);
+void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww,
+                  const uint16_t* wp, const uint16_t* wt, const float* gamma, const float* mean, const float* rstd,
+                  float* g_word, float* g_pos, float* g_type, float* part, HqOuts outs, int T, int H, int n_types,
+                  int pad_word, int pad_pos, float p, uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s);
+void hq_gelu_fwd(const uint16_t* pre, uint16_t* out, size_t n, hipStream_t s);
+void hq_gelu_bwd(const uint16_t* dout, const uint16_t* pre, uint16_t* dpre, float* part, HqOuts outs, int T, int N,
+                 bool accumulate, hipStream_t s);
+void hq_bias_grad(const uint16_t* dy, float* part, HqOuts outs, int T, int N, bool accumulate, hipStream_t s);
+
+// ---- attention.hip ----------------------------------------------------------------------------
+void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, float* lse, int B, int L, int nh, int dh,
+                 float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s);
+void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx, const float* lse, const float* key_bias,
+                 uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p, uint32_t seed, uint32_t opid,
+                 float scale, hipStream_t s);
+
+// ---- optim.hip --------------------------------------------------------------------------------
+struct HqOptChunk {      // one work item of the fused optimizer: <= kOptChunk elements of one segment
+  int64_t start;
+  int32_t numel;
+  int32_t group;         // param group index (weight decay / lr factor table)
+};
+constexpr int kOptChunk = 8192;
+constexpr int kOptMaxGroups = 8;
+struct HqOptGroups {
+  float lr[kOptMaxGroups];
+  float wd[kOptMaxGroups];
+};
+void hq_sq_norm_partials(const float* g, int64_t n, float* partials, int nparts, hipStream_t s);
+void hq_clip_coef(const float* partials, int nparts, float max_norm, float* norm_out, float* coef_out, hipStream_t s);
+void hq_adamw(float* master, uint16_t* compute, const float* grad, float* m, float* v, const HqOptChunk* chunks,
+              int nchunks, HqOptGroups groups, float beta1, float beta2, float eps, float step_size_mult,
+              const float* clip_coef, hipStream_t s);
+void hq_adamod(float* master, uint16_t* compute, const float* grad, float* m, float* v, float* n, const HqOptChunk* chunks,
+               int nchunks, HqOptGroups groups, float beta1, float beta2, float beta3, float eps, float bias_corr,
+               const float* clip_coef, hipStream_t s);
+void hq_cast_f32_bf16(const float* src, uint16_t* dst, int64_t n, float scale, hipStream_t s);
+void hq_cast_bf16_f32(const uint16_t* src, float* dst, int64_t n, float scale, hipStream_t s);

@@ -1,0 +1,35 @@
+// RCCL flat-bucket gradient reducer (see runtime/reducer.cpp).  No torch / rccl types in the
+// interface so bindings.cpp does not need the RCCL headers.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+
+std::string hq_rccl_unique_id();
+
+class HqReducer {
+ public:
+  HqReducer(int rank, int world, const std::string& unique_id, int device);
+  ~HqReducer();
+  HqReducer(const HqReducer&) = delete;
+  HqReducer& operator=(const HqReducer&) = delete;
+
+  void allreduce_f32(int64_t ptr, int64_t count, int64_t compute_stream);
+  void allreduce_bf16(int64_t ptr_f32, int64_t scratch_bf16, int64_t count, int64_t compute_stream);
+  void broadcast(int64_t ptr, int64_t count, int dtype, int root, int64_t compute_stream);
+  void wait(int64_t compute_stream);
+  void synchronize();
+  int64_t comm_stream() const { return (int64_t)stream_; }
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+
+ private:
+  static constexpr int kEvents = 64;
+  void* next_event();
+  void fence_from(int64_t compute_stream);
+  int rank_, world_, device_;
+  void* comm_ = nullptr;
+  void* stream_ = nullptr;
+  void* events_[kEvents] = {};
+  int ev_idx_ = 0;
+};

@@ -1,0 +1,506 @@
+// Row-wise fused kernels for the BERT encoder (gfx950, wave64).
+//
+//   ln_fwd   : z = dropout(a) + resid (rounded to bf16, as HF under autocast) ; y = LN(z)
+//   ln_bwd   : dz = LN_bwd(dy [+ dy2]) ; da = dropout_bwd(dz) ; per-block partial Σ(g·x̂), Σg, Σda
+//   embed_fwd: y = dropout(LN(word[id] + pos[pid] + type[tid]))
+//   embed_bwd: recompute x̂, LN_bwd, f32 atomics into word/pos grads (256-B contiguous per wave
+//              instruction via an LDS transpose), type/γ/β grads through deterministic partials
+//   gelu_fwd / gelu_bwd(+bias grad partials), bias_grad partials, colsum finalize
+//
+// Layout: one wave per row; lane owns 4 consecutive columns per 256-column chunk (8-byte bf16
+// vector access), NCH = ceil(H/256) chunks.  Column partial sums are reduced per block through
+// LDS and finished by hq_colsum (one 1024-thread block per 64 columns), so every gradient is
+// bitwise deterministic except the word/position embedding scatter (float atomics).
+#include "hq_common.h"
+#include "hq_kernels.h"
+
+namespace {
+
+constexpr int kRowsPerWave = 8;   // rows a wave walks in the backward kernels
+constexpr int kWaves = 4;         // 256-thread blocks
+
+template <int NCH>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict__ a, const uint16_t* __restrict__ resid,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     uint16_t* __restrict__ y, uint16_t* __restrict__ z,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out, int T,
+                                                     int H, float eps, uint32_t key, uint32_t thr, float kscale) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kWaves + wave;
+  if (row >= T) return;
+  const size_t base = (size_t)row * H;
+  float v[NCH][4];
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    if (col < H) {
+      float fa[4], fr[4], m[4] = {1.f, 1.f, 1.f, 1.f};
+      hq_unpack4(*reinterpret_cast<const uint2*>(a + base + col), fa);
+      hq_unpack4(*reinterpret_cast<const uint2*>(resid + base + col), fr);
+      if (thr) hq_keep4((uint32_t)(base + col), key, thr, kscale, m);
+      float zz[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) zz[i] = fa[i] * m[i] + fr[i];
+      uint2 packed = hq_pack4(zz);
+      *reinterpret_cast<uint2*>(z + base + col) = packed;
+      hq_unpack4(packed, v[c]);  // statistics of the stored (bf16) z, so backward is consistent
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sum += v[c][i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[c][i] = 0.f;
+    }
+  }
+  const float mean = hq_wave_sum(sum) / H;
+  float sq = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    if (col < H) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { float d = v[c][i] - mean; sq += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(hq_wave_sum(sq) / H + eps);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    if (col < H) {
+      const float4 g = *reinterpret_cast<const float4*>(gamma + col);
+      const float4 b = *reinterpret_cast<const float4*>(beta + col);
+      float o[4] = {(v[c][0] - mean) * rstd * g.x + b.x, (v[c][1] - mean) * rstd * g.y + b.y,
+                    (v[c][2] - mean) * rstd * g.z + b.z, (v[c][3] - mean) * rstd * g.w + b.w};
+      *reinterpret_cast<uint2*>(y + base + col) = hq_pack4(o);
+    }
+  }
+  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+}
+
+// Reduce NQ per-lane column accumulators over the 4 waves of the block into part[block][q][H].
+template <int NCH, int NQ>
+__device__ __forceinline__ void block_partials(float (&acc)[NQ][NCH][4], float* lds, float* part, int H) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 256 + lane * 4;
+      if (col < H) *reinterpret_cast<float4*>(lds + wave * H + col) = make_float4(acc[q][c][0], acc[q][c][1], acc[q][c][2], acc[q][c][3]);
+    }
+    __syncthreads();
+    for (int col = threadIdx.x; col < H; col += 256) {
+      float s = lds[col] + lds[H + col] + lds[2 * H + col] + lds[3 * H + col];
+      part[((size_t)blockIdx.x * NQ + q) * H + col] = s;
+    }
+    __syncthreads();
+  }
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dy2,
+                                                     const uint16_t* __restrict__ z, const float* __restrict__ gamma,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     uint16_t* __restrict__ dz_out, uint16_t* __restrict__ da_out,
+                                                     float* __restrict__ part, int T, int H, uint32_t key, uint32_t thr,
+                                                     float kscale) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float acc[3][NCH][4];
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[q][c][i] = 0.f;
+  float gam[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    float4 g = col < H ? *reinterpret_cast<const float4*>(gamma + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gam[c][0] = g.x; gam[c][1] = g.y; gam[c][2] = g.z; gam[c][3] = g.w;
+  }
+  const int row0 = blockIdx.x * kWaves * kRowsPerWave;
+  for (int r = 0; r < kRowsPerWave; ++r) {
+    const int row = row0 + r * kWaves + wave;
+    if (row >= T) break;
+    const size_t base = (size_t)row * H;
+    const float mu = mean[row], rs = rstd[row];
+    float g[NCH][4], xh[NCH][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 256 + lane * 4;
+      if (col < H) {
+        float fz[4];
+        hq_unpack4(*reinterpret_cast<const uint2*>(dy + base + col), g[c]);
+        if (dy2) {
+          float f2[4];
+          hq_unpack4(*reinterpret_cast<const uint2*>(dy2 + base + col), f2);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) g[c][i] += f2[i];
+        }
+        hq_unpack4(*reinterpret_cast<const uint2*>(z + base + col), fz);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          xh[c][i] = (fz[i] - mu) * rs;
+          acc[0][c][i] += g[c][i] * xh[c][i];
+          acc[1][c][i] += g[c][i];
+          const float dxh = g[c][i] * gam[c][i];
+          s1 += dxh;
+          s2 += dxh * xh[c][i];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { g[c][i] = 0.f; xh[c][i] = 0.f; }
+      }
+    }
+    s1 = hq_wave_sum(s1) / H;
+    s2 = hq_wave_sum(s2) / H;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 256 + lane * 4;
+      if (col < H) {
+        float dz[4], m[4] = {1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dz[i] = rs * (g[c][i] * gam[c][i] - s1 - xh[c][i] * s2);
+        *reinterpret_cast<uint2*>(dz_out + base + col) = hq_pack4(dz);
+        if (thr) hq_keep4((uint32_t)(base + col), key, thr, kscale, m);
+        float da[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { da[i] = dz[i] * m[i]; acc[2][c][i] += da[i]; }
+        *reinterpret_cast<uint2*>(da_out + base + col) = hq_pack4(da);
+      }
+    }
+  }
+  block_partials<NCH, 3>(acc, lds, part, H);
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ pids,
+                                                        const int64_t* __restrict__ tids, const uint16_t* __restrict__ ww,
+                                                        const uint16_t* __restrict__ wp, const uint16_t* __restrict__ wt,
+                                                        const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                        uint16_t* __restrict__ y, float* __restrict__ mean_out,
+                                                        float* __restrict__ rstd_out, int T, int H, float eps, uint32_t key,
+                                                        uint32_t thr, float kscale) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kWaves + wave;
+  if (row >= T) return;
+  const size_t rw = (size_t)ids[row] * H, rp = (size_t)pids[row] * H, rt = (size_t)tids[row] * H;
+  float v[NCH][4];
+  float sum = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    if (col < H) {
+      float f1[4], f2[4], f3[4];
+      hq_unpack4(*reinterpret_cast<const uint2*>(ww + rw + col), f1);
+      hq_unpack4(*reinterpret_cast<const uint2*>(wp + rp + col), f2);
+      hq_unpack4(*reinterpret_cast<const uint2*>(wt + rt + col), f3);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { v[c][i] = f1[i] + f2[i] + f3[i]; sum += v[c][i]; }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[c][i] = 0.f;
+    }
+  }
+  const float mu = hq_wave_sum(sum) / H;
+  float sq = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+    if (c * 256 + lane * 4 < H)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { float d = v[c][i] - mu; sq += d * d; }
+  const float rs = rsqrtf(hq_wave_sum(sq) / H + eps);
+  const size_t base = (size_t)row * H;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    if (col < H) {
+      const float4 g = *reinterpret_cast<const float4*>(gamma + col);
+      const float4 b = *reinterpret_cast<const float4*>(beta + col);
+      float m[4] = {1.f, 1.f, 1.f, 1.f};
+      if (thr) hq_keep4((uint32_t)(base + col), key, thr, kscale, m);
+      float o[4] = {((v[c][0] - mu) * rs * g.x + b.x) * m[0], ((v[c][1] - mu) * rs * g.y + b.y) * m[1],
+                    ((v[c][2] - mu) * rs * g.z + b.z) * m[2], ((v[c][3] - mu) * rs * g.w + b.w) * m[3]};
+      *reinterpret_cast<uint2*>(y + base + col) = hq_pack4(o);
+    }
+  }
+  if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
+}
+
+// part layout per block: [gamma | beta | type0 | type1] × H
+template <int NCH>
+__global__ __launch_bounds__(256) void embed_bwd_kernel(
+    const uint16_t* __restrict__ dy, const int64_t* __restrict__ ids, const int64_t* __restrict__ pids,
+    const int64_t* __restrict__ tids, const uint16_t* __restrict__ ww, const uint16_t* __restrict__ wp,
+    const uint16_t* __restrict__ wt, const float* __restrict__ gamma, const float* __restrict__ mean,
+    const float* __restrict__ rstd, float* __restrict__ g_word, float* __restrict__ g_pos, float* __restrict__ g_type,
+    float* __restrict__ part, int T, int H, int n_types, int pad_word, int pad_pos, uint32_t key, uint32_t thr,
+    float kscale) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][H] reduction scratch, reused as dx rows
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float acc[4][NCH][4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[q][c][i] = 0.f;
+  float gam[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    float4 g = col < H ? *reinterpret_cast<const float4*>(gamma + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gam[c][0] = g.x; gam[c][1] = g.y; gam[c][2] = g.z; gam[c][3] = g.w;
+  }
+  float* myrow = lds + wave * H;
+  const int row0 = blockIdx.x * kWaves * kRowsPerWave;
+  for (int r = 0; r < kRowsPerWave; ++r) {
+    const int row = row0 + r * kWaves + wave;
+    if (row >= T) break;
+    const int64_t id = ids[row], pid = pids[row], tid = tids[row];
+    const size_t base = (size_t)row * H;
+    const float mu = mean[row], rs = rstd[row];
+    float g[NCH][4], xh[NCH][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 256 + lane * 4;
+      if (col < H) {
+        float f1[4], f2[4], f3[4], m[4] = {1.f, 1.f, 1.f, 1.f};
+        hq_unpack4(*reinterpret_cast<const uint2*>(ww + (size_t)id * H + col), f1);
+        hq_unpack4(*reinterpret_cast<const uint2*>(wp + (size_t)pid * H + col), f2);
+        hq_unpack4(*reinterpret_cast<const uint2*>(wt + (size_t)tid * H + col), f3);
+        hq_unpack4(*reinterpret_cast<const uint2*>(dy + base + col), g[c]);
+        if (thr) hq_keep4((uint32_t)(base + col), key, thr, kscale, m);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          g[c][i] *= m[i];
+          xh[c][i] = (f1[i] + f2[i] + f3[i] - mu) * rs;
+          acc[0][c][i] += g[c][i] * xh[c][i];
+          acc[1][c][i] += g[c][i];
+          const float dxh = g[c][i] * gam[c][i];
+          s1 += dxh;
+          s2 += dxh * xh[c][i];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { g[c][i] = 0.f; xh[c][i] = 0.f; }
+      }
+    }
+    s1 = hq_wave_sum(s1) / H;
+    s2 = hq_wave_sum(s2) / H;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 256 + lane * 4;
+      if (col < H) {
+        float dx[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dx[i] = rs * (g[c][i] * gam[c][i] - s1 - xh[c][i] * s2);
+        if (n_types <= 2) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[2 + (tid & 1)][c][i] += dx[i];
+        }
+        *reinterpret_cast<float4*>(myrow + col) = make_float4(dx[0], dx[1], dx[2], dx[3]);
+      }
+    }
+    // wave-private LDS row, re-read lane-contiguous so each atomic wave-instruction is 256 B contiguous
+    // (LDS ops of one wave complete in issue order; the aliasing stores keep the compiler order)
+    const bool do_word = (int)id != pad_word, do_pos = (int)pid != pad_pos;
+    for (int col = lane; col < H; col += 64) {
+      const float d = myrow[col];
+      if (do_word) atomicAdd(g_word + (size_t)id * H + col, d);
+      if (do_pos) atomicAdd(g_pos + (size_t)pid * H + col, d);
+      if (n_types > 2) atomicAdd(g_type + (size_t)tid * H + col, d);
+    }
+  }
+  __syncthreads();
+  block_partials<NCH, 4>(acc, lds, part, H);
+}
+
+__global__ __launch_bounds__(256) void gelu_fwd_kernel(const uint16_t* __restrict__ pre, uint16_t* __restrict__ out, size_t n8) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float x[8], o[8];
+    hq_unpack8(reinterpret_cast<const uint4*>(pre)[i], x);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = 0.5f * x[k] * (1.f + erff(x[k] * 0.70710678118654752f));
+    reinterpret_cast<uint4*>(out)[i] = hq_pack8(o);
+  }
+}
+
+// dpre = dout * gelu'(pre); per-block column partials of dpre.  Block: 256 threads × 8 columns =
+// 2048-column tile, kRowsBlock rows.  grid = (ceil(N/2048), ceil(T/kRowsBlock)).
+constexpr int kRowsBlock = 32;
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const uint16_t* __restrict__ dout, const uint16_t* __restrict__ pre,
+                                                       uint16_t* __restrict__ dpre, float* __restrict__ part, int T, int N) {
+  const int col = (blockIdx.x * 256 + threadIdx.x) * 8;
+  const int r0 = blockIdx.y * kRowsBlock;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (col < N) {
+    for (int r = r0; r < min(T, r0 + kRowsBlock); ++r) {
+      const size_t off = (size_t)r * N + col;
+      float d[8], x[8], o[8];
+      hq_unpack8(*reinterpret_cast<const uint4*>(dout + off), d);
+      hq_unpack8(*reinterpret_cast<const uint4*>(pre + off), x);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float cdf = 0.5f * (1.f + erff(x[k] * 0.70710678118654752f));
+        const float pdf = __expf(-0.5f * x[k] * x[k]) * 0.3989422804014327f;
+        o[k] = d[k] * (cdf + x[k] * pdf);
+        acc[k] += o[k];
+      }
+      *reinterpret_cast<uint4*>(dpre + off) = hq_pack8(o);
+    }
+    float* dst = part + (size_t)blockIdx.y * N + col;
+    *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *reinterpret_cast<float4*>(dst + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  }
+}
+
+__global__ __launch_bounds__(256) void colpart_kernel(const uint16_t* __restrict__ x, float* __restrict__ part, int T, int N) {
+  const int col = (blockIdx.x * 256 + threadIdx.x) * 8;
+  const int r0 = blockIdx.y * kRowsBlock;
+  if (col >= N) return;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = r0; r < min(T, r0 + kRowsBlock); ++r) {
+    float d[8];
+    hq_unpack8(*reinterpret_cast<const uint4*>(x + (size_t)r * N + col), d);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] += d[k];
+  }
+  float* dst = part + (size_t)blockIdx.y * N + col;
+  *reinterpret_cast<float4*>(dst) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  *reinterpret_cast<float4*>(dst + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+}
+
+// out[q*H + c] (+)= Σ_p part[p][q][c]   for the columns named by (Q, H): part is [P][Q*H].
+// One 1024-thread block per 64 columns; 16 waves stride over P; LDS combine.  Deterministic.
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ part, int P, int N, HqOuts outs, int Hq, int accumulate) {
+  __shared__ float red[16][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int col = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (col < N) {
+    int p = wave;
+    for (; p + 48 < P; p += 64) {
+      s += part[(size_t)p * N + col] + part[(size_t)(p + 16) * N + col] + part[(size_t)(p + 32) * N + col] +
+           part[(size_t)(p + 48) * N + col];
+    }
+    for (; p < P; p += 16) s += part[(size_t)p * N + col];
+  }
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && col < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w][lane];
+    float* out = outs.p[col / Hq];
+    if (out) {
+      const int c = col % Hq;
+      out[c] = accumulate ? out[c] + t : t;
+    }
+  }
+}
+
+template <typename F>
+void dispatch_nch(int H, F&& f) {
+  const int nch = (H + 255) / 256;
+  switch (nch) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 5: f(std::integral_constant<int, 5>{}); break;
+    case 6: f(std::integral_constant<int, 6>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    default: fprintf(stderr, "hq: unsupported hidden size %d\n", H); abort();
+  }
+}
+
+void colsum(const float* part, int P, int N, HqOuts outs, int Hq, bool accumulate, hipStream_t s) {
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, part, P, N, outs, Hq, accumulate ? 1 : 0);
+}
+
+}  // namespace
+
+// ================================================================================== launchers
+void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, const float* beta, uint16_t* y, uint16_t* z,
+               float* mean, float* rstd, int T, int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s) {
+  const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
+  const uint32_t key = hq_op_key(seed, opid);
+  const float ks = hq_keep_scale(thr);
+  dispatch_nch(H, [&](auto nch) {
+    hipLaunchKernelGGL(ln_fwd_kernel<decltype(nch)::value>, dim3((T + kWaves - 1) / kWaves), dim3(256), 0, s, a, resid,
+                       gamma, beta, y, z, mean, rstd, T, H, eps, key, thr, ks);
+  });
+}
+
+int hq_ln_bwd_partials(int T) { return (T + kWaves * kRowsPerWave - 1) / (kWaves * kRowsPerWave); }
+
+void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const float* gamma, const float* mean,
+               const float* rstd, uint16_t* dz, uint16_t* da, float* part, HqOuts outs, int T, int H, float p,
+               uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s) {
+  const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
+  const uint32_t key = hq_op_key(seed, opid);
+  const float ks = hq_keep_scale(thr);
+  const int nb = hq_ln_bwd_partials(T);
+  dispatch_nch(H, [&](auto nch) {
+    hipLaunchKernelGGL(ln_bwd_kernel<decltype(nch)::value>, dim3(nb), dim3(256), 4 * H * sizeof(float), s, dy, dy2, z,
+                       gamma, mean, rstd, dz, da, part, T, H, key, thr, ks);
+  });
+  colsum(part, nb, 3 * H, outs, H, accumulate, s);
+}
+
+void hq_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww, const uint16_t* wp,
+                  const uint16_t* wt, const float* gamma, const float* beta, uint16_t* y, float* mean, float* rstd, int T,
+                  int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s) {
+  const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
+  const uint32_t key = hq_op_key(seed, opid);
+  const float ks = hq_keep_scale(thr);
+  dispatch_nch(H, [&](auto nch) {
+    hipLaunchKernelGGL(embed_fwd_kernel<decltype(nch)::value>, dim3((T + kWaves - 1) / kWaves), dim3(256), 0, s, ids,
+                       pids, tids, ww, wp, wt, gamma, beta, y, mean, rstd, T, H, eps, key, thr, ks);
+  });
+}
+
+void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww,
+                  const uint16_t* wp, const uint16_t* wt, const float* gamma, const float* mean, const float* rstd,
+                  float* g_word, float* g_pos, float* g_type, float* part, HqOuts outs, int T, int H,
+                  int n_types, int pad_word, int pad_pos, float p, uint32_t seed, uint32_t opid, bool accumulate,
+                  hipStream_t s) {
+  const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
+  const uint32_t key = hq_op_key(seed, opid);
+  const float ks = hq_keep_scale(thr);
+  const int nb = hq_ln_bwd_partials(T);
+  dispatch_nch(H, [&](auto nch) {
+    hipLaunchKernelGGL(embed_bwd_kernel<decltype(nch)::value>, dim3(nb), dim3(256), 4 * H * sizeof(float), s, dy, ids,
+                       pids, tids, ww, wp, wt, gamma, mean, rstd, g_word, g_pos, g_type, part, T, H, n_types, pad_word,
+                       pad_pos, key, thr, ks);
+  });
+  // outs: gamma, beta, type0, type1 (type rows only when n_types <= 2)
+  colsum(part, nb, 4 * H, outs, H, accumulate, s);
+}
+
+void hq_gelu_fwd(const uint16_t* pre, uint16_t* out, size_t n, hipStream_t s) {
+  const size_t n8 = n / 8;
+  const int grid = (int)std::min<size_t>((n8 + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(gelu_fwd_kernel, dim3(grid), dim3(256), 0, s, pre, out, n8);
+}
+
+int hq_rowblock_partials(int T) { return (T + kRowsBlock - 1) / kRowsBlock; }
+
+void hq_gelu_bwd(const uint16_t* dout, const uint16_t* pre, uint16_t* dpre, float* part, HqOuts outs, int T, int N,
+                 bool accumulate, hipStream_t s) {
+  const int nb = hq_rowblock_partials(T);
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3((N + 2047) / 2048, nb), dim3(256), 0, s, dout, pre, dpre, part, T, N);
+  if (outs.p[0]) colsum(part, nb, N, outs, N, accumulate, s);
+}
+
+void hq_bias_grad(const uint16_t* dy, float* part, HqOuts outs, int T, int N, bool accumulate, hipStream_t s) {
+  const int nb = hq_rowblock_partials(T);
+  hipLaunchKernelGGL(colpart_kernel, dim3((N + 2047) / 2048, nb), dim3(256), 0, s, dy, part, T, N);
+  colsum(part, nb, N, outs, N, accumulate, s);
+}

@@ -1,0 +1,194 @@
+// Fused optimizer kernels over the flat fp32 parameter / gradient arenas (gfx950).
+//
+// Replaces the reference's per-parameter optimizer + clip_grad_norm_ (≈8 elementwise kernels ×
+// 199 params + 199 norm kernels) with:
+//   hq_sq_norm_partials : one grid-stride pass over the whole grad arena (float4), per-block Σg²
+//   hq_clip_coef        : single block, deterministic sum → ‖g‖ and min(1, max_norm/(‖g‖+1e-6)) ON DEVICE
+//   hq_adamw / hq_adamod: one block per ≤8192-element chunk of a parameter segment; reads the
+//                         clip coefficient from device memory (no host sync), updates m, v (, n),
+//                         the fp32 master and writes the bf16 working copy in the same pass.
+// HF AdamW semantics (reference init.py:137, correct_bias=False): decay applied AFTER the update.
+// AdaMod semantics (reference modules/model/trainer/optim.py:76-98): decay BEFORE the update.
+#include "hq_common.h"
+#include "hq_kernels.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void sq_norm_kernel(const float* __restrict__ g, int64_t n, float* __restrict__ partials) {
+  __shared__ float red[4];
+  float s = 0.f;
+  const int64_t n4 = n / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(g)[i];
+    s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) s += g[i] * g[i];
+  s = hq_wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(256) void clip_coef_kernel(const float* __restrict__ partials, int nparts, float max_norm,
+                                                        float* __restrict__ norm_out, float* __restrict__ coef_out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += partials[i];
+  s = hq_wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(red[0] + red[1] + red[2] + red[3]);
+    norm_out[0] = norm;
+    if (coef_out) coef_out[0] = max_norm > 0.f ? fminf(1.f, max_norm / (norm + 1e-6f)) : 1.f;
+  }
+}
+
+struct AdamWArgs {
+  float beta1, beta2, eps, step_mult;
+};
+
+__device__ __forceinline__ void adamw_elem(float& p, float& m, float& v, float g, float lr, float wd, const AdamWArgs& a) {
+  m = a.beta1 * m + (1.f - a.beta1) * g;
+  v = a.beta2 * v + (1.f - a.beta2) * g * g;
+  const float denom = sqrtf(v) + a.eps;
+  p = p - (lr * a.step_mult) * (m / denom);
+  if (wd > 0.f) p = p - (lr * wd) * p;
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, uint16_t* __restrict__ compute,
+                                                    const float* __restrict__ grad, float* __restrict__ exp_avg,
+                                                    float* __restrict__ exp_avg_sq, const HqOptChunk* __restrict__ chunks,
+                                                    HqOptGroups groups, AdamWArgs a, const float* __restrict__ clip) {
+  const HqOptChunk c = chunks[blockIdx.x];
+  const float lr = groups.lr[c.group], wd = groups.wd[c.group];
+  const float cc = clip ? clip[0] : 1.f;
+  const int64_t s0 = c.start;
+  if ((s0 & 3) == 0) {
+    const int n4 = c.numel / 4;
+    for (int i = threadIdx.x; i < n4; i += 256) {
+      const int64_t o = s0 + 4 * (int64_t)i;
+      float4 p = *reinterpret_cast<float4*>(master + o);
+      float4 m = *reinterpret_cast<float4*>(exp_avg + o);
+      float4 v = *reinterpret_cast<float4*>(exp_avg_sq + o);
+      const float4 g = *reinterpret_cast<const float4*>(grad + o);
+      adamw_elem(p.x, m.x, v.x, g.x * cc, lr, wd, a);
+      adamw_elem(p.y, m.y, v.y, g.y * cc, lr, wd, a);
+      adamw_elem(p.z, m.z, v.z, g.z * cc, lr, wd, a);
+      adamw_elem(p.w, m.w, v.w, g.w * cc, lr, wd, a);
+      *reinterpret_cast<float4*>(master + o) = p;
+      *reinterpret_cast<float4*>(exp_avg + o) = m;
+      *reinterpret_cast<float4*>(exp_avg_sq + o) = v;
+      if (compute) {
+        const float pf[4] = {p.x, p.y, p.z, p.w};
+        *reinterpret_cast<uint2*>(compute + o) = hq_pack4(pf);
+      }
+    }
+    for (int i = n4 * 4 + threadIdx.x; i < c.numel; i += 256) {
+      const int64_t o = s0 + i;
+      adamw_elem(master[o], exp_avg[o], exp_avg_sq[o], grad[o] * cc, lr, wd, a);
+      if (compute) compute[o] = hq_f2bf(master[o]);
+    }
+  } else {
+    for (int i = threadIdx.x; i < c.numel; i += 256) {
+      const int64_t o = s0 + i;
+      adamw_elem(master[o], exp_avg[o], exp_avg_sq[o], grad[o] * cc, lr, wd, a);
+      if (compute) compute[o] = hq_f2bf(master[o]);
+    }
+  }
+}
+
+struct AdaModArgs {
+  float beta1, beta2, beta3, eps, base;  // base = bias-corrected step-size factor (times lr per group)
+};
+
+__global__ __launch_bounds__(256) void adamod_kernel(float* __restrict__ master, uint16_t* __restrict__ compute,
+                                                     const float* __restrict__ grad, float* __restrict__ exp_avg,
+                                                     float* __restrict__ exp_avg_sq, float* __restrict__ exp_avg_lr,
+                                                     const HqOptChunk* __restrict__ chunks, HqOptGroups groups, AdaModArgs a,
+                                                     const float* __restrict__ clip) {
+  const HqOptChunk c = chunks[blockIdx.x];
+  const float lr = groups.lr[c.group], wd = groups.wd[c.group];
+  const float cc = clip ? clip[0] : 1.f;
+  for (int i = threadIdx.x; i < c.numel; i += 256) {
+    const int64_t o = c.start + i;
+    const float g = grad[o] * cc;
+    float m = a.beta1 * exp_avg[o] + (1.f - a.beta1) * g;
+    float v = a.beta2 * exp_avg_sq[o] + (1.f - a.beta2) * g * g;
+    const float denom = sqrtf(v) + a.eps;
+    float p = master[o];
+    if (wd != 0.f) p = p - (wd * lr) * p;
+    float ss = (lr * a.base) / denom;
+    const float n = a.beta3 * exp_avg_lr[o] + (1.f - a.beta3) * ss;
+    ss = fminf(ss, n) * m;
+    p = p - ss;
+    exp_avg[o] = m;
+    exp_avg_sq[o] = v;
+    exp_avg_lr[o] = n;
+    master[o] = p;
+    if (compute) compute[o] = hq_f2bf(p);
+  }
+}
+
+__global__ __launch_bounds__(256) void cast_f32_bf16_kernel(const float* __restrict__ src, uint16_t* __restrict__ dst,
+                                                            int64_t n, float scale) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = n / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 v = reinterpret_cast<const float4*>(src)[i];
+    const float f[4] = {v.x * scale, v.y * scale, v.z * scale, v.w * scale};
+    reinterpret_cast<uint2*>(dst)[i] = hq_pack4(f);
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) dst[i] = hq_f2bf(src[i] * scale);
+}
+
+__global__ __launch_bounds__(256) void cast_bf16_f32_kernel(const uint16_t* __restrict__ src, float* __restrict__ dst,
+                                                            int64_t n, float scale) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = n / 4;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float f[4];
+    hq_unpack4(reinterpret_cast<const uint2*>(src)[i], f);
+    reinterpret_cast<float4*>(dst)[i] = make_float4(f[0] * scale, f[1] * scale, f[2] * scale, f[3] * scale);
+  }
+  if (blockIdx.x == 0)
+    for (int64_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) dst[i] = hq_bf2f(src[i]) * scale;
+}
+
+int grid_for(int64_t n4) { return (int)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 2048)); }
+
+}  // namespace
+
+void hq_sq_norm_partials(const float* g, int64_t n, float* partials, int nparts, hipStream_t s) {
+  hipLaunchKernelGGL(sq_norm_kernel, dim3(nparts), dim3(256), 0, s, g, n, partials);
+}
+
+void hq_clip_coef(const float* partials, int nparts, float max_norm, float* norm_out, float* coef_out, hipStream_t s) {
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(256), 0, s, partials, nparts, max_norm, norm_out, coef_out);
+}
+
+void hq_adamw(float* master, uint16_t* compute, const float* grad, float* m, float* v, const HqOptChunk* chunks, int nchunks,
+              HqOptGroups groups, float beta1, float beta2, float eps, float step_size_mult, const float* clip_coef,
+              hipStream_t s) {
+  AdamWArgs a{beta1, beta2, eps, step_size_mult};
+  hipLaunchKernelGGL(adamw_kernel, dim3(nchunks), dim3(256), 0, s, master, compute, grad, m, v, chunks, groups, a, clip_coef);
+}
+
+void hq_adamod(float* master, uint16_t* compute, const float* grad, float* m, float* v, float* n, const HqOptChunk* chunks,
+               int nchunks, HqOptGroups groups, float beta1, float beta2, float beta3, float eps, float bias_corr,
+               const float* clip_coef, hipStream_t s) {
+  AdaModArgs a{beta1, beta2, beta3, eps, bias_corr};
+  hipLaunchKernelGGL(adamod_kernel, dim3(nchunks), dim3(256), 0, s, master, compute, grad, m, v, n, chunks, groups, a,
+                     clip_coef);
+}
+
+void hq_cast_f32_bf16(const float* src, uint16_t* dst, int64_t n, float scale, hipStream_t s) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n / 4)), dim3(256), 0, s, src, dst, n, scale);
+}
+
+void hq_cast_bf16_f32(const uint16_t* src, float* dst, int64_t n, float scale, hipStream_t s) {
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n / 4)), dim3(256), 0, s, src, dst, n, scale);
+}

@@ -1,0 +1,413 @@
+"""BERT / RoBERTa encoder + QA heads, MI355X-first.
+
+Capability parity with the reference model (``modules/model/model/model.py:13-73``: HF
+``BertModel``/``RobertaModel`` + ``position_outputs`` Linear(H,2), ``classifier`` Dropout+Linear(H,5),
+``reg_start``/``reg_end`` Linear(H,1)+Sigmoid), re-designed around fused kernels:
+
+* The encoder is a chain of ``torch.autograd.Function``s — one for the embeddings, one per
+  encoder layer — each with an explicit backward.  Per layer forward = 4 hipBLASLt GEMMs +
+  3 fused HIP kernels (flash attention, residual+dropout+LayerNorm ×2, GELU); backward = 8 GEMMs
+  + 4 fused kernels.  Weight gradients are written straight into the fp32 grad arena and the
+  layer then signals the gradient reducer, which overlaps its RCCL all-reduce with the rest of
+  the backward (replaces DDP's per-parameter autograd hooks).
+* Dropout masks are regenerated from a counter hash (``ops.rng``) — nothing is stored.
+* Pooler + the four heads are tiny (B×H); they run as ordinary fp32 autograd on the master
+  parameters.
+* ``state_dict()`` keys are the HF names under ``transformer.`` plus the reference head names, so
+  reference checkpoints load and ours load into the reference (``embeddings.position_ids`` kept).
+"""
+from __future__ import annotations
+
+import math
+from typing import Callable, Dict, List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from .config import EncoderConfig
+from .params import Entry, ParamStore
+
+LABELS = ["yes", "no", "short", "long", "unknown"]
+
+
+# =========================================================================================== layout
+def build_entries(cfg: EncoderConfig) -> List[Entry]:
+    H, Fd, V, P, Tv = (cfg.hidden_size, cfg.intermediate_size, cfg.vocab_size, cfg.max_position_embeddings,
+                       cfg.type_vocab_size)
+    NL = cfg.num_labels
+
+    def lin(name, out_f, in_f, group, init="normal"):
+        return [Entry(name + ".weight", (out_f, in_f), group, init, [(name + ".weight", 0, out_f)]),
+                Entry(name + ".bias", (out_f,), group, "zeros" if init == "normal" else init,
+                      [(name + ".bias", 0, out_f)])]
+
+    def ln(name, group):
+        return [Entry(name + ".weight", (H,), group, "ones", [(name + ".weight", 0, H)]),
+                Entry(name + ".bias", (H,), group, "zeros", [(name + ".bias", 0, H)])]
+
+    out: List[Entry] = []
+    # QA heads (reference nn.Linear default init) + pooler: ready first in backward
+    out += lin("position_outputs", 2, H, "head", "linear_default")
+    out += lin("classifier.1", NL, H, "head", "linear_default")
+    out += lin("reg_start.0", 1, H, "head", "linear_default")
+    out += lin("reg_end.0", 1, H, "head", "linear_default")
+    out += lin("transformer.pooler.dense", H, H, "head")
+    for i in reversed(range(cfg.num_hidden_layers)):
+        p = f"transformer.encoder.layer.{i}."
+        g = f"layer.{i}"
+        a = p + "attention.self."
+        out.append(Entry(p + "qkv.weight", (3 * H, H), g, "normal",
+                         [(a + "query.weight", 0, H), (a + "key.weight", H, 2 * H), (a + "value.weight", 2 * H, 3 * H)]))
+        out.append(Entry(p + "qkv.bias", (3 * H,), g, "zeros",
+                         [(a + "query.bias", 0, H), (a + "key.bias", H, 2 * H), (a + "value.bias", 2 * H, 3 * H)]))
+        out += lin(p + "attention.output.dense", H, H, g)
+        out += ln(p + "attention.output.LayerNorm", g)
+        out += lin(p + "intermediate.dense", Fd, H, g)
+        out += lin(p + "output.dense", H, Fd, g)
+        out += ln(p + "output.LayerNorm", g)
+    e = "transformer.embeddings."
+    out += ln(e + "LayerNorm", "embeddings")
+    out.append(Entry(e + "token_type_embeddings.weight", (Tv, H), "embeddings", "normal",
+                     [(e + "token_type_embeddings.weight", 0, Tv)]))
+    out.append(Entry(e + "position_embeddings.weight", (P, H), "embeddings", "normal",
+                     [(e + "position_embeddings.weight", 0, P)]))
+    out.append(Entry(e + "word_embeddings.weight", (V, H), "embeddings", "normal",
+                     [(e + "word_embeddings.weight", 0, V)]))
+    return out
+
+
+def _init_store(store: ParamStore, cfg: EncoderConfig, generator: Optional[torch.Generator]):
+    store.allocate("cpu", cfg.initializer_range, generator)
+    for e in store.entries:
+        if e.init == "linear_default":
+            fan_in = e.shape[-1] if e.key.endswith(".weight") else store.by_key[e.key[:-4] + "weight"].shape[-1]
+            bound = 1.0 / math.sqrt(fan_in)
+            store.view(e.key, "master").uniform_(-bound, bound, generator=generator)
+    # HF zeroes the padding row of word embeddings at init
+    store.view("transformer.embeddings.word_embeddings.weight", "master")[cfg.pad_token_id].zero_()
+    store.mark_master_dirty()
+
+
+# ===================================================================================== autograd fns
+class _Ctx:
+    """Per-forward constants shared by the fused functions (not tensors)."""
+
+    def __init__(self, B, L, seed, training, model):
+        self.B, self.L, self.seed, self.training, self.model = B, L, seed, training, model
+
+
+class _EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, ids, pos_ids, type_ids, info: _Ctx):
+        m = info.model
+        cfg = m.config
+        st = m.store
+        e = "transformer.embeddings."
+        p = cfg.hidden_dropout_prob if info.training else 0.0
+        y, mean, rstd = ops.embed_fwd(ids, pos_ids, type_ids, st.view(e + "word_embeddings.weight"),
+                                      st.view(e + "position_embeddings.weight"),
+                                      st.view(e + "token_type_embeddings.weight"),
+                                      st.view(e + "LayerNorm.weight", "master"), st.view(e + "LayerNorm.bias", "master"),
+                                      cfg.layer_norm_eps, p, info.seed, 0, st.compute_dtype)
+        ctx.save_for_backward(ids, pos_ids, type_ids, mean, rstd)
+        ctx.info, ctx.p = info, p
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        ids, pos_ids, type_ids, mean, rstd = ctx.saved_tensors
+        info = ctx.info
+        m = info.model
+        st = m.store
+        e = "transformer.embeddings."
+        acc = m._take_accumulate("embeddings")
+        trainable = m.store.params[e + "word_embeddings.weight"].requires_grad
+        if trainable:
+            ops.embed_bwd(dy.contiguous(), ids, pos_ids, type_ids, st.view(e + "word_embeddings.weight"),
+                          st.view(e + "position_embeddings.weight"), st.view(e + "token_type_embeddings.weight"),
+                          st.view(e + "LayerNorm.weight", "master"), mean, rstd, ctx.p, info.seed, 0,
+                          st.view(e + "word_embeddings.weight", "grad"), st.view(e + "position_embeddings.weight", "grad"),
+                          st.view(e + "token_type_embeddings.weight", "grad"), st.view(e + "LayerNorm.weight", "grad"),
+                          st.view(e + "LayerNorm.bias", "grad"), acc, m.config.pad_token_id,
+                          m.config.pad_token_id if m.config.family == "roberta" else -1)
+            m._group_ready("embeddings")
+        return None, None, None, None, None
+
+
+class _LayerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, anchor, key_bias, idx: int, info: _Ctx):
+        m = info.model
+        cfg = m.config
+        st = m.store
+        B, L, nh = info.B, info.L, cfg.num_attention_heads
+        p = f"transformer.encoder.layer.{idx}."
+        ph = cfg.hidden_dropout_prob if info.training else 0.0
+        pa = cfg.attention_probs_dropout_prob if info.training else 0.0
+        scale = 1.0 / math.sqrt(cfg.head_dim)
+        op0 = 1 + 3 * idx
+        qkv = ops.linear_fwd(x, st.view(p + "qkv.weight"), st.view(p + "qkv.bias"))
+        ctxv, lse = ops.attn_fwd(qkv, key_bias, B, L, nh, pa, info.seed, op0, scale)
+        a1 = ops.linear_fwd(ctxv, st.view(p + "attention.output.dense.weight"), st.view(p + "attention.output.dense.bias"))
+        h1, z1, m1, r1 = ops.ln_fwd(a1, x, st.view(p + "attention.output.LayerNorm.weight", "master"),
+                                    st.view(p + "attention.output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph,
+                                    info.seed, op0 + 1)
+        pre = ops.linear_fwd(h1, st.view(p + "intermediate.dense.weight"), st.view(p + "intermediate.dense.bias"))
+        act = ops.gelu_fwd(pre)
+        a2 = ops.linear_fwd(act, st.view(p + "output.dense.weight"), st.view(p + "output.dense.bias"))
+        h2, z2, m2, r2 = ops.ln_fwd(a2, h1, st.view(p + "output.LayerNorm.weight", "master"),
+                                    st.view(p + "output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph,
+                                    info.seed, op0 + 2)
+        ctx.save_for_backward(x, key_bias, qkv, ctxv, lse, z1, m1, r1, h1, pre, act, z2, m2, r2)
+        ctx.info, ctx.idx, ctx.ph, ctx.pa, ctx.scale = info, idx, ph, pa, scale
+        return h2
+
+    @staticmethod
+    def backward(ctx, dh2):
+        x, key_bias, qkv, ctxv, lse, z1, m1, r1, h1, pre, act, z2, m2, r2 = ctx.saved_tensors
+        info = ctx.info
+        m = info.model
+        cfg = m.config
+        st = m.store
+        idx = ctx.idx
+        B, L, nh = info.B, info.L, cfg.num_attention_heads
+        p = f"transformer.encoder.layer.{idx}."
+        op0 = 1 + 3 * idx
+        grp = f"layer.{idx}"
+        trainable = st.params[p + "attention.self.query.weight"].requires_grad
+        acc = m._take_accumulate(grp) if trainable else False
+        G = (lambda k: st.view(p + k, "grad")) if trainable else (lambda k: None)
+        W = lambda k: st.view(p + k)  # noqa: E731
+        Wm = lambda k: st.view(p + k, "master")  # noqa: E731
+        dh2 = dh2.contiguous()
+
+        # --- FFN block ------------------------------------------------------------------------
+        dz2, da2 = ops.ln_bwd(dh2, None, z2, Wm("output.LayerNorm.weight"), m2, r2, ctx.ph, info.seed, op0 + 2,
+                              G("output.LayerNorm.weight"), G("output.LayerNorm.bias"), G("output.dense.bias"), acc)
+        if trainable:
+            ops.linear_wgrad(da2, act, G("output.dense.weight"), None, acc)
+        dact = ops.linear_dgrad(da2, W("output.dense.weight"))
+        dpre = ops.gelu_bwd(dact, pre, G("intermediate.dense.bias"), acc)
+        if trainable:
+            ops.linear_wgrad(dpre, h1, G("intermediate.dense.weight"), None, acc)
+        dh1_ffn = ops.linear_dgrad(dpre, W("intermediate.dense.weight"))
+        # --- attention block ------------------------------------------------------------------
+        dz1, da1 = ops.ln_bwd(dz2, dh1_ffn, z1, Wm("attention.output.LayerNorm.weight"), m1, r1, ctx.ph, info.seed,
+                              op0 + 1, G("attention.output.LayerNorm.weight"), G("attention.output.LayerNorm.bias"),
+                              G("attention.output.dense.bias"), acc)
+        if trainable:
+            ops.linear_wgrad(da1, ctxv, G("attention.output.dense.weight"), None, acc)
+        dctx = ops.linear_dgrad(da1, W("attention.output.dense.weight"))
+        dqkv = ops.attn_bwd(dctx, qkv, ctxv, lse, key_bias, B, L, nh, ctx.pa, info.seed, op0, ctx.scale)
+        if trainable:
+            ops.linear_wgrad(dqkv, x, G("qkv.weight"), G("qkv.bias"), acc)
+            m._group_ready(grp)
+        dx = ops.linear_dgrad_add(dqkv, W("qkv.weight"), dz1)
+        return dx, None, None, None, None
+
+
+# ============================================================================================ model
+def _ensure_module(root: nn.Module, path: List[str]) -> nn.Module:
+    mod = root
+    for part in path:
+        if not hasattr(mod, part) or not isinstance(getattr(mod, part), nn.Module):
+            mod.add_module(part, nn.Module())
+        mod = getattr(mod, part)
+    return mod
+
+
+class BertForQuestionAnswering(nn.Module):
+    """Encoder + 5 QA outputs; ``forward(input_ids, attention_mask, token_type_ids, position_ids,
+    head_mask) -> {start_class, end_class, start_reg, end_reg, cls}`` (reference ``model.py:43-73``)."""
+
+    def __init__(self, config: EncoderConfig, *, device=None, precision: str = "bf16", seed: Optional[int] = None):
+        super().__init__()
+        self.config = config
+        self.precision = precision
+        gen = torch.Generator().manual_seed(seed) if seed is not None else None
+        self.store = ParamStore(build_entries(config))
+        _init_store(self.store, config, gen)
+        for name, prm in self.store.params.items():
+            *path, leaf = name.split(".")
+            _ensure_module(self, path).register_parameter(leaf, prm)
+        emb = _ensure_module(self, ["transformer", "embeddings"])
+        emb.register_buffer("position_ids", torch.arange(config.max_position_embeddings).unsqueeze(0))
+        self._head_params = [prm for n, prm in self.store.params.items() if not n.startswith("transformer.encoder")
+                             and not n.startswith("transformer.embeddings")]
+        self._fresh: Dict[str, bool] = {}
+        self._grad_listener: Optional[Callable[[str], None]] = None
+        self._head_pending = 0
+        for prm in self._head_params:
+            prm.register_post_accumulate_grad_hook(self._head_hook)
+        self.zero_grad()
+        if device is not None:
+            self.to(device)
+
+    # -------------------------------------------------------------------- device / precision
+    def __deepcopy__(self, memo):
+        """Parameters are arena views, which ``copy.deepcopy`` would un-share: rebuild instead."""
+        import copy as _copy
+        new = type(self)(_copy.deepcopy(self.config), precision=self.precision)
+        new.store.master.copy_(self.store.master.detach().cpu())
+        new.store.mark_master_dirty()
+        new.train(self.training)
+        for n, p in self.named_parameters():
+            dict(new.named_parameters())[n].requires_grad_(p.requires_grad)
+        if self.store.device.type != "cpu":
+            new.to(self.store.device)
+        new.store.sync_compute()
+        return new
+
+    def _apply(self, fn, recurse=True):
+        probe = fn(torch.empty(0, dtype=torch.float32, device=self.store.device))
+        if probe.dtype != torch.float32:
+            raise RuntimeError("Cast the compute precision with --precision; master weights stay fp32.")
+        self.store.to(probe.device)
+        self.store.set_compute_dtype(self.compute_dtype_for(probe.device))
+        for mod in self.modules():
+            for k, b in list(mod._buffers.items()):
+                if b is not None:
+                    mod._buffers[k] = fn(b)
+        return self
+
+    def compute_dtype_for(self, device) -> torch.dtype:
+        if torch.device(device).type != "cuda":
+            return torch.float32
+        return {"bf16": torch.bfloat16, "fp32": torch.float32, "fp8": torch.bfloat16}[self.precision]
+
+    def set_precision(self, precision: str):
+        self.precision = precision
+        self.store.set_compute_dtype(self.compute_dtype_for(self.store.device))
+
+    @property
+    def device(self):
+        return self.store.device
+
+    # -------------------------------------------------------------------- grads / reducer hooks
+    def zero_grad(self, set_to_none: bool = False):
+        """Mark every gradient group "fresh": the next backward overwrites instead of accumulating
+        (no memset of the encoder arena).  Autograd-managed head grads are zeroed for real."""
+        for g, s, e in self.store.group_ranges():
+            self._fresh[g] = True
+        for prm in self._head_params:
+            prm.grad.zero_()
+        self._head_pending = len([p for p in self._head_params if p.requires_grad])
+
+    def _take_accumulate(self, group: str) -> bool:
+        fresh = self._fresh.get(group, True)
+        self._fresh[group] = False
+        return not fresh
+
+    def _group_ready(self, group: str):
+        if self._grad_listener is not None:
+            self._grad_listener(group)
+
+    def _head_hook(self, _p):
+        self._head_pending -= 1
+        if self._head_pending == 0:
+            self._fresh["head"] = False
+            self._group_ready("head")
+            self._head_pending = len([p for p in self._head_params if p.requires_grad])
+
+    def set_grad_listener(self, fn: Optional[Callable[[str], None]]):
+        self._grad_listener = fn
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        state_dict = dict(state_dict)
+        pid = "transformer.embeddings.position_ids"
+        if pid not in state_dict:
+            state_dict[pid] = self.transformer.embeddings.position_ids.clone()
+        res = super().load_state_dict(state_dict, strict=strict)
+        self.store.mark_master_dirty()
+        self.store.sync_compute()
+        return res
+
+    # -------------------------------------------------------------------- forward
+    def _position_ids(self, input_ids, position_ids):
+        B, L = input_ids.shape
+        if position_ids is not None:
+            return position_ids.expand(B, L)
+        if self.config.family == "roberta":
+            mask = input_ids.ne(self.config.pad_token_id).to(torch.int64)
+            return torch.cumsum(mask, dim=1) * mask + self.config.pad_token_id
+        return self.transformer.embeddings.position_ids[:, :L].expand(B, L)
+
+    def encode(self, input_ids, attention_mask=None, token_type_ids=None, position_ids=None):
+        cfg = self.config
+        B, L = input_ids.shape
+        if L > cfg.max_position_embeddings - cfg.position_offset:
+            raise ValueError(f"sequence length {L} exceeds max positions {cfg.max_position_embeddings}")
+        self.store.sync_compute()
+        dev = self.store.device
+        ids = input_ids.reshape(-1).to(dev, torch.int64)
+        tt = (token_type_ids if token_type_ids is not None else torch.zeros_like(input_ids)).reshape(-1).to(dev, torch.int64)
+        pos = self._position_ids(input_ids, position_ids).reshape(-1).to(dev, torch.int64)
+        if attention_mask is None:
+            key_bias = torch.zeros(B, L, dtype=torch.float32, device=dev)
+        else:
+            key_bias = (1.0 - attention_mask.to(dev, torch.float32)) * -10000.0
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if self.training else 0
+        info = _Ctx(B, L, seed, self.training, self)
+        anchor_e = self.store.params["transformer.embeddings.word_embeddings.weight"]
+        h = _EmbeddingFn.apply(anchor_e, ids, pos, tt, info)
+        for i in range(cfg.num_hidden_layers):
+            anchor = self.store.params[f"transformer.encoder.layer.{i}.attention.self.query.weight"]
+            h = _LayerFn.apply(h, anchor, key_bias, i, info)
+        return h.view(B, L, cfg.hidden_size)
+
+    def forward(self, input_ids, attention_mask=None, token_type_ids=None, position_ids=None, head_mask=None):
+        if head_mask is not None:
+            raise NotImplementedError("head_mask is not supported by the fused encoder")
+        seq = self.encode(input_ids, attention_mask, token_type_ids, position_ids)
+        P = self.store.params
+        seq32 = seq.float()
+        pooled = torch.tanh(F.linear(seq32[:, 0], P["transformer.pooler.dense.weight"], P["transformer.pooler.dense.bias"]))
+        pos_logits = F.linear(seq32, P["position_outputs.weight"], P["position_outputs.bias"])
+        start_logits, end_logits = pos_logits.split(1, dim=-1)
+        cls_in = F.dropout(pooled, self.config.hidden_dropout_prob, self.training)
+        cls = F.linear(cls_in, P["classifier.1.weight"], P["classifier.1.bias"])
+        reg_start = torch.sigmoid(F.linear(pooled, P["reg_start.0.weight"], P["reg_start.0.bias"])).squeeze(-1)
+        reg_end = torch.sigmoid(F.linear(pooled, P["reg_end.0.weight"], P["reg_end.0.bias"])).squeeze(-1)
+        return {"start_class": start_logits.squeeze(-1), "end_class": end_logits.squeeze(-1),
+                "start_reg": reg_start, "end_reg": reg_end, "cls": cls}
+
+
+def load_pretrained(model: BertForQuestionAnswering, path: str) -> List[str]:
+    """Load HF-named encoder weights from a local file/dir (safetensors or weights-only torch pickle).
+    Keys may be bare (``embeddings.…``), ``bert.``/``roberta.``-prefixed or already ``transformer.``-prefixed."""
+    import os
+    files = []
+    if os.path.isdir(path):
+        for fn in ("model.safetensors", "pytorch_model.bin"):
+            if os.path.exists(os.path.join(path, fn)):
+                files.append(os.path.join(path, fn))
+                break
+    else:
+        files.append(path)
+    if not files:
+        raise FileNotFoundError(f"no weights in {path}")
+    f = files[0]
+    if f.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        sd = load_file(f)
+    else:
+        sd = torch.load(f, map_location="cpu", weights_only=True)
+        if isinstance(sd, dict) and "model" in sd and isinstance(sd["model"], dict):
+            sd = sd["model"]
+    own = model.state_dict()
+    mapped = {}
+    for k, v in sd.items():
+        k2 = k
+        for pre in ("bert.", "roberta."):
+            if k2.startswith(pre):
+                k2 = k2[len(pre):]
+        k2 = k2.replace("LayerNorm.gamma", "LayerNorm.weight").replace("LayerNorm.beta", "LayerNorm.bias")
+        if not k2.startswith("transformer.") and ("transformer." + k2) in own:
+            k2 = "transformer." + k2
+        if k2 in own and own[k2].shape == v.shape:
+            mapped[k2] = v
+    missing = [k for k in own if k not in mapped]
+    model.load_state_dict({**own, **mapped}, strict=True)
+    return missing

@@ -1,0 +1,171 @@
+"""Flat parameter / gradient arenas.
+
+All trainable tensors live in three contiguous device buffers:
+
+* ``master``  fp32 — the ``nn.Parameter`` objects are *views* into it (HF names, so
+  ``state_dict()`` matches ``transformers.BertModel`` + the reference QA heads);
+* ``compute`` bf16 — working copy read by the GEMMs / fused kernels, rewritten by the fused
+  optimizer kernel every step (on CPU / fp32 it *is* ``master``);
+* ``grad``    fp32 — ``param.grad`` are views; the fused layer backward kernels write weight
+  gradients straight into it, so the gradient reducer all-reduces contiguous arena slices
+  with no bucket copies (replaces the torch DDP Reducer's copy-in/copy-out).
+
+Arena order = backward-readiness order (QA heads, pooler, layer N-1 … layer 0, embeddings), so
+every all-reduce bucket is one contiguous range and buckets complete front to back.
+Fused tensors (QKV = query‖key‖value rows) are single arena entries whose HF-named pieces are
+row slices; every entry starts 256-byte aligned for 16-B vector access in the kernels.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+_ALIGN = 64  # elements (256 B of fp32, 128 B of bf16)
+
+
+@dataclass
+class Entry:
+    key: str
+    shape: Tuple[int, ...]
+    group: str
+    init: str = "normal"                      # normal | zeros | ones
+    views: List[Tuple[str, int, int]] = field(default_factory=list)   # (hf_name, row0, row1)
+    offset: int = 0
+
+    @property
+    def numel(self) -> int:
+        n = 1
+        for s in self.shape:
+            n *= s
+        return n
+
+
+def no_decay(name: str) -> bool:
+    """Reference ``init.py:125-129``: no weight decay for bias / LayerNorm params."""
+    return any(nd in name for nd in ("bias", "LayerNorm.bias", "LayerNorm.weight"))
+
+
+class ParamStore:
+    def __init__(self, entries: Sequence[Entry]):
+        self.entries: List[Entry] = list(entries)
+        off = 0
+        for e in self.entries:
+            off = (off + _ALIGN - 1) // _ALIGN * _ALIGN
+            e.offset = off
+            off += e.numel
+        self.total = (off + _ALIGN - 1) // _ALIGN * _ALIGN
+        self.by_key: Dict[str, Entry] = {e.key: e for e in self.entries}
+        self.master: Optional[torch.Tensor] = None
+        self.grad: Optional[torch.Tensor] = None
+        self.compute: Optional[torch.Tensor] = None
+        self.compute_dtype = torch.float32
+        self.params: Dict[str, nn.Parameter] = {}
+        self._dirty = True
+
+    # ------------------------------------------------------------------ allocation
+    def allocate(self, device, init_std: float, generator: Optional[torch.Generator] = None):
+        self.master = torch.zeros(self.total, dtype=torch.float32, device="cpu")
+        for e in self.entries:
+            v = self.master[e.offset:e.offset + e.numel].view(e.shape)
+            if e.init == "normal":
+                v.normal_(0.0, init_std, generator=generator)
+            elif e.init == "ones":
+                v.fill_(1.0)
+        self.master = self.master.to(device)
+        self.grad = torch.zeros(self.total, dtype=torch.float32, device=device)
+        self._make_params()
+        self.set_compute_dtype(self.compute_dtype)
+
+    def _make_params(self):
+        fresh = not self.params
+        for e in self.entries:
+            rows = e.shape[0]
+            row_numel = e.numel // rows
+            for hf_name, r0, r1 in e.views:
+                shape = (r1 - r0,) + tuple(e.shape[1:])
+                a = e.offset + r0 * row_numel
+                b = e.offset + r1 * row_numel
+                mv = self.master[a:b].view(shape)
+                gv = self.grad[a:b].view(shape)
+                if fresh:
+                    p = nn.Parameter(mv, requires_grad=True)
+                    self.params[hf_name] = p
+                else:
+                    p = self.params[hf_name]
+                    p.data = mv
+                p.grad = gv
+
+    def set_compute_dtype(self, dtype: torch.dtype):
+        self.compute_dtype = dtype
+        if self.master is None:
+            return
+        if dtype == torch.float32:
+            self.compute = self.master
+        else:
+            self.compute = torch.empty(self.total, dtype=dtype, device=self.master.device)
+            self.compute.copy_(self.master)
+        self._dirty = False
+
+    def to(self, device):
+        device = torch.device(device)
+        if self.master is None or self.master.device == device:
+            return self
+        self.master = self.master.to(device)
+        self.grad = self.grad.to(device)
+        self._make_params()
+        self.set_compute_dtype(self.compute_dtype if device.type == "cuda" else torch.float32)
+        return self
+
+    @property
+    def device(self):
+        return self.master.device
+
+    # ------------------------------------------------------------------ views
+    def view(self, key: str, which: str = "compute") -> torch.Tensor:
+        e = self.by_key[key]
+        buf = {"compute": self.compute, "master": self.master, "grad": self.grad}[which]
+        return buf[e.offset:e.offset + e.numel].view(e.shape)
+
+    def mark_master_dirty(self):
+        self._dirty = True
+
+    def sync_compute(self):
+        """Refresh the bf16 working copy after host-side edits of master (load, init)."""
+        if self._dirty and self.compute is not None and self.compute.data_ptr() != self.master.data_ptr():
+            self.compute.copy_(self.master)
+        self._dirty = False
+
+    def mark_clean(self):
+        self._dirty = False
+
+    # ------------------------------------------------------------------ layout queries
+    def segments(self, names: Optional[Iterable[str]] = None) -> List[Tuple[int, int, str]]:
+        """(start, numel, hf_name) for every HF parameter (optionally restricted to ``names``)."""
+        wanted = None if names is None else set(names)
+        out = []
+        for e in self.entries:
+            row_numel = e.numel // e.shape[0]
+            for hf_name, r0, r1 in e.views:
+                if wanted is not None and hf_name not in wanted:
+                    continue
+                out.append((e.offset + r0 * row_numel, (r1 - r0) * row_numel, hf_name))
+        return out
+
+    def group_ranges(self) -> List[Tuple[str, int, int]]:
+        """Contiguous (group, start, end) ranges in arena order."""
+        out: List[Tuple[str, int, int]] = []
+        for e in self.entries:
+            end = e.offset + e.numel
+            if out and out[-1][0] == e.group:
+                out[-1] = (e.group, out[-1][1], end)
+            else:
+                out.append((e.group, e.offset, end))
+        # extend each range to the next range's start (covers alignment padding, keeps buckets contiguous)
+        fixed = []
+        for i, (g, s, _) in enumerate(out):
+            e_ = out[i + 1][1] if i + 1 < len(out) else self.total
+            fixed.append((g, s, e_))
+        return fixed

@@ -1,0 +1,157 @@
+"""HIP kernel numerics vs the fp32 PyTorch reference of the same op (ops/reference.py).
+
+Inputs are bf16 (what the kernels consume); the oracle runs the same math in fp32 on the CPU on
+those exact bf16 values, including the identical dropout masks (shared counter hash)."""
+import math
+
+import pytest
+import torch
+
+from ml_recipe_distributed_pytorch_amd import _native
+from ml_recipe_distributed_pytorch_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, atol, rtol, what):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).sum().item()
+    assert bad == 0, f"{what}: {bad} / {a.numel()} outside tol, max err {err.max().item():.3e}"
+
+
+def _bf(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("H", [128, 768, 1024])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_ln_fwd_bwd(cuda, H, p):
+    k = _native.kernels()
+    torch.manual_seed(0)
+    T = 1000
+    a, r = _bf(torch.randn(T, H)), _bf(torch.randn(T, H))
+    gamma, beta = torch.randn(H) * 0.5 + 1, torch.randn(H) * 0.1
+    y, z, m, rs = k.ln_fwd(a.to(cuda), r.to(cuda), gamma.to(cuda), beta.to(cuda), 1e-12, p, 1234, 7)
+    yr, zr, mr, rr = ref.ln_fwd(a, r, gamma, beta, 1e-12, p, 1234, 7)
+    _close(z, zr, 1e-2, 1e-2, "z")
+    _close(y, yr, 3e-2, 2e-2, "y")
+    _close(m, mr, 1e-3, 1e-3, "mean")
+    _close(rs, rr, 1e-3, 2e-3, "rstd")
+    dy, dy2 = _bf(torch.randn(T, H)), _bf(torch.randn(T, H))
+    for acc in (False, True):
+        gg = [torch.randn(H).to(cuda) for _ in range(3)]
+        ggr = [g.cpu().clone() for g in gg]
+        dz, da = k.ln_bwd(dy.to(cuda), dy2.to(cuda), z, gamma.to(cuda), m, rs, p, 1234, 7, gg[0], gg[1], gg[2], acc)
+        dzr, dar = ref.ln_bwd(dy, dy2, z.cpu(), gamma, m.cpu(), rs.cpu(), p, 1234, 7, ggr[0], ggr[1], ggr[2], acc)
+        _close(dz, dzr, 3e-2, 2e-2, "dz")
+        _close(da, dar, 3e-2, 2e-2, "da")
+        for i, n in enumerate(["dgamma", "dbeta", "dbias"]):
+            _close(gg[i], ggr[i], 5e-2, 1e-3, n)
+
+
+@pytest.mark.parametrize("H,ntypes", [(768, 2), (128, 1)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_embedding(cuda, H, ntypes, p):
+    k = _native.kernels()
+    torch.manual_seed(1)
+    V, P, B, L = 1000, 64, 4, 50
+    T = B * L
+    ww, wp, wt = _bf(torch.randn(V, H) * 0.05), _bf(torch.randn(P, H) * 0.05), _bf(torch.randn(ntypes, H) * 0.05)
+    gamma, beta = torch.randn(H) * 0.3 + 1, torch.randn(H) * 0.1
+    ids = torch.randint(0, V, (T,))
+    ids[::7] = 0
+    pids = torch.arange(L).repeat(B)
+    tids = torch.randint(0, ntypes, (T,))
+    dev = lambda t: t.to(cuda)  # noqa: E731
+    y, m, rs = k.embed_fwd(dev(ids), dev(pids), dev(tids), dev(ww), dev(wp), dev(wt), dev(gamma), dev(beta), 1e-12, p, 99, 0)
+    yr, mr, rr = ref.embed_fwd(ids, pids, tids, ww, wp, wt, gamma, beta, 1e-12, p, 99, 0, torch.float32)
+    _close(y, yr, 3e-2, 2e-2, "y")
+    _close(m, mr, 1e-4, 1e-3, "mean")
+    dy = _bf(torch.randn(T, H))
+    gw, gp, gt = torch.zeros(V, H), torch.zeros(P, H), torch.zeros(ntypes, H)
+    gg, gb = torch.zeros(H), torch.zeros(H)
+    out = [dev(t) for t in (gw, gp, gt, gg, gb)]
+    k.embed_bwd(dev(dy), dev(ids), dev(pids), dev(tids), dev(ww), dev(wp), dev(wt), dev(gamma), m, rs, p, 99, 0, *out,
+                False, 0, -1)
+    ref.embed_bwd(dy, ids, pids, tids, ww, wp, wt, gamma, m.cpu(), rs.cpu(), p, 99, 0, gw, gp, gt, gg, gb, False, 0, -1)
+    for a, b, n in zip(out, (gw, gp, gt, gg, gb), ["word", "pos", "type", "gamma", "beta"]):
+        _close(a, b, 5e-2, 2e-2, n)
+    assert out[0][0].abs().max().item() == 0.0, "padding row must get no gradient"
+
+
+def test_gelu_and_bias_grad(cuda):
+    k = _native.kernels()
+    torch.manual_seed(2)
+    T, N = 300, 3072
+    pre = _bf(torch.randn(T, N) * 2)
+    out = k.gelu_fwd(pre.to(cuda))
+    _close(out, ref.gelu_fwd(pre.float()), 2e-2, 1e-2, "gelu")
+    dout = _bf(torch.randn(T, N))
+    gb = torch.randn(N)
+    gbd = gb.to(cuda)
+    d = k.gelu_bwd(dout.to(cuda), pre.to(cuda), gbd, True)
+    dr = ref.gelu_bwd(dout, pre, gb, True)
+    _close(d, dr, 2e-2, 2e-2, "dgelu")
+    _close(gbd, gb, 5e-2, 1e-3, "gelu bias grad")
+    g2 = torch.zeros(N, device=cuda)
+    k.bias_grad(d, g2, False)
+    _close(g2, d.float().sum(0), 1e-2, 1e-4, "bias_grad")
+
+
+def _attn_case(cuda, B, L, nh, p, masked):
+    k = _native.kernels()
+    torch.manual_seed(3)
+    H = nh * 64
+    qkv = _bf(torch.randn(B * L, 3 * H))
+    kb = torch.zeros(B, L)
+    if masked:
+        for b in range(B):
+            kb[b, L - 1 - 7 * b:] = -10000.0
+    scale = 1.0 / 8.0
+    ctx, lse = k.attn_fwd(qkv.to(cuda), kb.to(cuda), B, L, nh, p, 555, 3, scale)
+    ctxr, lser = ref.attn_fwd(qkv, kb, B, L, nh, p, 555, 3, scale)
+    _close(lse, lser, 1e-2, 1e-3, "lse")
+    _close(ctx, ctxr, 2e-2, 2e-2, "ctx")
+    dctx = _bf(torch.randn(B * L, H))
+    dq = k.attn_bwd(dctx.to(cuda), qkv.to(cuda), ctx, lse, kb.to(cuda), B, L, nh, p, 555, 3, scale)
+    dqr = ref.attn_bwd(dctx, qkv, ctx.cpu(), lse.cpu(), kb, B, L, nh, p, 555, 3, scale)
+    _close(dq, dqr, 3e-2, 3e-2, "dqkv")
+
+
+@pytest.mark.parametrize("L", [384, 128, 100, 24])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attention(cuda, L, p):
+    _attn_case(cuda, 2, L, 2, p, masked=True)
+
+
+def test_attention_bert_base_shape(cuda):
+    _attn_case(cuda, 2, 384, 12, 0.1, masked=False)
+
+
+def test_adamw_and_norm(cuda):
+    k = _native.kernels()
+    torch.manual_seed(4)
+    n = 20011
+    master = torch.randn(n)
+    grad = torch.randn(n)
+    m, v = torch.randn(n) * 0.01, torch.rand(n) * 0.01
+    segs = [(0, 5003, 0.01), (5003, 15000, 0.0), (20003, 8, 0.01)]
+    chunks = []
+    for gi, (s, c, wd) in enumerate(segs):
+        for off in range(0, c, 8192):
+            chunks.append([s + off, min(8192, c - off) | ((0 if wd > 0 else 1) << 32)])
+    ch = torch.tensor(chunks, dtype=torch.int64)
+    md, gd, mmd, vvd = master.to(cuda), grad.to(cuda), m.to(cuda), v.to(cuda)
+    comp = torch.empty(n, dtype=torch.bfloat16, device=cuda)
+    norm, coef = k.grad_norm(gd, 1.0)
+    assert abs(norm.item() - grad.norm().item()) / grad.norm().item() < 1e-5
+    assert abs(coef.item() - 1.0 / (grad.norm().item() + 1e-6)) < 1e-6
+    k.adamw(md, comp, gd, mmd, vvd, ch.to(cuda), [1e-3, 1e-3], [0.01, 0.0], 0.9, 0.999, 1e-6, 1.0, coef)
+    ref.adamw_step(master, None, grad, m, v, [(s, c, wd) for s, c, wd in segs], lr=1e-3, beta1=0.9, beta2=0.999,
+                   eps=1e-6, clip_coef=coef.cpu(), correct_bias=False, step=1)
+    _close(md, master, 1e-6, 1e-5, "master")
+    _close(mmd, m, 1e-7, 1e-5, "exp_avg")
+    _close(comp, master, 1e-2, 1e-2, "bf16 copy")
