@@ -1,0 +1,154 @@
+#!/usr/bin/env python
+"""Headline benchmark: whole-node training samples/s, BERT-base QA fine-tuning at seq=384, bf16.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched by
+``torch.distributed.run`` (one rank per GPU, RCCL over xGMI).  Each timed step is a complete
+optimizer step of the recipe's training loop (``config/test_bert.cfg`` loss/optimizer settings):
+host batch synthesis (native dummy-QA generator, pinned) → H2D → fused BERT-base forward →
+5-way QA loss → backward with bucketed RCCL all-reduce overlapped → on-device grad-norm clip →
+fused AdamW → LR schedule.  Weak scaling: ``--batch`` samples per GPU per step.
+Rank 0 prints ONE JSON line; ``value`` is the whole-job aggregate (max elapsed over ranks).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from types import SimpleNamespace
+
+METRIC = "samples/sec (whole node) BERT-base QA fine-tune seq=384 at 1/2/4/8 MI355X"
+BASELINE_VALUE = None  # the reference publishes no throughput numbers
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="samples per GPU per optimizer step")
+    ap.add_argument("--seq", type=int, default=384)
+    ap.add_argument("--model", default="bert-base-uncased")
+    ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--bucket_cap_mb", type=float, default=32.0)
+    ap.add_argument("--profile", action="store_true", help="per-phase timers (adds syncs; not for the headline)")
+    ap.add_argument("--json_out", default=None)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from ml_recipe_distributed_pytorch_amd.data.dummy import SpecialIds, synth_batch_native
+    from ml_recipe_distributed_pytorch_amd.models.bert import BertForQuestionAnswering
+    from ml_recipe_distributed_pytorch_amd.models.config import get_config
+    from ml_recipe_distributed_pytorch_amd.models.losses import build_loss
+    from ml_recipe_distributed_pytorch_amd.parallel import dist as hqdist
+    from ml_recipe_distributed_pytorch_amd.parallel.reducer import GradReducer
+    from ml_recipe_distributed_pytorch_amd.train.engine import TrainEngine
+    from ml_recipe_distributed_pytorch_amd.train.optim import FusedAdamW, get_linear_schedule_with_warmup
+    from ml_recipe_distributed_pytorch_amd.train.trainer import optimizer_groups
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        info = hqdist.init_distributed("nccl")
+        rank, device = info.rank, info.device
+    else:
+        rank, device = 0, torch.device("cuda", 0)
+        torch.cuda.set_device(device)
+    if world != args.gpus and rank == 0:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+
+    cfg = get_config(args.model)
+    model = BertForQuestionAnswering(cfg, seed=1234).to(device).train()
+    # config/test_bert.cfg: loss=smooth(0.01), all five loss weights 1, lr 1e-5, wd 1e-4, clip 1
+    lp = SimpleNamespace(loss="smooth", smooth_alpha=0.01, focal_alpha=1, focal_gamma=2, w_start=1, w_end=1,
+                         w_start_reg=1, w_end_reg=1, w_cls=1)
+    loss_fn = build_loss(lp)
+    groups = optimizer_groups(model.named_parameters(), 1e-4)
+    opt = FusedAdamW(groups, model.store, lr=1e-5, eps=1e-6, correct_bias=False, zero_grad_fn=model.zero_grad)
+    total = args.warmup + args.steps
+    sched = get_linear_schedule_with_warmup(opt, int(0.05 * total), total)
+    reducer = GradReducer(model, bucket_cap_mb=args.bucket_cap_mb, allreduce_dtype=args.allreduce_dtype) if world > 1 else None
+    engine = TrainEngine(model, loss_fn, opt, scheduler=sched, reducer=reducer, max_grad_norm=1.0, profile=args.profile)
+
+    sp = SpecialIds(cfg.vocab_size, cfg.pad_token_id, cfg.unk_token_id, cfg.cls_token_id, cfg.sep_token_id,
+                    "bert" if cfg.family == "bert" else "roberta")
+    B, L, Q = args.batch, args.seq, 64
+    slots = [synth_batch_native(B, L, Q, sp, seed=rank * 1_000_003 + i) for i in range(2)]
+    events = [torch.cuda.Event() for _ in slots]
+    for e in events:
+        e.record()
+    step_no = [0]
+
+    def next_batch():
+        i = step_no[0]
+        s = i % 2
+        events[s].synchronize()              # previous H2D out of this pinned slot has finished
+        inputs, labels = slots[s]
+        from ml_recipe_distributed_pytorch_amd.data.dummy import _refill
+        _refill(slots[s], sp, Q, seed=rank * 1_000_003 + 7919 * (i + 2))
+        dev_in = {k: v.to(device, non_blocking=True) for k, v in inputs.items()}
+        dev_lb = {k: v.to(device, non_blocking=True) for k, v in labels.items()}
+        events[s].record()
+        step_no[0] += 1
+        return dev_in, dev_lb
+
+    def one_step():
+        inputs, labels = next_batch()
+        return engine.step([(inputs, labels)])
+
+    for _ in range(args.warmup):
+        res = one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        hqdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    phase = {}
+    for _ in range(args.steps):
+        res = one_step()
+        for k, v in res.timings.items():
+            phase[k] = phase.get(k, 0.0) + v
+    torch.cuda.synchronize()
+    if world > 1:
+        hqdist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = res.losses.to_floats().get("loss", float("nan"))
+    ms = elapsed / args.steps * 1e3
+    value = world * B * args.steps / elapsed
+    flops_per_sample = 6 * 85.0e6 * L + 12 * L * L * cfg.hidden_size * cfg.num_hidden_layers  # SURVEY §6.2 model
+    out = {"metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None), "dtype": "bf16",
+           "data": "synthetic (dummy-QA generator, random-init weights)",
+           "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": L,
+                      "parallelism": f"dp{world}", "allreduce_dtype": args.allreduce_dtype,
+                      "bucket_cap_mb": args.bucket_cap_mb},
+           "mfu_bf16_dense": round(value * flops_per_sample / (world * 2.5e15), 4),
+           "final_loss": round(final_loss, 4)}
+    if args.profile:
+        out["phase_ms"] = {k: round(v / args.steps, 3) for k, v in phase.items()}
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    if reducer is not None:
+        reducer.close()
+    if world > 1:
+        hqdist.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -78,6 +78,23 @@ def build_entries(cfg: EncoderConfig) -> List[Entry]:
     return out
 
 
+def hf_param_order(cfg: EncoderConfig) -> List[str]:
+    """``named_parameters()`` order of HF ``BertModel`` + the reference heads (``model.py:20-41``), so that
+    optimizer-state indices line up with reference checkpoints."""
+    e = "transformer.embeddings."
+    names = [e + "word_embeddings.weight", e + "position_embeddings.weight", e + "token_type_embeddings.weight",
+             e + "LayerNorm.weight", e + "LayerNorm.bias"]
+    for i in range(cfg.num_hidden_layers):
+        p = f"transformer.encoder.layer.{i}."
+        for sub in ("attention.self.query", "attention.self.key", "attention.self.value", "attention.output.dense",
+                    "attention.output.LayerNorm", "intermediate.dense", "output.dense", "output.LayerNorm"):
+            names += [p + sub + ".weight", p + sub + ".bias"]
+    names += ["transformer.pooler.dense.weight", "transformer.pooler.dense.bias"]
+    for h in ("position_outputs", "classifier.1", "reg_start.0", "reg_end.0"):
+        names += [h + ".weight", h + ".bias"]
+    return names
+
+
 def _init_store(store: ParamStore, cfg: EncoderConfig, generator: Optional[torch.Generator]):
     store.allocate("cpu", cfg.initializer_range, generator)
     for e in store.entries:
@@ -229,7 +246,10 @@ class BertForQuestionAnswering(nn.Module):
         gen = torch.Generator().manual_seed(seed) if seed is not None else None
         self.store = ParamStore(build_entries(config))
         _init_store(self.store, config, gen)
-        for name, prm in self.store.params.items():
+        order = hf_param_order(config)
+        assert sorted(order) == sorted(self.store.params), "param layout / HF order mismatch"
+        for name in order:
+            prm = self.store.params[name]
             *path, leaf = name.split(".")
             _ensure_module(self, path).register_parameter(leaf, prm)
         emb = _ensure_module(self, ["transformer", "embeddings"])

@@ -1,0 +1,182 @@
+"""Data-parallel gradient reducer over the flat grad arena (replaces torch DDP).
+
+Buckets are contiguous arena ranges built from the model's readiness groups (QA head+pooler,
+layer N-1 … layer 0, embeddings — the order backward produces them), merged until each reaches
+``bucket_cap_mb``.  The fused layer backward calls ``_on_group_ready``; when every group of a
+bucket has reported, the bucket's all-reduce is issued immediately, so communication overlaps
+the remaining backward.  ``finalize()`` makes the compute stream wait for the last bucket.
+
+* GPU + nccl: the native C++ ``Reducer`` owns an RCCL communicator and a high-priority comm
+  stream; ncclAvg in place on the arena slice (fp32) or through a bf16 scratch (``allreduce_dtype``).
+* CPU / gloo (and GPU when ``native=False``): ``torch.distributed.all_reduce(async_op=True)``.
+* ``prepare(sync=False)`` = DDP ``no_sync``: no communication during accumulation micro-batches
+  (fixes reference D1, which all-reduced every micro-batch).
+
+Sizing for xGMI: MI355X peers are point-to-point links (7 × ~153 GB/s per GPU); RCCL splits a
+bucket over its channels/rings, so 32 MiB buckets give each channel multi-MiB chunks while the first
+bucket (heads + last layer, ~30 MB) still starts early in the backward.
+"""
+from __future__ import annotations
+
+import itertools
+import logging
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .._native import kernels
+
+logger = logging.getLogger(__name__)
+_uid_counter = itertools.count()
+
+
+class Bucket:
+    __slots__ = ("index", "start", "end", "groups", "pending", "launched", "work")
+
+    def __init__(self, index, start, end, groups):
+        self.index, self.start, self.end, self.groups = index, start, end, list(groups)
+        self.pending = len(self.groups)
+        self.launched = False
+        self.work = None
+
+    @property
+    def numel(self):
+        return self.end - self.start
+
+
+class GradReducer:
+    def __init__(self, model, *, bucket_cap_mb: float = 32.0, allreduce_dtype: str = "fp32",
+                 native: Optional[bool] = None, broadcast_params: bool = True, group=None):
+        self.model = model
+        self.store = model.store
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.bucket_cap = int(bucket_cap_mb * 1024 * 1024)
+        self.allreduce_dtype = allreduce_dtype
+        self.active = False
+        self.buckets: List[Bucket] = []
+        self.group_to_bucket: Dict[str, Bucket] = {}
+        self._native = None
+        self._scratch = None
+        self.stats = {"buckets_launched": 0, "bytes": 0}
+        on_gpu = self.store.device.type == "cuda"
+        backend = dist.get_backend(group) if dist.is_initialized() else None
+        if native is None:
+            native = on_gpu and backend == "nccl"
+        if self.world > 1 and native:
+            self._native = self._make_native()
+        self._build_buckets()
+        model.set_grad_listener(self._on_group_ready)
+        if self.world > 1 and broadcast_params:
+            self.broadcast_parameters()
+
+    # ------------------------------------------------------------------ setup
+    def _make_native(self):
+        key = f"hq_rccl_uid_{next(_uid_counter)}"
+        store = dist.distributed_c10d._get_default_store()
+        if self.rank == 0:
+            uid = kernels().rccl_unique_id()
+            store.set(key, uid)
+        else:
+            uid = store.get(key)
+        dev = self.store.device.index if self.store.device.index is not None else torch.cuda.current_device()
+        red = kernels().Reducer(self.rank, self.world, bytes(uid), dev)
+        logger.info(f"native RCCL reducer up (rank {self.rank}/{self.world}, device {dev})")
+        return red
+
+    def _build_buckets(self):
+        trainable = {n for n, p in self.model.named_parameters() if p.requires_grad}
+        group_has_trainable = {}
+        for e in self.store.entries:
+            for hf, _, _ in e.views:
+                if hf in trainable:
+                    group_has_trainable[e.group] = True
+        elem = 4 if self.allreduce_dtype == "fp32" else 2
+        buckets: List[Tuple[int, int, List[str]]] = []
+        for g, s, e in self.store.group_ranges():
+            if not group_has_trainable.get(g):
+                continue
+            if buckets and (buckets[-1][1] == s) and (e - buckets[-1][0]) * elem <= self.bucket_cap:
+                bs, _, gs = buckets[-1]
+                buckets[-1] = (bs, e, gs + [g])
+            else:
+                buckets.append((s, e, [g]))
+        self.buckets = [Bucket(i, s, e, gs) for i, (s, e, gs) in enumerate(buckets)]
+        self.group_to_bucket = {g: b for b in self.buckets for g in b.groups}
+        if self.allreduce_dtype == "bf16" and self._native is not None and self.buckets:
+            n = max(b.numel for b in self.buckets)
+            self._scratch = torch.empty(self.store.total, dtype=torch.bfloat16, device=self.store.device)
+        logger.info("grad buckets (MiB): " + ", ".join(f"{b.numel * elem / 2**20:.1f}" for b in self.buckets))
+
+    def broadcast_parameters(self):
+        """Rank 0's weights to everyone (DDP constructor semantics)."""
+        m = self.store.master
+        if self._native is not None:
+            self._native.broadcast(m.data_ptr(), m.numel(), 0, 0, torch.cuda.current_stream().cuda_stream)
+            self._native.wait(torch.cuda.current_stream().cuda_stream)
+        else:
+            dist.broadcast(m, 0, group=self.group)
+        self.store.mark_master_dirty()
+        self.store.sync_compute()
+
+    # ------------------------------------------------------------------ per step
+    def prepare(self, sync: bool = True):
+        self.active = sync and self.world > 1
+        for b in self.buckets:
+            b.pending = len(b.groups)
+            b.launched = False
+            b.work = None
+
+    def _on_group_ready(self, group: str):
+        if not self.active:
+            return
+        b = self.group_to_bucket.get(group)
+        if b is None:
+            return
+        b.pending -= 1
+        if b.pending == 0:
+            self._launch(b)
+
+    def _launch(self, b: Bucket):
+        if b.launched:
+            return
+        b.launched = True
+        view = self.store.grad[b.start:b.end]
+        self.stats["buckets_launched"] += 1
+        if self._native is not None:
+            stream = torch.cuda.current_stream().cuda_stream
+            if self.allreduce_dtype == "bf16":
+                self._native.allreduce_bf16(view.data_ptr(), self._scratch[b.start:b.end].data_ptr(), b.numel, stream)
+            else:
+                self._native.allreduce_f32(view.data_ptr(), b.numel, stream)
+        else:
+            backend = dist.get_backend(self.group)
+            if backend == "nccl":
+                b.work = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+            else:
+                b.work = dist.all_reduce(view, group=self.group, async_op=True)
+
+    def finalize(self):
+        if not self.active:
+            return
+        for b in self.buckets:      # groups that never reported (e.g. unused heads): reduce anyway, in order
+            if not b.launched:
+                self._launch(b)
+        if self._native is not None:
+            self._native.wait(torch.cuda.current_stream().cuda_stream)
+        else:
+            scale = None if dist.get_backend(self.group) == "nccl" else 1.0 / self.world
+            for b in self.buckets:
+                if b.work is not None:
+                    b.work.wait()
+                    if scale is not None:
+                        self.store.grad[b.start:b.end].mul_(scale)
+        self.active = False
+
+    def close(self):
+        if self._native is not None:
+            self._native.synchronize()
+            self._native = None
+        self.model.set_grad_listener(None)

@@ -1,0 +1,110 @@
+"""One optimizer step of QA fine-tuning: the hot loop shared by ``Trainer`` and ``bench.py``.
+
+Per optimizer step (reference ``trainer.py:266-300`` semantics, re-engineered):
+  for each of ``batch_split`` micro-batches:
+      reducer.prepare(sync = last micro-batch)        # no_sync accumulation (fix of D1)
+      preds = model(**inputs); loss = Σ w_k·loss_k    # fused encoder, fp32 heads
+      (loss / batch_split).backward()                 # layer backward → arena grads → bucket all-reduce
+  reducer.finalize()                                  # compute stream waits for the last bucket
+  norm, coef = grad_norm_and_clip(arena)              # device scalars, no host sync
+  optimizer.step(clip_coef=coef)                      # one fused AdamW kernel (+ bf16 copy-out)
+  optimizer.zero_grad(); scheduler.step()
+Loss values stay on device (``LossRecord``); callers sync them at their logging cadence.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+import torch
+
+from ..models.losses import LossRecord
+from .optim import grad_norm_and_clip
+
+
+def to_device(data, device, non_blocking=True):
+    if isinstance(data, (list, tuple)):
+        return [to_device(d, device, non_blocking) for d in data]
+    if isinstance(data, dict):
+        return {k: to_device(v, device, non_blocking) for k, v in data.items()}
+    if torch.is_tensor(data):
+        return data.to(device, non_blocking=non_blocking)
+    return data
+
+
+@dataclass
+class StepResult:
+    losses: LossRecord
+    grad_norm: Optional[torch.Tensor]
+    lr: float
+    timings: Dict[str, float] = field(default_factory=dict)
+
+
+class TrainEngine:
+    def __init__(self, model, loss_fn, optimizer, *, scheduler=None, reducer=None, max_grad_norm: float = 1.0,
+                 batch_split: int = 1, no_sync_accum: bool = True, profile: bool = False):
+        self.model = model
+        self.loss_fn = loss_fn
+        self.optimizer = optimizer
+        self.scheduler = scheduler
+        self.reducer = reducer
+        self.max_grad_norm = max_grad_norm
+        self.batch_split = max(1, int(batch_split))
+        self.no_sync_accum = no_sync_accum
+        self.profile = profile
+        self.micro = 0
+
+    @property
+    def device(self):
+        return self.model.store.device
+
+    def _sync(self):
+        if self.profile and self.device.type == "cuda":
+            torch.cuda.synchronize()
+
+    def micro_step(self, inputs, labels) -> Optional[StepResult]:
+        """Forward+backward of one micro-batch; runs the optimizer on the accumulation boundary."""
+        t = {}
+        t0 = time.perf_counter()
+        boundary = (self.micro + 1) % self.batch_split == 0
+        if self.reducer is not None:
+            self.reducer.prepare(sync=boundary or not self.no_sync_accum)
+        preds = self.model(**inputs)
+        loss = self.loss_fn(preds, labels)
+        self._sync()
+        t1 = time.perf_counter()
+        (loss / self.batch_split).backward()
+        if self.reducer is not None and not boundary and not self.no_sync_accum:
+            self.reducer.finalize()
+        self._sync()
+        t2 = time.perf_counter()
+        self.micro += 1
+        t["fwd_ms"], t["bwd_ms"] = (t1 - t0) * 1e3, (t2 - t1) * 1e3
+        if not boundary:
+            return None
+        return self._apply(t)
+
+    def _apply(self, t) -> StepResult:
+        t2 = time.perf_counter()
+        if self.reducer is not None:
+            self.reducer.finalize()
+        self._sync()
+        t3 = time.perf_counter()
+        norm, coef = grad_norm_and_clip(self.model.store, self.max_grad_norm)
+        lr = self.optimizer.param_groups[0]["lr"]
+        self.optimizer.step(clip_coef=coef)
+        self.optimizer.zero_grad()
+        if self.scheduler is not None:
+            self.scheduler.step()
+        self._sync()
+        t4 = time.perf_counter()
+        t["comm_wait_ms"], t["optim_ms"] = (t3 - t2) * 1e3, (t4 - t3) * 1e3
+        return StepResult(losses=self.loss_fn.last, grad_norm=norm, lr=lr, timings=t)
+
+    def step(self, micro_batches) -> StepResult:
+        res = None
+        for inputs, labels in micro_batches:
+            res = self.micro_step(inputs, labels)
+        assert res is not None, "number of micro-batches must equal batch_split"
+        return res
