@@ -173,24 +173,31 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor key_bias, int64_t B, int64_t L, 
   c10::DeviceGuard g(qkv.device());
   auto ctx = at::empty({B * L, H}, qkv.options());
   auto lse = at::empty({B, nh, L}, key_bias.options());
-  hq_attn_fwd(ptr<uint16_t>(qkv), ptr<float>(key_bias), ptr<uint16_t>(ctx), ptr<float>(lse), (int)B, (int)L, (int)nh, 64,
-              (float)p, u32(seed), u32(opid), (float)scale, cur_stream());
-  return {ctx, lse};
+  const int64_t mbytes = p > 0 ? (int64_t)hq_attn_mask_bytes((int)B, (int)L, (int)nh) : 0;
+  auto mbits = at::empty({mbytes / 2}, qkv.options().dtype(at::kShort));
+  hq_attn_fwd(ptr<uint16_t>(qkv), ptr<float>(key_bias), ptr<uint16_t>(ctx), ptr<float>(lse),
+              mbytes ? ptr<uint16_t>(mbits) : nullptr, (int)B, (int)L, (int)nh, 64, (float)p, u32(seed), u32(opid),
+              (float)scale, cur_stream());
+  return {ctx, lse, mbits};
 }
 
-Tensor attn_bwd(Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, int64_t B, int64_t L, int64_t nh, double p,
-                int64_t seed, int64_t opid, double scale) {
+Tensor attn_bwd(Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, Tensor mbits, int64_t B, int64_t L,
+                int64_t nh, double p, double scale) {
   check_attn(qkv, key_bias, B, L, nh);
   check(dctx, BF16, "dctx"); check(ctx, BF16, "ctx"); check(lse, F32, "lse");
   const int64_t H = qkv.size(1) / 3;
   TORCH_CHECK(dctx.size(0) == B * L && dctx.size(1) == H && ctx.sizes() == dctx.sizes(), "ctx shapes");
   TORCH_CHECK(lse.numel() == B * nh * L, "lse shape");
+  if (p > 0) {
+    check(mbits, at::kShort, "mbits");
+    TORCH_CHECK(mbits.numel() * 2 == (int64_t)hq_attn_mask_bytes((int)B, (int)L, (int)nh), "dropout mask size");
+  }
   c10::DeviceGuard g(qkv.device());
   auto dqkv = at::empty_like(qkv);
   auto delta = at::empty({B, nh, L}, lse.options());
   hq_attn_bwd(ptr<uint16_t>(dctx), ptr<uint16_t>(qkv), ptr<uint16_t>(ctx), ptr<float>(lse), ptr<float>(key_bias),
-              ptr<uint16_t>(dqkv), ptr<float>(delta), (int)B, (int)L, (int)nh, 64, (float)p, u32(seed), u32(opid),
-              (float)scale, cur_stream());
+              p > 0 ? ptr<uint16_t>(mbits) : nullptr, ptr<uint16_t>(dqkv), ptr<float>(delta), (int)B, (int)L, (int)nh, 64,
+              (float)p, (float)scale, cur_stream());
   return dqkv;
 }
 

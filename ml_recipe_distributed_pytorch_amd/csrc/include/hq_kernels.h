@@ -32,11 +32,12 @@ void hq_gelu_bwd(const uint16_t* dout, const uint16_t* pre, uint16_t* dpre, floa
 void hq_bias_grad(const uint16_t* dy, float* part, HqOuts outs, int T, int N, bool accumulate, hipStream_t s);
 
 // ---- attention.hip ----------------------------------------------------------------------------
-void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, float* lse, int B, int L, int nh, int dh,
-                 float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s);
+size_t hq_attn_mask_bytes(int B, int L, int nh);   // dropout keep-bits written by fwd, read by bwd
+void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, float* lse, uint16_t* mbits, int B, int L,
+                 int nh, int dh, float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s);
 void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx, const float* lse, const float* key_bias,
-                 uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p, uint32_t seed, uint32_t opid,
-                 float scale, hipStream_t s);
+                 const uint16_t* mbits, uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p, float scale,
+                 hipStream_t s);
 
 // ---- optim.hip --------------------------------------------------------------------------------
 struct HqOptChunk {      // one work item of the fused optimizer: <= kOptChunk elements of one segment

@@ -1,28 +1,32 @@
 // Flash attention for BERT (head_dim 64, L <= 512, additive key mask, fused dropout) on gfx950.
 //
 // Input is the packed QKV GEMM output [T, 3H] (token-major; head h of Q/K/V at column
-// {0,H,2H} + 64h), so no head-split transpose is ever materialised; output ctx is written
-// straight in [T, H] and the backward writes dQ/dK/dV straight into packed dQKV [T, 3H].
+// {0,H,2H} + 64h), so no head-split transpose is ever materialised; ctx is written straight in
+// [T, H] and the backward writes dQ/dK/dV straight into packed dQKV [T, 3H].
 //
-// MFMA: v_mfma_f32_32x32x16_bf16 (32x32 tile, K=16, wave64).  Per wave 32 queries (fwd / dQ)
-// or 32 keys (dK/dV).  Orientation is chosen so every softmax statistic is lane-local:
-//   fwd : Sᵀ = K·Qᵀ (query on the lane) → online softmax needs one cross-half exchange per tile;
-//         Oᵀ += Vᵀ·Pᵀ takes Pᵀ straight from the accumulator registers as the B operand
-//         (cdna_hip_programming.md §3 "accumulator tile as the next MFMA's operand") and Vᵀ from
-//         LDS via ds_read_b64_tr_b16 (T10).
-//   dKdV: S = Q·Kᵀ (key on the lane); dVᵀ += dOᵀ·Pd and dKᵀ += Qᵀ·dS with Pd/dS from registers.
-//   dQ  : Sᵀ = K·Qᵀ (query on the lane); dQᵀ += Kᵀ·dSᵀ.
-// Two backward kernels (dK/dV per key block, dQ per query block) instead of dQ float atomics:
-// deterministic, and at L<=512 the recomputed QKᵀ/dOVᵀ is cheaper than 1.3 TB/s atomics.
-// Dropout on P uses the counter hash of hq_common.h with element index ((b·nh+h)·L+q)·L+k.
+// Structure (v2, "whole head per workgroup"): at BERT lengths a head's K and V (L·64·2 B each,
+// 96 KB at L=384) fit in LDS, so one workgroup of NWB waves loads them ONCE with every thread
+// issuing its 16-B loads up front (a single exposed HBM latency), one barrier, and then every
+// wave streams its 32 queries (fwd / dQ) or 32 keys (dK/dV) over the whole sequence with NO
+// further barriers.  (v1 staged 64-key tiles with two barriers each and no prefetch: 3-4x slower.)
+//
+// MFMA: v_mfma_f32_32x32x16_bf16 (32x32 tile, K=16, wave64).  Orientation keeps every softmax
+// statistic lane-local:
+//   fwd : Sᵀ = K·Qᵀ (query on the lane); Oᵀ += Vᵀ·Pᵀ with Pᵀ fed from the accumulator registers as
+//         the B operand (cdna_hip_programming.md §3) and Vᵀ via ds_read_b64_tr_b16 (T10).
+//         Online softmax rescales O only when some lane's running max grew (exact: α=1 otherwise).
+//   dQ  : Sᵀ, dPᵀ = V·dOᵀ (query on the lane); dQᵀ += Kᵀ·dSᵀ.  Also computes δ = rowsum(dO·O).
+//   dKdV: S = Q·Kᵀ, dP = dO·Vᵀ (key on the lane); dVᵀ += dOᵀ·Pd, dKᵀ += Qᵀ·dS.
+// Dropout: the forward draws keep bits from the counter hash (hq_common.h, element index
+// ((b·nh+h)·L+q)·L+k, bit-identical to ops/rng.py) and stores them as one 16-bit word per lane per
+// 32×32 subtile (14 MB per BERT-base layer at B=64); the backward kernels read the bits instead of
+// re-hashing (dKdV gathers its key's bits with ds_bpermute).
 #include "hq_common.h"
 #include "hq_kernels.h"
 
 namespace {
 
-constexpr int D = 64;          // head dim
-constexpr int KT = 64;         // keys per LDS tile (fwd, dQ)
-constexpr int QT = 64;         // queries per LDS tile (dK/dV)
+constexpr int D = 64;  // head dim
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
@@ -32,14 +36,13 @@ __device__ __forceinline__ f32x16_t mfma32(const bf16x8_t& a, const bf16x8_t& b,
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
-// 16-byte LDS row read: 8 bf16 at tile[row][col..col+7] (row stride D elements)
 __device__ __forceinline__ bf16x8_t lds_row8(const uint16_t* tile, int row, int col) {
   return *reinterpret_cast<const bf16x8_t*>(tile + row * D + col);
 }
 
-// A operand "Xᵀ" of a 32x32x16 MFMA from a row-major [rows][64] LDS tile, k-step s of a 32-row
-// subtile starting at row0: lane supplies X[row(s,hh,j)][d] with d = dblk*32 + (lane&31) and
-// row(s,hh,j) = row0 + 16s + 4hh + (j&3) + 8(j>>2)  (the k order of an accumulator-fed B operand).
+// A operand "Xᵀ" of a 32x32x16 MFMA from a row-major [rows][64] LDS image: lane supplies
+// X[row(s,hh,j)][d], d = dblk*32 + (lane&31), row = row0 + 16s + 4hh + (j&3) + 8(j>>2) (the k order
+// of an accumulator-fed B operand).
 __device__ __forceinline__ bf16x8_t lds_tr8(const uint16_t* tile, int row0, int s, int dblk, int lane) {
   const int g = lane >> 4, i = lane & 15;
   const int hh = g >> 1, dsub = g & 1;
@@ -53,48 +56,69 @@ __device__ __forceinline__ bf16x8_t lds_tr8(const uint16_t* tile, int row0, int 
   return out;
 }
 
-// accumulator registers 8s..8s+7 → bf16 B fragment
 __device__ __forceinline__ bf16x8_t pack_b(const float* v, int s) {
-  bf16x8_t out;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) out[j] = (short)hq_f2bf(v[8 * s + j]);
-  return out;
+  const uint32_t w0 = hq_pack2(v[8 * s + 0], v[8 * s + 1]), w1 = hq_pack2(v[8 * s + 2], v[8 * s + 3]);
+  const uint32_t w2 = hq_pack2(v[8 * s + 4], v[8 * s + 5]), w3 = hq_pack2(v[8 * s + 6], v[8 * s + 7]);
+  typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+  u32x4 u = {w0, w1, w2, w3};
+  return __builtin_bit_cast(bf16x8_t, u);
 }
 
-// row (within a 32-row MFMA tile) of accumulator register r for lane-half hh
 __device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
 
-// cooperative global→LDS copy of a [64][64] bf16 tile: rows row0.. of a [*, ld] matrix (zero past nrows)
-__device__ __forceinline__ void stage_tile(uint16_t* lds, const uint16_t* src, size_t ld, int row0, int nrows) {
+// Cooperative copy of rows [0, Lp) of a [*, ld] bf16 matrix (64 columns starting at src) into a
+// [Lp][64] LDS image; rows >= L are zero.  Each thread issues all its 16-B loads before any store.
+template <int NT>
+__device__ __forceinline__ void load_head(uint16_t* dst, const uint16_t* src, size_t ld, int L, int Lp) {
+  constexpr int kMax = 8;  // up to 512 rows × 8 chunks / (NT threads)
+  uint4 buf[kMax];
+  const int n = Lp * 8;
 #pragma unroll
-  for (int pass = 0; pass < 2; ++pass) {
-    const int t = threadIdx.x + pass * 256;
-    const int row = t >> 3, chunk = t & 7;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (row0 + row < nrows) v = *reinterpret_cast<const uint4*>(src + (size_t)(row0 + row) * ld + chunk * 8);
-    *reinterpret_cast<uint4*>(lds + row * D + chunk * 8) = v;
+  for (int i = 0; i < kMax; ++i) {
+    const int t = threadIdx.x + i * NT;
+    buf[i] = make_uint4(0, 0, 0, 0);
+    if (t < n) {
+      const int row = t >> 3;
+      if (row < L) buf[i] = *reinterpret_cast<const uint4*>(src + (size_t)row * ld + (t & 7) * 8);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < kMax; ++i) {
+    const int t = threadIdx.x + i * NT;
+    if (t < n) *reinterpret_cast<uint4*>(dst + (t >> 3) * D + (t & 7) * 8) = buf[i];
   }
 }
 
 // ============================================================================ forward
-__global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, const float* __restrict__ key_bias,
-                                                       uint16_t* __restrict__ ctx, float* __restrict__ lse, int L, int nh,
-                                                       float c_scale, uint32_t key, uint32_t thr, float kscale) {
-  __shared__ __attribute__((aligned(16))) uint16_t sK[KT * D];
-  __shared__ __attribute__((aligned(16))) uint16_t sV[KT * D];
-  __shared__ __attribute__((aligned(16))) float sB[KT];
+template <int NWB>
+__global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __restrict__ qkv,
+                                                            const float* __restrict__ key_bias,
+                                                            uint16_t* __restrict__ ctx, float* __restrict__ lse,
+                                                            uint16_t* __restrict__ mbits, int L, int nh, float c_scale,
+                                                            uint32_t key, uint32_t thr, float kscale) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int Lp = (L + 31) & ~31, n32 = Lp >> 5;
+  uint16_t* sK = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* sV = sK + Lp * D;
+  float* sB = reinterpret_cast<float*>(sV + Lp * D);
   const int H = nh * D, ld = 3 * H;
-  const int bh = blockIdx.y, b = bh / nh, h = bh % nh;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int hh = lane >> 5;
-  const int qi = blockIdx.x * 128 + wave * 32 + (lane & 31);
+  const int bh = blockIdx.x, b = bh / nh, h = bh % nh;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, hh = lane >> 5;
+  const int qs = blockIdx.y * NWB + wave;  // 32-query subtile
+  const int qi = qs * 32 + (lane & 31);
   const uint16_t* base = qkv + (size_t)b * L * ld + h * D;
 
   bf16x8_t qf[4];
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    qf[s] = (qi < L) ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)qi * ld + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-  }
+  for (int s = 0; s < 4; ++s)
+    qf[s] = (qi < L) ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)qi * ld + 16 * s + 8 * hh)
+                     : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  load_head<NWB * 64>(sK, base + H, ld, L, Lp);
+  load_head<NWB * 64>(sV, base + 2 * H, ld, L, Lp);
+  for (int t = threadIdx.x; t < Lp; t += NWB * 64) sB[t] = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -INFINITY;
+  __syncthreads();
+  if (qs * 32 >= L) return;
+
   f32x16_t o[2];
 #pragma unroll
   for (int d = 0; d < 2; ++d)
@@ -103,78 +127,70 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   float m_run = -INFINITY, l_run = 0.f;
   const uint32_t row_idx = ((uint32_t)bh * L + (uint32_t)min(qi, L - 1)) * (uint32_t)L;
   const bool pair_ok = ((L & 1) == 0);
+  uint16_t* my_bits = mbits ? mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane : nullptr;
 
-  for (int k0 = 0; k0 < L; k0 += KT) {
-    stage_tile(sK, base + H, ld, k0, L);
-    stage_tile(sV, base + 2 * H, ld, k0, L);
-    if (threadIdx.x < KT) {
-      const int kk = k0 + threadIdx.x;
-      sB[threadIdx.x] = kk < L ? key_bias[(size_t)b * L + kk] * LOG2E : -INFINITY;
-    }
-    __syncthreads();
-    float sc[2][16];
+  for (int kt = 0; kt < n32; ++kt) {
+    f32x16_t acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = mfma32(lds_row8(sK, kt * 32 + (lane & 31), 16 * s + 8 * hh), qf[s], acc);
+    float sc[16];
     float mx = -INFINITY;
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      f32x16_t acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc = mfma32(lds_row8(sK, sub * 32 + (lane & 31), 16 * s + 8 * hh), qf[s], acc);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 bb = *reinterpret_cast<const float4*>(sB + sub * 32 + 8 * g + 4 * hh);
-        sc[sub][4 * g + 0] = acc[4 * g + 0] * c_scale + bb.x;
-        sc[sub][4 * g + 1] = acc[4 * g + 1] * c_scale + bb.y;
-        sc[sub][4 * g + 2] = acc[4 * g + 2] * c_scale + bb.z;
-        sc[sub][4 * g + 3] = acc[4 * g + 3] * c_scale + bb.w;
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[sub][r]);
+    for (int g = 0; g < 4; ++g) {
+      const float4 bb = *reinterpret_cast<const float4*>(sB + kt * 32 + 8 * g + 4 * hh);
+      sc[4 * g + 0] = fmaf(acc[4 * g + 0], c_scale, bb.x);
+      sc[4 * g + 1] = fmaf(acc[4 * g + 1], c_scale, bb.y);
+      sc[4 * g + 2] = fmaf(acc[4 * g + 2], c_scale, bb.z);
+      sc[4 * g + 3] = fmaf(acc[4 * g + 3], c_scale, bb.w);
     }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f(m_run - m_new);
-    m_run = m_new;
+    if (__any(mx > m_run)) {  // exact rescale skip: α = 1 for every lane whose max did not grow
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = exp2f(m_run - m_new);
+      m_run = m_new;
+      l_run *= alpha;
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+    }
     float rs = 0.f;
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        sc[sub][r] = exp2f(sc[sub][r] - m_new);
-        rs += sc[sub][r];
-      }
-    l_run = l_run * alpha + rs;
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+    for (int r = 0; r < 16; ++r) {
+      sc[r] = exp2f(sc[r] - m_run);
+      rs += sc[r];
+    }
+    l_run += rs;
     if (thr) {
+      uint32_t bits = 0;
 #pragma unroll
-      for (int sub = 0; sub < 2; ++sub)
+      for (int g = 0; g < 4; ++g) {
+        const uint32_t idx0 = row_idx + kt * 32 + 8 * g + 4 * hh;
+        float mk[4];
+        if (pair_ok) {
+          hq_keep4(idx0, key, thr, kscale, mk);
+        } else {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const uint32_t idx0 = row_idx + k0 + sub * 32 + 8 * g + 4 * hh;
-          float mk[4];
-          if (pair_ok) {
-            hq_keep4(idx0, key, thr, kscale, mk);
-          } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) mk[i] = hq_keep(idx0 + i, key, thr) ? kscale : 0.f;
-          }
-#pragma unroll
-          for (int i = 0; i < 4; ++i) sc[sub][4 * g + i] *= mk[i];
+          for (int i = 0; i < 4; ++i) mk[i] = hq_keep(idx0 + i, key, thr) ? kscale : 0.f;
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          sc[4 * g + i] *= mk[i];
+          bits |= (mk[i] != 0.f ? 1u : 0u) << (4 * g + i);
+        }
+      }
+      if (my_bits) my_bits[(size_t)kt * 64] = (uint16_t)bits;
     }
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub)
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8_t pb = pack_b(sc, s);
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8_t pb = pack_b(sc[sub], s);
-#pragma unroll
-        for (int d = 0; d < 2; ++d) o[d] = mfma32(lds_tr8(sV, sub * 32, s, d, lane), pb, o[d]);
-      }
-    __syncthreads();
+      for (int d = 0; d < 2; ++d) o[d] = mfma32(lds_tr8(sV, kt * 32, s, d, lane), pb, o[d]);
+    }
   }
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
   const float inv = 1.f / l_tot;
@@ -191,209 +207,90 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   }
 }
 
-// ============================================================================ backward
-// delta[bh][q] = Σ_d dO·O   (one thread per (token, head))
-__global__ __launch_bounds__(256) void attn_delta_kernel(const uint16_t* __restrict__ dctx, const uint16_t* __restrict__ ctx,
-                                                         float* __restrict__ delta, int T, int L, int nh) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= T * nh) return;
-  const int t = i / nh, h = i % nh;
-  const int H = nh * D;
-  const uint4* a = reinterpret_cast<const uint4*>(dctx + (size_t)t * H + h * D);
-  const uint4* c = reinterpret_cast<const uint4*>(ctx + (size_t)t * H + h * D);
-  float s = 0.f;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float x[8], y[8];
-    hq_unpack8(a[k], x);
-    hq_unpack8(c[k], y);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += x[j] * y[j];
-  }
-  const int b = t / L, q = t % L;
-  delta[((size_t)b * nh + h) * L + q] = s;
-}
-
-// dK, dV for 128 keys per block (32 per wave), looping over all queries in 64-row LDS tiles
-__global__ __launch_bounds__(256) void attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dctx,
-                                                            const float* __restrict__ lse, const float* __restrict__ delta,
-                                                            const float* __restrict__ key_bias, uint16_t* __restrict__ dqkv,
-                                                            int L, int nh, float c_scale, float scale, uint32_t key,
-                                                            uint32_t thr, float kscale) {
-  __shared__ __attribute__((aligned(16))) uint16_t sQ[QT * D];
-  __shared__ __attribute__((aligned(16))) uint16_t sO[QT * D];   // dO tile
-  __shared__ __attribute__((aligned(16))) float sL[QT];           // lse·log2e (+inf past L)
-  __shared__ __attribute__((aligned(16))) float sD[QT];           // delta
+// ============================================================================ backward: dQ (+ δ)
+template <int NWB>
+__global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv,
+                                                               const uint16_t* __restrict__ dctx,
+                                                               const uint16_t* __restrict__ ctx,
+                                                               const float* __restrict__ lse,
+                                                               const float* __restrict__ key_bias,
+                                                               const uint16_t* __restrict__ mbits,
+                                                               float* __restrict__ delta, uint16_t* __restrict__ dqkv,
+                                                               int L, int nh, float c_scale, float scale, float kscale) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int Lp = (L + 31) & ~31, n32 = Lp >> 5;
+  uint16_t* sK = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* sV = sK + Lp * D;
+  float* sB = reinterpret_cast<float*>(sV + Lp * D);
   const int H = nh * D, ld = 3 * H;
-  const int bh = blockIdx.y, b = bh / nh, h = bh % nh;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int hh = lane >> 5;
-  const int kj = blockIdx.x * 128 + wave * 32 + (lane & 31);  // this lane's key (S column)
-  const uint16_t* base = qkv + (size_t)b * L * ld + h * D;
-  const uint16_t* dbase = dctx + (size_t)b * L * H + h * D;
-
-  bf16x8_t kf[4], vf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const bool ok = kj < L;
-    kf[s] = ok ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)kj * ld + H + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-    vf[s] = ok ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)kj * ld + 2 * H + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-  }
-  const float kb = kj < L ? key_bias[(size_t)b * L + kj] * LOG2E : -INFINITY;
-  f32x16_t dv[2], dk[2];
-#pragma unroll
-  for (int d = 0; d < 2; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { dv[d][r] = 0.f; dk[d][r] = 0.f; }
-
-  for (int q0 = 0; q0 < L; q0 += QT) {
-    stage_tile(sQ, base, ld, q0, L);
-    stage_tile(sO, dbase, H, q0, L);
-    if (threadIdx.x < QT) {
-      const int qq = q0 + threadIdx.x;
-      sL[threadIdx.x] = qq < L ? lse[(size_t)bh * L + qq] * LOG2E : INFINITY;
-      sD[threadIdx.x] = qq < L ? delta[(size_t)bh * L + qq] : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      f32x16_t s_acc, p_acc;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { s_acc[r] = 0.f; p_acc[r] = 0.f; }
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        s_acc = mfma32(lds_row8(sQ, sub * 32 + (lane & 31), 16 * s + 8 * hh), kf[s], s_acc);
-        p_acc = mfma32(lds_row8(sO, sub * 32 + (lane & 31), 16 * s + 8 * hh), vf[s], p_acc);
-      }
-      float pd[16], ds[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 l4 = *reinterpret_cast<const float4*>(sL + sub * 32 + 8 * g + 4 * hh);
-        const float4 d4 = *reinterpret_cast<const float4*>(sD + sub * 32 + 8 * g + 4 * hh);
-        const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
-        const float dlt[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = 4 * g + i;
-          const float P = exp2f(s_acc[r] * c_scale + kb - lv[i]);
-          float mk = 1.f;
-          if (thr) {
-            const int q = q0 + sub * 32 + acc_row(r, hh);
-            const uint32_t idx = ((uint32_t)bh * L + (uint32_t)min(q, L - 1)) * (uint32_t)L + (uint32_t)min(kj, L - 1);
-            mk = hq_keep(idx, key, thr) ? kscale : 0.f;
-          }
-          pd[r] = P * mk;
-          ds[r] = P * (p_acc[r] * mk - dlt[i]);
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8_t pb = pack_b(pd, s);
-        const bf16x8_t sb = pack_b(ds, s);
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          dv[d] = mfma32(lds_tr8(sO, sub * 32, s, d, lane), pb, dv[d]);
-          dk[d] = mfma32(lds_tr8(sQ, sub * 32, s, d, lane), sb, dk[d]);
-        }
-      }
-    }
-    __syncthreads();
-  }
-  if (kj < L) {
-    uint16_t* out = dqkv + ((size_t)b * L + kj) * ld + h * D;
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float k4[4] = {dk[d][4 * g] * scale, dk[d][4 * g + 1] * scale, dk[d][4 * g + 2] * scale, dk[d][4 * g + 3] * scale};
-        float v4[4] = {dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]};
-        *reinterpret_cast<uint2*>(out + H + d * 32 + 8 * g + 4 * hh) = hq_pack4(k4);
-        *reinterpret_cast<uint2*>(out + 2 * H + d * 32 + 8 * g + 4 * hh) = hq_pack4(v4);
-      }
-  }
-}
-
-// dQ for 128 queries per block (32 per wave), looping over all keys in 64-row LDS tiles
-__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dctx,
-                                                          const float* __restrict__ lse, const float* __restrict__ delta,
-                                                          const float* __restrict__ key_bias, uint16_t* __restrict__ dqkv,
-                                                          int L, int nh, float c_scale, float scale, uint32_t key,
-                                                          uint32_t thr, float kscale) {
-  __shared__ __attribute__((aligned(16))) uint16_t sK[KT * D];
-  __shared__ __attribute__((aligned(16))) uint16_t sV[KT * D];
-  __shared__ __attribute__((aligned(16))) float sB[KT];
-  const int H = nh * D, ld = 3 * H;
-  const int bh = blockIdx.y, b = bh / nh, h = bh % nh;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int hh = lane >> 5;
-  const int qi = blockIdx.x * 128 + wave * 32 + (lane & 31);
+  const int bh = blockIdx.x, b = bh / nh, h = bh % nh;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, hh = lane >> 5;
+  const int qs = blockIdx.y * NWB + wave;
+  const int qi = qs * 32 + (lane & 31);
   const bool qok = qi < L;
   const uint16_t* base = qkv + (size_t)b * L * ld + h * D;
+  const size_t orow = ((size_t)b * L + qi) * H + h * D;
+
   bf16x8_t qf[4], of[4];
+  float dpart = 0.f;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     qf[s] = qok ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)qi * ld + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-    of[s] = qok ? *reinterpret_cast<const bf16x8_t*>(dctx + ((size_t)b * L + qi) * H + h * D + 16 * s + 8 * hh)
-                : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    of[s] = qok ? *reinterpret_cast<const bf16x8_t*>(dctx + orow + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    if (qok) {
+      float x[8], y[8];
+      hq_unpack8(__builtin_bit_cast(uint4, of[s]), x);
+      hq_unpack8(*reinterpret_cast<const uint4*>(ctx + orow + 16 * s + 8 * hh), y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dpart += x[j] * y[j];
+    }
   }
+  load_head<NWB * 64>(sK, base + H, ld, L, Lp);
+  load_head<NWB * 64>(sV, base + 2 * H, ld, L, Lp);
+  for (int t = threadIdx.x; t < Lp; t += NWB * 64) sB[t] = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -INFINITY;
+  const float dlt = dpart + __shfl_xor(dpart, 32, 64);  // δ = rowsum(dO·O) over all 64 dims
   const float lq = qok ? lse[(size_t)bh * L + qi] * LOG2E : INFINITY;
-  const float dq_delta = qok ? delta[(size_t)bh * L + qi] : 0.f;
-  const uint32_t row_idx = ((uint32_t)bh * L + (uint32_t)min(qi, L - 1)) * (uint32_t)L;
-  const bool pair_ok = ((L & 1) == 0);
+  if (qok && hh == 0) delta[(size_t)bh * L + qi] = dlt;
+  __syncthreads();
+  if (qs * 32 >= L) return;
+
   f32x16_t dq[2];
 #pragma unroll
   for (int d = 0; d < 2; ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
+  const uint16_t* my_bits = mbits ? mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane : nullptr;
 
-  for (int k0 = 0; k0 < L; k0 += KT) {
-    stage_tile(sK, base + H, ld, k0, L);
-    stage_tile(sV, base + 2 * H, ld, k0, L);
-    if (threadIdx.x < KT) {
-      const int kk = k0 + threadIdx.x;
-      sB[threadIdx.x] = kk < L ? key_bias[(size_t)b * L + kk] * LOG2E : -INFINITY;
+  for (int kt = 0; kt < n32; ++kt) {
+    f32x16_t s_acc, p_acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { s_acc[r] = 0.f; p_acc[r] = 0.f; }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s_acc = mfma32(lds_row8(sK, kt * 32 + (lane & 31), 16 * s + 8 * hh), qf[s], s_acc);
+      p_acc = mfma32(lds_row8(sV, kt * 32 + (lane & 31), 16 * s + 8 * hh), of[s], p_acc);
     }
-    __syncthreads();
+    const uint32_t bits = my_bits ? (uint32_t)my_bits[(size_t)kt * 64] : 0xFFFFu;
+    const float ks = my_bits ? kscale : 1.f;
+    float ds[16];
 #pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      f32x16_t s_acc, p_acc;
+    for (int g = 0; g < 4; ++g) {
+      const float4 bb = *reinterpret_cast<const float4*>(sB + kt * 32 + 8 * g + 4 * hh);
+      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { s_acc[r] = 0.f; p_acc[r] = 0.f; }
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        s_acc = mfma32(lds_row8(sK, sub * 32 + (lane & 31), 16 * s + 8 * hh), qf[s], s_acc);
-        p_acc = mfma32(lds_row8(sV, sub * 32 + (lane & 31), 16 * s + 8 * hh), of[s], p_acc);
-      }
-      float ds[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 bb = *reinterpret_cast<const float4*>(sB + sub * 32 + 8 * g + 4 * hh);
-        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
-        float mk[4] = {1.f, 1.f, 1.f, 1.f};
-        if (thr) {
-          const uint32_t idx0 = row_idx + k0 + sub * 32 + 8 * g + 4 * hh;
-          if (pair_ok) {
-            hq_keep4(idx0, key, thr, kscale, mk);
-          } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) mk[i] = hq_keep(idx0 + i, key, thr) ? kscale : 0.f;
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int r = 4 * g + i;
-          const float P = exp2f(s_acc[r] * c_scale + bv[i] - lq);
-          ds[r] = P * (p_acc[r] * mk[i] - dq_delta);
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8_t sb = pack_b(ds, s);
-#pragma unroll
-        for (int d = 0; d < 2; ++d) dq[d] = mfma32(lds_tr8(sK, sub * 32, s, d, lane), sb, dq[d]);
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * g + i;
+        const float P = exp2f(fmaf(s_acc[r], c_scale, bv[i]) - lq);
+        const float mk = ((bits >> r) & 1u) ? ks : 0.f;
+        ds[r] = P * fmaf(p_acc[r], mk, -dlt);
       }
     }
-    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8_t sb = pack_b(ds, s);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) dq[d] = mfma32(lds_tr8(sK, kt * 32, s, d, lane), sb, dq[d]);
+    }
   }
   if (qok) {
     uint16_t* out = dqkv + ((size_t)b * L + qi) * ld + h * D;
@@ -407,28 +304,190 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
   }
 }
 
+// ============================================================================ backward: dK, dV
+template <int NWB>
+__global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv,
+                                                                 const uint16_t* __restrict__ dctx,
+                                                                 const float* __restrict__ lse,
+                                                                 const float* __restrict__ delta,
+                                                                 const float* __restrict__ key_bias,
+                                                                 const uint16_t* __restrict__ mbits,
+                                                                 uint16_t* __restrict__ dqkv, int L, int nh,
+                                                                 float c_scale, float scale, float kscale) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int Lp = (L + 31) & ~31, n32 = Lp >> 5;
+  uint16_t* sQ = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* sO = sQ + Lp * D;  // dO
+  float* sL = reinterpret_cast<float*>(sO + Lp * D);  // lse·log2e (+inf past L)
+  float* sD = sL + Lp;                                // δ
+  const int H = nh * D, ld = 3 * H;
+  const int bh = blockIdx.x, b = bh / nh, h = bh % nh;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, hh = lane >> 5;
+  const int ks_idx = blockIdx.y * NWB + wave;  // 32-key subtile
+  const int kj = ks_idx * 32 + (lane & 31);
+  const bool kok = kj < L;
+  const uint16_t* base = qkv + (size_t)b * L * ld + h * D;
+
+  bf16x8_t kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = kok ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)kj * ld + H + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    vf[s] = kok ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)kj * ld + 2 * H + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  const float kb = kok ? key_bias[(size_t)b * L + kj] * LOG2E : -INFINITY;
+  load_head<NWB * 64>(sQ, base, ld, L, Lp);
+  load_head<NWB * 64>(sO, dctx + (size_t)b * L * H + h * D, H, L, Lp);
+  for (int t = threadIdx.x; t < Lp; t += NWB * 64) {
+    sL[t] = t < L ? lse[(size_t)bh * L + t] * LOG2E : INFINITY;
+    sD[t] = t < L ? delta[(size_t)bh * L + t] : 0.f;
+  }
+  __syncthreads();
+  if (ks_idx * 32 >= L) return;
+
+  f32x16_t dv[2], dk[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dv[d][r] = 0.f; dk[d][r] = 0.f; }
+  // forward bit layout: word of fwd-lane l' = q + 32·hh', bit r' with acc_row(r', hh') = key-in-subtile
+  const int krel = lane & 31;
+  const int hh_f = (krel >> 2) & 1;
+  const int r_f = (krel & 3) + 4 * (krel >> 3);
+
+  for (int qt = 0; qt < n32; ++qt) {
+    f32x16_t s_acc, p_acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { s_acc[r] = 0.f; p_acc[r] = 0.f; }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      s_acc = mfma32(lds_row8(sQ, qt * 32 + (lane & 31), 16 * s + 8 * hh), kf[s], s_acc);
+      p_acc = mfma32(lds_row8(sO, qt * 32 + (lane & 31), 16 * s + 8 * hh), vf[s], p_acc);
+    }
+    uint32_t word = 0xFFFFu;
+    float ksc = 1.f;
+    if (mbits) {
+      word = mbits[(((size_t)bh * n32 + qt) * n32 + ks_idx) * 64 + lane];
+      ksc = kscale;
+    }
+    float pd[16], ds[16];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 l4 = *reinterpret_cast<const float4*>(sL + qt * 32 + 8 * g + 4 * hh);
+      const float4 d4 = *reinterpret_cast<const float4*>(sD + qt * 32 + 8 * g + 4 * hh);
+      const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+      const float dl[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 4 * g + i;
+        const int qrel = acc_row(r, hh);
+        // bit (qrel, krel) lives in fwd lane qrel + 32·hh_f, bit r_f
+        const uint32_t w = mbits ? (uint32_t)__shfl((int)word, qrel + 32 * hh_f, 64) : 0xFFFFu;
+        const float mk = ((w >> r_f) & 1u) ? ksc : 0.f;
+        const float P = exp2f(fmaf(s_acc[r], c_scale, kb) - lv[i]);
+        pd[r] = P * mk;
+        ds[r] = P * fmaf(p_acc[r], mk, -dl[i]);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8_t pb = pack_b(pd, s);
+      const bf16x8_t sb = pack_b(ds, s);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        dv[d] = mfma32(lds_tr8(sO, qt * 32, s, d, lane), pb, dv[d]);
+        dk[d] = mfma32(lds_tr8(sQ, qt * 32, s, d, lane), sb, dk[d]);
+      }
+    }
+  }
+  if (kok) {
+    uint16_t* out = dqkv + ((size_t)b * L + kj) * ld + h * D;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        float k4[4] = {dk[d][4 * g] * scale, dk[d][4 * g + 1] * scale, dk[d][4 * g + 2] * scale, dk[d][4 * g + 3] * scale};
+        float v4[4] = {dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]};
+        *reinterpret_cast<uint2*>(out + H + d * 32 + 8 * g + 4 * hh) = hq_pack4(k4);
+        *reinterpret_cast<uint2*>(out + 2 * H + d * 32 + 8 * g + 4 * hh) = hq_pack4(v4);
+      }
+  }
+}
+
+// waves per workgroup for a sequence of L: all 32-row subtiles of a head in one workgroup up to
+// 12 waves (L <= 384: 3 waves/SIMD), else 8 waves with the head split over grid.y.
+int waves_for(int L) {
+  const int n32 = (L + 31) / 32;
+  return n32 <= 12 ? n32 : 8;
+}
+
+template <template <int> class K, typename F>
+void dispatch_waves(int nw, F&& f) {
+  switch (nw) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 3: f(std::integral_constant<int, 3>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 5: f(std::integral_constant<int, 5>{}); break;
+    case 6: f(std::integral_constant<int, 6>{}); break;
+    case 7: f(std::integral_constant<int, 7>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    case 9: f(std::integral_constant<int, 9>{}); break;
+    case 10: f(std::integral_constant<int, 10>{}); break;
+    case 11: f(std::integral_constant<int, 11>{}); break;
+    case 12: f(std::integral_constant<int, 12>{}); break;
+    default: fprintf(stderr, "hq attention: bad wave count %d\n", nw); abort();
+  }
+}
+
+template <int N> struct FwdTag {};
+
 }  // namespace
 
-void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, float* lse, int B, int L, int nh, int dh,
-                 float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s) {
-  if (dh != D) { fprintf(stderr, "hq_attn_fwd: head_dim %d unsupported (64 only)\n", dh); abort(); }
+size_t hq_attn_mask_bytes(int B, int L, int nh) {
+  const size_t n32 = (size_t)(L + 31) / 32;
+  return (size_t)B * nh * n32 * n32 * 64 * sizeof(uint16_t);
+}
+
+void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, float* lse, uint16_t* mbits, int B, int L,
+                 int nh, int dh, float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s) {
+  if (dh != D || L > 512) { fprintf(stderr, "hq_attn_fwd: head_dim %d / L %d unsupported\n", dh, L); abort(); }
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const uint32_t key = hq_op_key(seed, opid);
-  hipLaunchKernelGGL(attn_fwd_kernel, dim3((L + 127) / 128, B * nh), dim3(256), 0, s, qkv, key_bias, ctx, lse, L, nh,
-                     scale * LOG2E, key, thr, hq_keep_scale(thr));
+  const int Lp = (L + 31) & ~31, n32 = Lp / 32;
+  const int nw = waves_for(L);
+  const size_t lds = (size_t)Lp * D * 2 * 2 + Lp * sizeof(float);
+  dispatch_waves<FwdTag>(nw, [&](auto c) {
+    constexpr int NW = decltype(c)::value;
+    static bool attr = (hipFuncSetAttribute((const void*)attn_fwd_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            160 * 1024) == hipSuccess);
+    (void)attr;
+    hipLaunchKernelGGL(attn_fwd_kernel<NW>, dim3(B * nh, (n32 + NW - 1) / NW), dim3(NW * 64), lds, s, qkv, key_bias,
+                       ctx, lse, thr ? mbits : nullptr, L, nh, scale * LOG2E, key, thr, hq_keep_scale(thr));
+  });
 }
 
 void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx, const float* lse, const float* key_bias,
-                 uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p, uint32_t seed, uint32_t opid,
+                 const uint16_t* mbits, uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p,
                  float scale, hipStream_t s) {
-  if (dh != D) { fprintf(stderr, "hq_attn_bwd: head_dim %d unsupported (64 only)\n", dh); abort(); }
+  if (dh != D || L > 512) { fprintf(stderr, "hq_attn_bwd: head_dim %d / L %d unsupported\n", dh, L); abort(); }
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
-  const uint32_t key = hq_op_key(seed, opid);
   const float ks = hq_keep_scale(thr);
-  const int T = B * L;
-  hipLaunchKernelGGL(attn_delta_kernel, dim3((T * nh + 255) / 256), dim3(256), 0, s, dctx, ctx, delta, T, L, nh);
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, dim3((L + 127) / 128, B * nh), dim3(256), 0, s, qkv, dctx, lse, delta, key_bias,
-                     dqkv, L, nh, scale * LOG2E, scale, key, thr, ks);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, dim3((L + 127) / 128, B * nh), dim3(256), 0, s, qkv, dctx, lse, delta, key_bias,
-                     dqkv, L, nh, scale * LOG2E, scale, key, thr, ks);
+  const uint16_t* bits = thr ? mbits : nullptr;
+  const int Lp = (L + 31) & ~31, n32 = Lp / 32;
+  const int nw = waves_for(L);
+  const size_t lds_dq = (size_t)Lp * D * 2 * 2 + Lp * sizeof(float);
+  const size_t lds_kv = (size_t)Lp * D * 2 * 2 + 2 * Lp * sizeof(float);
+  dispatch_waves<FwdTag>(nw, [&](auto c) {
+    constexpr int NW = decltype(c)::value;
+    static bool attr = (hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                            160 * 1024) == hipSuccess) &&
+                       (hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<NW>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess);
+    (void)attr;
+    const dim3 grid(B * nh, (n32 + NW - 1) / NW);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<NW>, grid, dim3(NW * 64), lds_dq, s, qkv, dctx, ctx, lse, key_bias, bits, delta,
+                       dqkv, L, nh, scale * LOG2E, scale, ks);
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<NW>, grid, dim3(NW * 64), lds_kv, s, qkv, dctx, lse, delta, key_bias, bits,
+                       dqkv, L, nh, scale * LOG2E, scale, ks);
+  });
 }

@@ -166,7 +166,7 @@ class _LayerFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(cfg.head_dim)
         op0 = 1 + 3 * idx
         qkv = ops.linear_fwd(x, st.view(p + "qkv.weight"), st.view(p + "qkv.bias"))
-        ctxv, lse = ops.attn_fwd(qkv, key_bias, B, L, nh, pa, info.seed, op0, scale)
+        ctxv, lse, bits = ops.attn_fwd(qkv, key_bias, B, L, nh, pa, info.seed, op0, scale)
         a1 = ops.linear_fwd(ctxv, st.view(p + "attention.output.dense.weight"), st.view(p + "attention.output.dense.bias"))
         h1, z1, m1, r1 = ops.ln_fwd(a1, x, st.view(p + "attention.output.LayerNorm.weight", "master"),
                                     st.view(p + "attention.output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph,
@@ -178,6 +178,7 @@ class _LayerFn(torch.autograd.Function):
                                     st.view(p + "output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph,
                                     info.seed, op0 + 2)
         ctx.save_for_backward(x, key_bias, qkv, ctxv, lse, z1, m1, r1, h1, pre, act, z2, m2, r2)
+        ctx.bits = bits
         ctx.info, ctx.idx, ctx.ph, ctx.pa, ctx.scale = info, idx, ph, pa, scale
         return h2
 
@@ -217,7 +218,8 @@ class _LayerFn(torch.autograd.Function):
         if trainable:
             ops.linear_wgrad(da1, ctxv, G("attention.output.dense.weight"), None, acc)
         dctx = ops.linear_dgrad(da1, W("attention.output.dense.weight"))
-        dqkv = ops.attn_bwd(dctx, qkv, ctxv, lse, key_bias, B, L, nh, ctx.pa, info.seed, op0, ctx.scale)
+        dqkv = ops.attn_bwd(dctx, qkv, ctxv, lse, key_bias, ctx.bits, B, L, nh, ctx.pa, info.seed, op0, ctx.scale)
+        ctx.bits = None
         if trainable:
             ops.linear_wgrad(dqkv, x, G("qkv.weight"), G("qkv.bias"), acc)
             m._group_ready(grp)

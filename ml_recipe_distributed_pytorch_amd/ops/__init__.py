@@ -66,16 +66,19 @@ def gelu_bwd(dout, pre, g_bias, accumulate):
 
 # ------------------------------------------------------------------------------------- attention
 def attn_fwd(qkv, key_bias, B, L, nh, p, seed, opid, scale):
+    """Returns (ctx [T,H], lse [B,nh,L] fp32, keep-bits or None).  The HIP forward stores the dropout
+    keep-bits it drew so the backward never re-hashes; the CPU reference regenerates them."""
     if qkv.is_cuda:
-        return tuple(_k().attn_fwd(qkv, key_bias, int(B), int(L), int(nh), float(p), int(seed), int(opid),
-                                   float(scale)))
-    return ref.attn_fwd(qkv, key_bias, B, L, nh, p, seed, opid, scale)
+        ctx, lse, bits = _k().attn_fwd(qkv, key_bias, int(B), int(L), int(nh), float(p), int(seed), int(opid),
+                                       float(scale))
+        return ctx, lse, bits
+    ctx, lse = ref.attn_fwd(qkv, key_bias, B, L, nh, p, seed, opid, scale)
+    return ctx, lse, None
 
 
-def attn_bwd(dctx, qkv, ctx, lse, key_bias, B, L, nh, p, seed, opid, scale):
+def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale):
     if dctx.is_cuda:
-        return _k().attn_bwd(dctx, qkv, ctx, lse, key_bias, int(B), int(L), int(nh), float(p), int(seed),
-                             int(opid), float(scale))
+        return _k().attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, int(B), int(L), int(nh), float(p), float(scale))
     return ref.attn_bwd(dctx, qkv, ctx, lse, key_bias, B, L, nh, p, seed, opid, scale)
 
 
@@ -100,10 +103,30 @@ def linear_dgrad_add(dy, w, resid):
     return ref.linear_dgrad_add(dy, w, resid)
 
 
+def _wgrad_splits(T: int, N: int, K: int) -> int:
+    """Split-K factor for dW = dyᵀ·x (reduction over T tokens, output only N×K).  hipBLASLt runs these
+    long-K/small-MN GEMMs at 220-500 TF on MI355X (a 768×768 output is 9 tiles of 256² for 256 CUs);
+    a batched split over T restores occupancy (measured 410-880 TF, tools/gemm_bench.py)."""
+    tiles = max(1, (N * K) // (256 * 256))
+    s = 1
+    while s < 8 and tiles * s * 2 <= 220 and T % (s * 2) == 0 and T // (s * 2) >= 2048:
+        s *= 2
+    return s
+
+
 def linear_wgrad(dy, x, g_w, g_b, accumulate):
     """g_w (fp32 arena view) (+)= dyᵀ·x with fp32 GEMM output; g_b (+)= column sums of dy."""
     if dy.is_cuda:
-        if accumulate:
+        T, N = dy.shape
+        K = x.shape[1]
+        s = _wgrad_splits(T, N, K)
+        if s > 1:
+            part = torch.bmm(dy.view(s, T // s, N).transpose(1, 2), x.view(s, T // s, K), out_dtype=torch.float32)
+            if accumulate:
+                g_w.add_(part.sum(0))
+            else:
+                torch.sum(part, 0, out=g_w)
+        elif accumulate:
             g_w.add_(torch.mm(dy.t(), x, out_dtype=torch.float32))
         else:
             torch.mm(dy.t(), x, out_dtype=torch.float32, out=g_w)

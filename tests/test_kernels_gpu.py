@@ -111,17 +111,17 @@ def _attn_case(cuda, B, L, nh, p, masked):
         for b in range(B):
             kb[b, L - 1 - 7 * b:] = -10000.0
     scale = 1.0 / 8.0
-    ctx, lse = k.attn_fwd(qkv.to(cuda), kb.to(cuda), B, L, nh, p, 555, 3, scale)
+    ctx, lse, bits = k.attn_fwd(qkv.to(cuda), kb.to(cuda), B, L, nh, p, 555, 3, scale)
     ctxr, lser = ref.attn_fwd(qkv, kb, B, L, nh, p, 555, 3, scale)
     _close(lse, lser, 1e-2, 1e-3, "lse")
     _close(ctx, ctxr, 2e-2, 2e-2, "ctx")
     dctx = _bf(torch.randn(B * L, H))
-    dq = k.attn_bwd(dctx.to(cuda), qkv.to(cuda), ctx, lse, kb.to(cuda), B, L, nh, p, 555, 3, scale)
+    dq = k.attn_bwd(dctx.to(cuda), qkv.to(cuda), ctx, lse, kb.to(cuda), bits, B, L, nh, p, scale)
     dqr = ref.attn_bwd(dctx, qkv, ctx.cpu(), lse.cpu(), kb, B, L, nh, p, 555, 3, scale)
     _close(dq, dqr, 3e-2, 3e-2, "dqkv")
 
 
-@pytest.mark.parametrize("L", [384, 128, 100, 24])
+@pytest.mark.parametrize("L", [384, 512, 128, 100, 24, 7])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_attention(cuda, L, p):
     _attn_case(cuda, 2, L, 2, p, masked=True)

@@ -1,0 +1,3 @@
+set -o pipefail
+timeout -k 10 200 python tools/attn_bench.py 2>&1 | grep -v amdgpu.ids
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --batch 64 2>&1 | tail -1
