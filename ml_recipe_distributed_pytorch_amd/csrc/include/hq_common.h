@@ -15,14 +15,16 @@ typedef __attribute__((ext_vector_type(16))) float f32x16_t;  // 32x32 MFMA accu
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 
 // ------------------------------------------------------------------------------ bf16 helpers
+typedef __bf16 hq_bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float hq_f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float hq_bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
-__device__ __forceinline__ uint16_t hq_f2bf(float f) {
-  __hip_bfloat16 b = __float2bfloat16(f);   // RNE; hipcc emits v_cvt_pk_bf16_f32 on gfx950
-  return *reinterpret_cast<uint16_t*>(&b);
-}
+// RNE f32 -> bf16.  A vector convert of a PAIR lowers to ONE v_cvt_pk_bf16_f32 on gfx950 (NaN-safe);
+// converting the halves separately costs 4 instructions per pair.
 __device__ __forceinline__ uint32_t hq_pack2(float lo, float hi) {
-  return (uint32_t)hq_f2bf(lo) | ((uint32_t)hq_f2bf(hi) << 16);
+  hq_f32x2_t f = {lo, hi};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f, hq_bf16x2_t));
 }
+__device__ __forceinline__ uint16_t hq_f2bf(float f) { return (uint16_t)(hq_pack2(f, 0.f) & 0xFFFFu); }
 __device__ __forceinline__ void hq_unpack8(const uint4& v, float* f) {
   f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xFFFF0000u);
   f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xFFFF0000u);

@@ -36,8 +36,55 @@ __device__ __forceinline__ f32x16_t mfma32(const bf16x8_t& a, const bf16x8_t& b,
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// LDS images are [rows][64] bf16 (128-B rows) with the 16-B chunk index XOR-swizzled by
+//   f(row) = ((row>>1)&1)<<2 | ((row>>3)&3)
+// found by exhaustive search (tools/lds_swizzle_search.py) to make BOTH access patterns bank-conflict
+// free: ds_read_b128 row reads (16 rows of a lane group, one chunk) and ds_read_b64_tr_b16 reads
+// (4 rows × 64 B per 32-lane half).  Unswizzled the row reads are 8-way conflicted (T2).
+__device__ __forceinline__ int swz(int row) { return (((row >> 1) & 1) << 2) | ((row >> 3) & 3); }
+__device__ __forceinline__ int lds_off(int row, int col) {  // element offset of (row, col)
+  return row * D + ((((col >> 3) ^ swz(row)) << 3) | (col & 7));
+}
+
 __device__ __forceinline__ bf16x8_t lds_row8(const uint16_t* tile, int row, int col) {
-  return *reinterpret_cast<const bf16x8_t*>(tile + row * D + col);
+  return *reinterpret_cast<const bf16x8_t*>(tile + lds_off(row, col));
+}
+
+// swz(row) only depends on row bits 1..4, so every offset inside a 32-row subtile is a lane constant:
+// precompute them once (12 VGPRs) instead of re-deriving the XOR per access in VALU-bound loops.
+struct LdsOffsets {
+  int row[4];        // ds_read_b128 row reads: row (lane&31), chunk 16s + 8hh
+  int tr[2][2][2];   // ds_read_b64_tr_b16: [s][dblk][lo/hi]
+  __device__ __forceinline__ void init(int lane) {
+    const int hh = lane >> 5;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) row[s] = lds_off(lane & 31, 16 * s + 8 * hh);
+    const int g = lane >> 4, i = lane & 15;
+    const int th = g >> 1, dsub = g & 1;
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        const int r = 16 * s + 4 * th + (i >> 2);
+        const int c = d * 32 + 16 * dsub + 4 * (i & 3);
+        tr[s][d][0] = lds_off(r, c);
+        tr[s][d][1] = lds_off(r + 8, c);
+      }
+  }
+};
+
+__device__ __forceinline__ bf16x8_t row8(const uint16_t* tile, int row0, const LdsOffsets& o, int s) {
+  return *reinterpret_cast<const bf16x8_t*>(tile + row0 * D + o.row[s]);
+}
+
+__device__ __forceinline__ bf16x8_t tr8(const uint16_t* tile, int row0, const LdsOffsets& o, int s, int dblk) {
+  const uint16_t* t = tile + row0 * D;
+  const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(t + o.tr[s][dblk][0]));
+  const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(t + o.tr[s][dblk][1]));
+  bf16x8_t out;
+  out[0] = lo[0]; out[1] = lo[1]; out[2] = lo[2]; out[3] = lo[3];
+  out[4] = hi[0]; out[5] = hi[1]; out[6] = hi[2]; out[7] = hi[3];
+  return out;
 }
 
 // A operand "Xᵀ" of a 32x32x16 MFMA from a row-major [rows][64] LDS image: lane supplies
@@ -48,8 +95,8 @@ __device__ __forceinline__ bf16x8_t lds_tr8(const uint16_t* tile, int row0, int 
   const int hh = g >> 1, dsub = g & 1;
   const int r = row0 + 16 * s + 4 * hh + (i >> 2);
   const int c = dblk * 32 + 16 * dsub + 4 * (i & 3);
-  const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(tile + r * D + c));
-  const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(tile + (r + 8) * D + c));
+  const bf16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(tile + lds_off(r, c)));
+  const bf16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(tile + lds_off(r + 8, c)));
   bf16x8_t out;
   out[0] = lo[0]; out[1] = lo[1]; out[2] = lo[2]; out[3] = lo[3];
   out[4] = hi[0]; out[5] = hi[1]; out[6] = hi[2]; out[7] = hi[3];
@@ -85,12 +132,12 @@ __device__ __forceinline__ void load_head(uint16_t* dst, const uint16_t* src, si
 #pragma unroll
   for (int i = 0; i < kMax; ++i) {
     const int t = threadIdx.x + i * NT;
-    if (t < n) *reinterpret_cast<uint4*>(dst + (t >> 3) * D + (t & 7) * 8) = buf[i];
+    if (t < n) *reinterpret_cast<uint4*>(dst + lds_off(t >> 3, (t & 7) * 8)) = buf[i];
   }
 }
 
 // ============================================================================ forward
-template <int NWB>
+template <int NWB, bool DROP, bool EVEN>
 __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __restrict__ qkv,
                                                             const float* __restrict__ key_bias,
                                                             uint16_t* __restrict__ ctx, float* __restrict__ lse,
@@ -118,6 +165,8 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
   for (int t = threadIdx.x; t < Lp; t += NWB * 64) sB[t] = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -INFINITY;
   __syncthreads();
   if (qs * 32 >= L) return;
+  LdsOffsets lo_;
+  lo_.init(lane);
 
   f32x16_t o[2];
 #pragma unroll
@@ -126,15 +175,14 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
   const uint32_t row_idx = ((uint32_t)bh * L + (uint32_t)min(qi, L - 1)) * (uint32_t)L;
-  const bool pair_ok = ((L & 1) == 0);
-  uint16_t* my_bits = mbits ? mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane : nullptr;
+  uint16_t* my_bits = mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane;
 
   for (int kt = 0; kt < n32; ++kt) {
     f32x16_t acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma32(lds_row8(sK, kt * 32 + (lane & 31), 16 * s + 8 * hh), qf[s], acc);
+    for (int s = 0; s < 4; ++s) acc = mfma32(row8(sK, kt * 32, lo_, s), qf[s], acc);
     float sc[16];
     float mx = -INFINITY;
 #pragma unroll
@@ -150,7 +198,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     if (__any(mx > m_run)) {  // exact rescale skip: α = 1 for every lane whose max did not grow
       const float m_new = fmaxf(m_run, mx);
-      const float alpha = exp2f(m_run - m_new);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
       m_run = m_new;
       l_run *= alpha;
 #pragma unroll
@@ -161,17 +209,17 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
     float rs = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      sc[r] = exp2f(sc[r] - m_run);
+      sc[r] = __builtin_amdgcn_exp2f(sc[r] - m_run);
       rs += sc[r];
     }
     l_run += rs;
-    if (thr) {
+    if constexpr (DROP) {
       uint32_t bits = 0;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const uint32_t idx0 = row_idx + kt * 32 + 8 * g + 4 * hh;
         float mk[4];
-        if (pair_ok) {
+        if constexpr (EVEN) {
           hq_keep4(idx0, key, thr, kscale, mk);
         } else {
 #pragma unroll
@@ -183,13 +231,13 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
           bits |= (mk[i] != 0.f ? 1u : 0u) << (4 * g + i);
         }
       }
-      if (my_bits) my_bits[(size_t)kt * 64] = (uint16_t)bits;
+      my_bits[(size_t)kt * 64] = (uint16_t)bits;
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const bf16x8_t pb = pack_b(sc, s);
 #pragma unroll
-      for (int d = 0; d < 2; ++d) o[d] = mfma32(lds_tr8(sV, kt * 32, s, d, lane), pb, o[d]);
+      for (int d = 0; d < 2; ++d) o[d] = mfma32(tr8(sV, kt * 32, lo_, s, d), pb, o[d]);
     }
   }
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
@@ -203,12 +251,12 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
         float v4[4] = {o[d][4 * g] * inv, o[d][4 * g + 1] * inv, o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv};
         *reinterpret_cast<uint2*>(out + d * 32 + 8 * g + 4 * hh) = hq_pack4(v4);
       }
-    if (hh == 0) lse[(size_t)bh * L + qi] = (m_run + log2f(l_tot)) * LN2;
+    if (hh == 0) lse[(size_t)bh * L + qi] = (m_run + __builtin_amdgcn_logf(l_tot)) * LN2;  // v_log_f32 = log2
   }
 }
 
 // ============================================================================ backward: dQ (+ δ)
-template <int NWB>
+template <int NWB, bool DROP>
 __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv,
                                                                const uint16_t* __restrict__ dctx,
                                                                const uint16_t* __restrict__ ctx,
@@ -253,13 +301,15 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
   if (qok && hh == 0) delta[(size_t)bh * L + qi] = dlt;
   __syncthreads();
   if (qs * 32 >= L) return;
+  LdsOffsets lo_;
+  lo_.init(lane);
 
   f32x16_t dq[2];
 #pragma unroll
   for (int d = 0; d < 2; ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
-  const uint16_t* my_bits = mbits ? mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane : nullptr;
+  const uint16_t* my_bits = mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane;
 
   for (int kt = 0; kt < n32; ++kt) {
     f32x16_t s_acc, p_acc;
@@ -267,11 +317,15 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
     for (int r = 0; r < 16; ++r) { s_acc[r] = 0.f; p_acc[r] = 0.f; }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      s_acc = mfma32(lds_row8(sK, kt * 32 + (lane & 31), 16 * s + 8 * hh), qf[s], s_acc);
-      p_acc = mfma32(lds_row8(sV, kt * 32 + (lane & 31), 16 * s + 8 * hh), of[s], p_acc);
+      s_acc = mfma32(row8(sK, kt * 32, lo_, s), qf[s], s_acc);
+      p_acc = mfma32(row8(sV, kt * 32, lo_, s), of[s], p_acc);
     }
-    const uint32_t bits = my_bits ? (uint32_t)my_bits[(size_t)kt * 64] : 0xFFFFu;
-    const float ks = my_bits ? kscale : 1.f;
+    uint32_t bits = 0xFFFFu;
+    float ks = 1.f;
+    if constexpr (DROP) {
+      bits = (uint32_t)my_bits[(size_t)kt * 64];
+      ks = kscale;
+    }
     float ds[16];
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
@@ -280,7 +334,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int r = 4 * g + i;
-        const float P = exp2f(fmaf(s_acc[r], c_scale, bv[i]) - lq);
+        const float P = __builtin_amdgcn_exp2f(fmaf(s_acc[r], c_scale, bv[i]) - lq);
         const float mk = ((bits >> r) & 1u) ? ks : 0.f;
         ds[r] = P * fmaf(p_acc[r], mk, -dlt);
       }
@@ -289,7 +343,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
     for (int s = 0; s < 2; ++s) {
       const bf16x8_t sb = pack_b(ds, s);
 #pragma unroll
-      for (int d = 0; d < 2; ++d) dq[d] = mfma32(lds_tr8(sK, kt * 32, s, d, lane), sb, dq[d]);
+      for (int d = 0; d < 2; ++d) dq[d] = mfma32(tr8(sK, kt * 32, lo_, s, d), sb, dq[d]);
     }
   }
   if (qok) {
@@ -305,7 +359,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
 }
 
 // ============================================================================ backward: dK, dV
-template <int NWB>
+template <int NWB, bool DROP>
 __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv,
                                                                  const uint16_t* __restrict__ dctx,
                                                                  const float* __restrict__ lse,
@@ -343,73 +397,114 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
   }
   __syncthreads();
   if (ks_idx * 32 >= L) return;
+  LdsOffsets lo_;
+  lo_.init(lane);
 
-  f32x16_t dv[2], dk[2];
-#pragma unroll
-  for (int d = 0; d < 2; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { dv[d][r] = 0.f; dk[d][r] = 0.f; }
+  // Two passes over the queries (dV, then dK with S recomputed): +25 % MFMA, but the live set of a
+  // single pass (K/V fragments + dV/dK accumulators + S/dP tiles ≈ 200 VGPRs) spills at the 168-VGPR
+  // budget of 12 waves per workgroup.
   // forward bit layout: word of fwd-lane l' = q + 32·hh', bit r' with acc_row(r', hh') = key-in-subtile
   const int krel = lane & 31;
   const int hh_f = (krel >> 2) & 1;
   const int r_f = (krel & 3) + 4 * (krel >> 3);
+  const float ksc = DROP ? kscale : 1.f;
+  uint16_t* out = dqkv + ((size_t)b * L + min(kj, L - 1)) * ld + h * D;
 
-  for (int qt = 0; qt < n32; ++qt) {
-    f32x16_t s_acc, p_acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) { s_acc[r] = 0.f; p_acc[r] = 0.f; }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      s_acc = mfma32(lds_row8(sQ, qt * 32 + (lane & 31), 16 * s + 8 * hh), kf[s], s_acc);
-      p_acc = mfma32(lds_row8(sO, qt * 32 + (lane & 31), 16 * s + 8 * hh), vf[s], p_acc);
-    }
-    uint32_t word = 0xFFFFu;
-    float ksc = 1.f;
-    if (mbits) {
-      word = mbits[(((size_t)bh * n32 + qt) * n32 + ks_idx) * 64 + lane];
-      ksc = kscale;
-    }
-    float pd[16], ds[16];
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float4 l4 = *reinterpret_cast<const float4*>(sL + qt * 32 + 8 * g + 4 * hh);
-      const float4 d4 = *reinterpret_cast<const float4*>(sD + qt * 32 + 8 * g + 4 * hh);
-      const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
-      const float dl[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 4 * g + i;
-        const int qrel = acc_row(r, hh);
-        // bit (qrel, krel) lives in fwd lane qrel + 32·hh_f, bit r_f
-        const uint32_t w = mbits ? (uint32_t)__shfl((int)word, qrel + 32 * hh_f, 64) : 0xFFFFu;
-        const float mk = ((w >> r_f) & 1u) ? ksc : 0.f;
-        const float P = exp2f(fmaf(s_acc[r], c_scale, kb) - lv[i]);
-        pd[r] = P * mk;
-        ds[r] = P * fmaf(p_acc[r], mk, -dl[i]);
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8_t pb = pack_b(pd, s);
-      const bf16x8_t sb = pack_b(ds, s);
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {
-        dv[d] = mfma32(lds_tr8(sO, qt * 32, s, d, lane), pb, dv[d]);
-        dk[d] = mfma32(lds_tr8(sQ, qt * 32, s, d, lane), sb, dk[d]);
-      }
-    }
-  }
-  if (kok) {
-    uint16_t* out = dqkv + ((size_t)b * L + kj) * ld + h * D;
+  // ------------------------------------------------------------------ pass 1: dVᵀ += dOᵀ·Pd
+  {
+    f32x16_t dv[2];
 #pragma unroll
     for (int d = 0; d < 2; ++d)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float k4[4] = {dk[d][4 * g] * scale, dk[d][4 * g + 1] * scale, dk[d][4 * g + 2] * scale, dk[d][4 * g + 3] * scale};
-        float v4[4] = {dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]};
-        *reinterpret_cast<uint2*>(out + H + d * 32 + 8 * g + 4 * hh) = hq_pack4(k4);
-        *reinterpret_cast<uint2*>(out + 2 * H + d * 32 + 8 * g + 4 * hh) = hq_pack4(v4);
+      for (int r = 0; r < 16; ++r) dv[d][r] = 0.f;
+    for (int qt = 0; qt < n32; ++qt) {
+      f32x16_t s_acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s_acc[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) s_acc = mfma32(row8(sQ, qt * 32, lo_, s), kf[s], s_acc);
+      const uint32_t word = DROP ? (uint32_t)mbits[(((size_t)bh * n32 + qt) * n32 + ks_idx) * 64 + lane] : 0xFFFFu;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float pd[8];
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg) {
+          const int g = 2 * s + gg;
+          const float4 l4 = *reinterpret_cast<const float4*>(sL + qt * 32 + 8 * g + 4 * hh);
+          const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 4 * g + i;
+            const uint32_t w = DROP ? (uint32_t)__shfl((int)word, acc_row(r, hh) + 32 * hh_f, 64) : 0xFFFFu;
+            const float mk = ((w >> r_f) & 1u) ? ksc : 0.f;
+            pd[4 * gg + i] = __builtin_amdgcn_exp2f(fmaf(s_acc[r], c_scale, kb) - lv[i]) * mk;
+          }
+        }
+        const bf16x8_t pb = pack_b(pd, 0);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) dv[d] = mfma32(tr8(sO, qt * 32, lo_, s, d), pb, dv[d]);
       }
+    }
+    if (kok) {
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float v4[4] = {dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]};
+          *reinterpret_cast<uint2*>(out + 2 * H + d * 32 + 8 * g + 4 * hh) = hq_pack4(v4);
+        }
+    }
+  }
+  // ------------------------------------------------------------------ pass 2: dKᵀ += Qᵀ·dS
+  {
+    f32x16_t dk[2];
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dk[d][r] = 0.f;
+    for (int qt = 0; qt < n32; ++qt) {
+      f32x16_t s_acc, p_acc;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s_acc[r] = 0.f; p_acc[r] = 0.f; }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        s_acc = mfma32(row8(sQ, qt * 32, lo_, s), kf[s], s_acc);
+        p_acc = mfma32(row8(sO, qt * 32, lo_, s), vf[s], p_acc);
+      }
+      const uint32_t word = DROP ? (uint32_t)mbits[(((size_t)bh * n32 + qt) * n32 + ks_idx) * 64 + lane] : 0xFFFFu;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float ds[8];
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg) {
+          const int g = 2 * s + gg;
+          const float4 l4 = *reinterpret_cast<const float4*>(sL + qt * 32 + 8 * g + 4 * hh);
+          const float4 d4 = *reinterpret_cast<const float4*>(sD + qt * 32 + 8 * g + 4 * hh);
+          const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
+          const float dl[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 4 * g + i;
+            const uint32_t w = DROP ? (uint32_t)__shfl((int)word, acc_row(r, hh) + 32 * hh_f, 64) : 0xFFFFu;
+            const float mk = ((w >> r_f) & 1u) ? ksc : 0.f;
+            const float P = __builtin_amdgcn_exp2f(fmaf(s_acc[r], c_scale, kb) - lv[i]);
+            ds[4 * gg + i] = P * fmaf(p_acc[r], mk, -dl[i]);
+          }
+        }
+        const bf16x8_t sb = pack_b(ds, 0);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) dk[d] = mfma32(tr8(sQ, qt * 32, lo_, s, d), sb, dk[d]);
+      }
+    }
+    if (kok) {
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float k4[4] = {dk[d][4 * g] * scale, dk[d][4 * g + 1] * scale, dk[d][4 * g + 2] * scale, dk[d][4 * g + 3] * scale};
+          *reinterpret_cast<uint2*>(out + H + d * 32 + 8 * g + 4 * hh) = hq_pack4(k4);
+        }
+    }
   }
 }
 
@@ -458,11 +553,16 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
   const size_t lds = (size_t)Lp * D * 2 * 2 + Lp * sizeof(float);
   dispatch_waves<FwdTag>(nw, [&](auto c) {
     constexpr int NW = decltype(c)::value;
-    static bool attr = (hipFuncSetAttribute((const void*)attn_fwd_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            160 * 1024) == hipSuccess);
-    (void)attr;
-    hipLaunchKernelGGL(attn_fwd_kernel<NW>, dim3(B * nh, (n32 + NW - 1) / NW), dim3(NW * 64), lds, s, qkv, key_bias,
-                       ctx, lse, thr ? mbits : nullptr, L, nh, scale * LOG2E, key, thr, hq_keep_scale(thr));
+    auto launch = [&](auto kern) {
+      static bool attr =
+          (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess);
+      (void)attr;
+      hipLaunchKernelGGL(kern, dim3(B * nh, (n32 + NW - 1) / NW), dim3(NW * 64), lds, s, qkv, key_bias, ctx, lse,
+                         thr ? mbits : nullptr, L, nh, scale * LOG2E, key, thr, hq_keep_scale(thr));
+    };
+    if (!thr) launch(attn_fwd_kernel<NW, false, true>);
+    else if ((L & 1) == 0) launch(attn_fwd_kernel<NW, true, true>);
+    else launch(attn_fwd_kernel<NW, true, false>);
   });
 }
 
@@ -479,15 +579,18 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
   const size_t lds_kv = (size_t)Lp * D * 2 * 2 + 2 * Lp * sizeof(float);
   dispatch_waves<FwdTag>(nw, [&](auto c) {
     constexpr int NW = decltype(c)::value;
-    static bool attr = (hipFuncSetAttribute((const void*)attn_bwd_dq_kernel<NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                            160 * 1024) == hipSuccess) &&
-                       (hipFuncSetAttribute((const void*)attn_bwd_dkdv_kernel<NW>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess);
-    (void)attr;
     const dim3 grid(B * nh, (n32 + NW - 1) / NW);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<NW>, grid, dim3(NW * 64), lds_dq, s, qkv, dctx, ctx, lse, key_bias, bits, delta,
-                       dqkv, L, nh, scale * LOG2E, scale, ks);
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<NW>, grid, dim3(NW * 64), lds_kv, s, qkv, dctx, lse, delta, key_bias, bits,
-                       dqkv, L, nh, scale * LOG2E, scale, ks);
+    auto launch = [&](auto kdq, auto kkv) {
+      static bool attr =
+          (hipFuncSetAttribute((const void*)kdq, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess) &&
+          (hipFuncSetAttribute((const void*)kkv, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess);
+      (void)attr;
+      hipLaunchKernelGGL(kdq, grid, dim3(NW * 64), lds_dq, s, qkv, dctx, ctx, lse, key_bias, bits, delta, dqkv, L, nh,
+                         scale * LOG2E, scale, ks);
+      hipLaunchKernelGGL(kkv, grid, dim3(NW * 64), lds_kv, s, qkv, dctx, lse, delta, key_bias, bits, dqkv, L, nh,
+                         scale * LOG2E, scale, ks);
+    };
+    if (bits) launch(attn_bwd_dq_kernel<NW, true>, attn_bwd_dkdv_kernel<NW, true>);
+    else launch(attn_bwd_dq_kernel<NW, false>, attn_bwd_dkdv_kernel<NW, false>);
   });
 }
