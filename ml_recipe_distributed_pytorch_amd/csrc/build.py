@@ -48,9 +48,9 @@ def _headers() -> List[str]:
     return sorted(os.path.join(inc, f) for f in os.listdir(inc) if f.endswith(".h"))
 
 
-def _compile(src: str, flags: List[str], compiler: str, force: bool) -> str:
+def _compile(src: str, flags: List[str], compiler: str, force: bool, deps: List[str] = ()) -> str:
     os.makedirs(BUILD, exist_ok=True)
-    key = _digest([src] + _headers(), flags + [compiler])
+    key = _digest([src] + _headers() + list(deps), flags + [compiler])
     obj = os.path.join(BUILD, os.path.basename(src) + f".{key}.o")
     if force or not os.path.exists(obj):
         _sh([compiler] + flags + ["-c", src, "-o", obj + ".tmp"])
@@ -96,15 +96,27 @@ def build_kernels(jobs: int = 8, force: bool = False, verbose: bool = True) -> s
     return out
 
 
+def _unicode_tables() -> str:
+    gen_dir = os.path.join(BUILD, "gen")
+    os.makedirs(gen_dir, exist_ok=True)
+    out = os.path.join(gen_dir, "unicode_tables.inc")
+    if not os.path.exists(out):
+        _sh([sys.executable, os.path.join(HERE, "host", "gen_unicode.py"), out + ".tmp"])
+        os.replace(out + ".tmp", out)
+    return out
+
+
 def build_host(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
     import pybind11
     host_dir = os.path.join(HERE, "host")
+    tables = _unicode_tables()
     srcs = sorted(os.path.join(host_dir, f) for f in os.listdir(host_dir) if f.endswith(".cpp"))
-    flags = ["-O3", "-fPIC", "-std=c++17", "-pthread", "-I" + host_dir, "-I" + pybind11.get_include(),
-             "-I" + sysconfig.get_paths()["include"], "-fvisibility=hidden"]
+    flags = ["-O3", "-fPIC", "-std=c++17", "-pthread", "-I" + host_dir, "-I" + os.path.dirname(tables),
+             "-I" + pybind11.get_include(), "-I" + sysconfig.get_paths()["include"], "-fvisibility=hidden"]
     cxx = shutil.which("g++") or "c++"
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, flags, cxx, force), srcs))
+        objs = list(ex.map(lambda s: _compile(s, flags, cxx, force, [tables, os.path.join(host_dir, "hq_host.h")]),
+                           srcs))
     out = os.path.join(PKG, "_hq_host" + EXT)
     _sh([cxx, "-shared", "-pthread", "-o", out + ".tmp"] + objs)
     os.replace(out + ".tmp", out)
