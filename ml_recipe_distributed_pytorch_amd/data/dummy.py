@@ -120,3 +120,31 @@ def _refill(batch, sp: SpecialIds, q: int, seed: int, threads: int = 4):
     host().synth_dummy(ids.data_ptr(), tt.data_ptr(), mask.data_ptr(), B, L, q, sp.vocab_size, sp.pad_token_id,
                        sp.unk_token_id, sp.cls_token_id, sp.sep_token_id, sp.model_name == "bert", seed & 0xFFFFFFFFFFFF,
                        threads)
+
+
+class DummyChunkDataset:
+    """Validation-side dummy data (``validate --dummy_dataset``, fix of D12): every "document" expands
+    into ``n_chunks`` random windows shaped like ``ChunkDataset`` output (no NQ file or vocab needed)."""
+
+    def __init__(self, tokenizer=None, *args, max_seq_len: int = 384, max_question_len: int = 64,
+                 dataset_len: int = 1000, n_chunks: int = 3, special_ids: Optional[SpecialIds] = None, **kwargs):
+        self.max_seq_len, self.max_question_len = max_seq_len, max_question_len
+        self.dataset_len, self.n_chunks = dataset_len, n_chunks
+        self.sp = special_ids or (SpecialIds.from_tokenizer(tokenizer) if tokenizer is not None else SpecialIds())
+
+    def __len__(self):
+        return self.dataset_len
+
+    def __getitem__(self, idx):
+        from .items import ChunkItem
+        L, q = self.max_seq_len, self.max_question_len
+        ids = synth_ids(np.random.default_rng(int(idx)), self.n_chunks, L, q, self.sp)
+        doc_len = L - q - 3
+        items = []
+        for c in range(self.n_chunks):
+            items.append(ChunkItem(item_id=f"dummy-{idx}", input_ids=ids[c].tolist(), start_id=q + 2, end_id=L - 2,
+                                   label_id=0, true_text="", true_question="", true_label=0, true_start=c * doc_len,
+                                   true_end=c * doc_len + doc_len - 1, question_len=q, t2o=[],
+                                   chunk_start=c * doc_len, chunk_end=(c + 1) * doc_len,
+                                   start_position=(q + 2) / L, end_position=(L - 2) / L))
+        return items

@@ -20,6 +20,8 @@ class Tokenizer:
     def __init__(self, model_name: str, vocab_file: str, *, merges_file: Optional[str] = None, lowercase: bool = True,
                  handle_chinese_chars: bool = False, dropout: Optional[float] = None, legacy: bool = False,
                  seed: int = 0):
+        self._args = dict(model_name=model_name, vocab_file=vocab_file, merges_file=merges_file, lowercase=lowercase,
+                          handle_chinese_chars=handle_chinese_chars, dropout=dropout, legacy=legacy, seed=seed)
         self.model_name = model_name
         self.legacy = legacy
         if model_name == "bert":
@@ -34,6 +36,14 @@ class Tokenizer:
             self._tok = host().ByteLevelBPE(vocab_file, merges_file, float(dropout or 0.0), seed)
         else:
             raise NotImplementedError(f"Tokenizer initialization for model {model_name} is not implemented.")
+
+    def __getstate__(self):
+        # the native tokenizer is rebuilt from its files: picklable for spawn/Pool workers (the
+        # reference's validate swapped in the slow HF tokenizer for that reason, validate.py:38-40)
+        return self._args
+
+    def __setstate__(self, args):
+        self.__init__(**args)
 
     def __len__(self):
         return len(self._tok)

@@ -173,6 +173,8 @@ def get_trainer_parser() -> ArgumentParser:
                         help="Checkpoint for train_metrics evaluation (fix of D9).")
     parser.add_argument("--eval_shard", action="store_true",
                         help="Shard evaluation across ranks and all-reduce the metrics (default: rank-0 eval).")
+    parser.add_argument("--nproc_per_node", type=cast2(int), default=None,
+                        help="Processes per node (default: #visible GPUs, or 1 on CPU). On CPU >1 spawns gloo ranks.")
     return parser
 
 

@@ -1,0 +1,10 @@
+"""Drop-in shim for the reference CLI (`python modules/train_metrics.py -c <cfg> [--flags]`)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from ml_recipe_distributed_pytorch_amd.cli.train_metrics import cli  # noqa: E402
+
+if __name__ == "__main__":
+    cli()
