@@ -288,6 +288,9 @@ class BertForQuestionAnswering(nn.Module):
             raise RuntimeError("Cast the compute precision with --precision; master weights stay fp32.")
         self.store.to(probe.device)
         self.store.set_compute_dtype(self.compute_dtype_for(probe.device))
+        if probe.device.type == "cuda":
+            from ..ops.tuning import enable_tuned_gemms
+            enable_tuned_gemms()
         for mod in self.modules():
             for k, b in list(mod._buffers.items()):
                 if b is not None:

@@ -1,0 +1,87 @@
+"""Config surface: configargparse-compatible parsing, two-parser split, round trip."""
+import os
+
+import pytest
+
+from ml_recipe_distributed_pytorch_amd.utils import flags
+from ml_recipe_distributed_pytorch_amd.utils.cfgparse import ArgumentParser
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CFG = os.path.join(ROOT, "config", "test_bert.cfg")
+
+
+def _write(tmp_path, text, name="a.cfg"):
+    p = tmp_path / name
+    p.write_text(text)
+    return str(p)
+
+
+def test_config_file_basic(tmp_path):
+    p = ArgumentParser()
+    p.add_argument("-c", "--config_file", is_config_file=True)
+    p.add_argument("--lr", type=float, default=1.0)
+    p.add_argument("--name", type=str, default="x")
+    p.add_argument("--flag", action="store_true")
+    p.add_argument("--off", action="store_true")
+    p.add_argument("--none", type=flags.cast2(int), default=3)
+    path = _write(tmp_path, "# comment\nlr = 0.5\nname=abc  # trailing\nflag=True\noff = False\nnone=None\n")
+    a = p.parse_args(["-c", path])
+    assert a.lr == 0.5 and a.name == "abc" and a.flag is True and a.off is False and a.none is None
+
+
+def test_cli_overrides_config(tmp_path):
+    p = ArgumentParser()
+    p.add_argument("-c", "--config_file", is_config_file=True)
+    p.add_argument("--lr", type=float, default=1.0)
+    path = _write(tmp_path, "lr = 0.5\n")
+    assert p.parse_args(["-c", path, "--lr", "2"]).lr == 2.0
+    assert p.parse_args(["--lr", "3", "-c", path]).lr == 3.0
+    assert p.parse_args(["-c", path]).lr == 0.5
+
+
+def test_unknown_keys_surface(tmp_path):
+    p = ArgumentParser()
+    p.add_argument("-c", "--config_file", is_config_file=True)
+    p.add_argument("--lr", type=float, default=1.0)
+    path = _write(tmp_path, "lr = 0.5\nmystery = 7\n")
+    a, unknown = p.parse_known_args(["-c", path])
+    assert a.lr == 0.5 and "--mystery=7" in unknown
+
+
+def test_reference_config_two_parsers():
+    (tp, mp), (params, model_params) = flags.get_params((flags.get_trainer_parser, flags.get_model_parser),
+                                                        ["-c", CFG])
+    assert model_params.model == "bert-base-uncased" and model_params.lowercase is True
+    assert model_params.merges_file is None
+    assert params.dummy_dataset and params.debug and params.apex_level == "O1"
+    assert params.train_batch_size == 256 and params.loss == "smooth" and params.smooth_alpha == 0.01
+    assert params.best_order == ">" and params.last is None and params.seed is None
+    assert str(params.dump_dir) == "results"
+
+
+def test_get_params_rejects_unknown_everywhere(tmp_path):
+    path = _write(tmp_path, open(CFG).read() + "\nnot_a_flag = 1\n")
+    with pytest.raises(SystemExit):
+        flags.get_params((flags.get_trainer_parser, flags.get_model_parser), ["-c", path])
+
+
+def test_write_and_reload_config(tmp_path):
+    (tp, mp), (params, model_params) = flags.get_params((flags.get_trainer_parser, flags.get_model_parser),
+                                                        ["-c", CFG, "--lr", "3e-5"])
+    out = tmp_path / "trainer.cfg"
+    flags.write_config_file(tp, params, out)
+    text = out.read_text()
+    assert "lr = 3e-05" in text and "config_file" not in text
+    _, again = flags.load_config_file(flags.get_trainer_parser, str(out))
+    for k in ("lr", "train_batch_size", "loss", "dummy_dataset", "apex_level", "warmup_coef", "best_order"):
+        assert getattr(again, k) == getattr(params, k), k
+    mo = tmp_path / "model.cfg"
+    flags.write_config_file(mp, model_params, mo)
+    _, m2 = flags.load_config_file(flags.get_model_parser, str(mo))
+    assert m2.model == model_params.model and m2.hidden_dropout_prob == model_params.hidden_dropout_prob
+
+
+def test_predictor_parser_validate_cfg():
+    path = os.path.join(ROOT, "config", "validate.cfg")
+    _, (p, m) = flags.get_params((flags.get_predictor_parser, flags.get_model_parser), ["-c", path])
+    assert p.limit == 100 and p.split_by_sentence and p.truncate and p.max_seq_len == 512
