@@ -97,6 +97,23 @@ __device__ __forceinline__ void block_partials(float (&acc)[NQ][NCH][4], float* 
   }
 }
 
+// Rows of one wave are software-pipelined: the next row's dy/dy2/z loads are in flight while the
+// current row is reduced and stored (the kernel is HBM-latency bound at 3 waves/SIMD otherwise).
+template <int NCH>
+__device__ __forceinline__ void ln_bwd_load(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dy2,
+                                            const uint16_t* __restrict__ z, size_t base, int lane, int H,
+                                            uint2 (&vdy)[NCH], uint2 (&vdy2)[NCH], uint2 (&vz)[NCH]) {
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    if (col < H) {
+      vdy[c] = *reinterpret_cast<const uint2*>(dy + base + col);
+      vdy2[c] = dy2 ? *reinterpret_cast<const uint2*>(dy2 + base + col) : make_uint2(0u, 0u);
+      vz[c] = *reinterpret_cast<const uint2*>(z + base + col);
+    }
+  }
+}
+
 template <int NCH>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dy2,
                                                      const uint16_t* __restrict__ z, const float* __restrict__ gamma,
@@ -120,57 +137,73 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
     float4 g = col < H ? *reinterpret_cast<const float4*>(gamma + col) : make_float4(0.f, 0.f, 0.f, 0.f);
     gam[c][0] = g.x; gam[c][1] = g.y; gam[c][2] = g.z; gam[c][3] = g.w;
   }
-  const int row0 = blockIdx.x * kWaves * kRowsPerWave;
+  const int row0 = blockIdx.x * kWaves * kRowsPerWave + wave;
+  uint2 cdy[NCH], cdy2[NCH], cz[NCH];
+  float cmu = 0.f, crs = 0.f;
+  if (row0 < T) {
+    ln_bwd_load<NCH>(dy, dy2, z, (size_t)row0 * H, lane, H, cdy, cdy2, cz);
+    cmu = mean[row0];
+    crs = rstd[row0];
+  }
+#pragma unroll
   for (int r = 0; r < kRowsPerWave; ++r) {
-    const int row = row0 + r * kWaves + wave;
-    if (row >= T) break;
-    const size_t base = (size_t)row * H;
-    const float mu = mean[row], rs = rstd[row];
-    float g[NCH][4], xh[NCH][4];
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int col = c * 256 + lane * 4;
-      if (col < H) {
-        float fz[4];
-        hq_unpack4(*reinterpret_cast<const uint2*>(dy + base + col), g[c]);
-        if (dy2) {
-          float f2[4];
-          hq_unpack4(*reinterpret_cast<const uint2*>(dy2 + base + col), f2);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) g[c][i] += f2[i];
-        }
-        hq_unpack4(*reinterpret_cast<const uint2*>(z + base + col), fz);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          xh[c][i] = (fz[i] - mu) * rs;
-          acc[0][c][i] += g[c][i] * xh[c][i];
-          acc[1][c][i] += g[c][i];
-          const float dxh = g[c][i] * gam[c][i];
-          s1 += dxh;
-          s2 += dxh * xh[c][i];
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { g[c][i] = 0.f; xh[c][i] = 0.f; }
+    const int row = row0 + r * kWaves;
+    if (row < T) {
+      const size_t base = (size_t)row * H;
+      uint2 ndy[NCH], ndy2[NCH], nz[NCH];
+      float nmu = 0.f, nrs = 0.f;
+      const int nrow = row + kWaves;
+      if (r + 1 < kRowsPerWave && nrow < T) {
+        ln_bwd_load<NCH>(dy, dy2, z, (size_t)nrow * H, lane, H, ndy, ndy2, nz);
+        nmu = mean[nrow];
+        nrs = rstd[nrow];
       }
-    }
-    s1 = hq_wave_sum(s1) / H;
-    s2 = hq_wave_sum(s2) / H;
+      float g[NCH][4], xh[NCH][4];
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int col = c * 256 + lane * 4;
-      if (col < H) {
-        float dz[4], m[4] = {1.f, 1.f, 1.f, 1.f};
+      for (int c = 0; c < NCH; ++c) {
+        const int col = c * 256 + lane * 4;
+        if (col < H) {
+          float fz[4], f2[4];
+          hq_unpack4(cdy[c], g[c]);
+          hq_unpack4(cdy2[c], f2);
+          hq_unpack4(cz[c], fz);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) dz[i] = rs * (g[c][i] * gam[c][i] - s1 - xh[c][i] * s2);
-        *reinterpret_cast<uint2*>(dz_out + base + col) = hq_pack4(dz);
-        if (thr) hq_keep4((uint32_t)(base + col), key, thr, kscale, m);
-        float da[4];
+          for (int i = 0; i < 4; ++i) {
+            g[c][i] += f2[i];
+            xh[c][i] = (fz[i] - cmu) * crs;
+            acc[0][c][i] += g[c][i] * xh[c][i];
+            acc[1][c][i] += g[c][i];
+            const float dxh = g[c][i] * gam[c][i];
+            s1 += dxh;
+            s2 += dxh * xh[c][i];
+          }
+        } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { da[i] = dz[i] * m[i]; acc[2][c][i] += da[i]; }
-        *reinterpret_cast<uint2*>(da_out + base + col) = hq_pack4(da);
+          for (int i = 0; i < 4; ++i) { g[c][i] = 0.f; xh[c][i] = 0.f; }
+        }
       }
+      s1 = hq_wave_sum(s1) / H;
+      s2 = hq_wave_sum(s2) / H;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int col = c * 256 + lane * 4;
+        if (col < H) {
+          float dz[4], m[4] = {1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dz[i] = crs * (g[c][i] * gam[c][i] - s1 - xh[c][i] * s2);
+          *reinterpret_cast<uint2*>(dz_out + base + col) = hq_pack4(dz);
+          if (thr) hq_keep4((uint32_t)(base + col), key, thr, kscale, m);
+          float da[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) { da[i] = dz[i] * m[i]; acc[2][c][i] += da[i]; }
+          *reinterpret_cast<uint2*>(da_out + base + col) = hq_pack4(da);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) { cdy[c] = ndy[c]; cdy2[c] = ndy2[c]; cz[c] = nz[c]; }
+      cmu = nmu;
+      crs = nrs;
     }
   }
   block_partials<NCH, 3>(acc, lds, part, H);

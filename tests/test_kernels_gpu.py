@@ -155,3 +155,26 @@ def test_adamw_and_norm(cuda):
     _close(md, master, 1e-6, 1e-5, "master")
     _close(mmd, m, 1e-7, 1e-5, "exp_avg")
     _close(comp, master, 1e-2, 1e-2, "bf16 copy")
+
+
+@pytest.mark.gpu
+def test_native_rccl_reducer_single_rank(cuda):
+    """RCCL communicator bootstrap + allreduce(avg) fp32/bf16 + broadcast on the comm stream (world 1)."""
+    k = _native.kernels()
+    red = k.Reducer(0, 1, bytes(k.rccl_unique_id()), cuda.index)
+    x = torch.randn(1 << 20, device=cuda)
+    ref_x = x.clone()
+    stream = torch.cuda.current_stream().cuda_stream
+    red.allreduce_f32(x.data_ptr(), x.numel(), stream)
+    red.wait(stream)
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref_x)
+    scratch = torch.empty(x.numel(), dtype=torch.bfloat16, device=cuda)
+    red.allreduce_bf16(x.data_ptr(), scratch.data_ptr(), x.numel(), stream)
+    red.wait(stream)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(x, ref_x.bfloat16().float())
+    red.broadcast(x.data_ptr(), x.numel(), 0, 0, stream)
+    red.wait(stream)
+    red.synchronize()
+    assert red.world == 1 and red.rank == 0
