@@ -40,6 +40,8 @@ def enable_tuned_gemms(mode: str | None = None) -> bool:
         out = os.environ.get("HQ_TUNABLEOP_FILE")
         if out:
             tunable.set_filename(out)
+            import atexit
+            atexit.register(tunable.write_file)
     ok = False
     if os.path.exists(SHIPPED):
         try:

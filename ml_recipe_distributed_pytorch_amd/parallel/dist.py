@@ -67,6 +67,8 @@ def init_distributed(backend: str, *, init_method: Optional[str] = None, world_s
         device = torch.device("cuda", local_rank)   # local index (reference D3 used the global rank)
     else:
         device = torch.device("cpu")
+    # surface RCCL failures as exceptions instead of hangs
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if not dist.is_initialized():
         kw = dict(backend=backend, init_method=init_method, world_size=world_size, rank=rank,
                   timeout=datetime.timedelta(seconds=timeout_s))

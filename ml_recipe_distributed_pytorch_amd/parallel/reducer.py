@@ -61,6 +61,7 @@ class GradReducer:
         self._native = None
         self._scratch = None
         self.stats = {"buckets_launched": 0, "bytes": 0}
+        self._seq_hash = 0       # running hash of the (bucket, numel) launch sequence (SURVEY §5.2 checker)
         on_gpu = self.store.device.type == "cuda"
         backend = dist.get_backend(group) if dist.is_initialized() else None
         if native is None:
@@ -145,6 +146,8 @@ class GradReducer:
         b.launched = True
         view = self.store.grad[b.start:b.end]
         self.stats["buckets_launched"] += 1
+        self.stats["bytes"] += b.numel * (2 if self.allreduce_dtype == "bf16" else 4)
+        self._seq_hash = (self._seq_hash * 1_000_003 + b.index * 65_537 + b.numel) & 0x7FFFFFFFFFFFFFFF
         if self._native is not None:
             stream = torch.cuda.current_stream().cuda_stream
             if self.allreduce_dtype == "bf16":
@@ -174,6 +177,24 @@ class GradReducer:
                     if scale is not None:
                         self.store.grad[b.start:b.end].mul_(scale)
         self.active = False
+
+    def verify_sequence(self):
+        """Collective-sequence checker: every rank must have issued the same bucket all-reduces in the
+        same order (a divergence is exactly what deadlocks or silently corrupts RCCL/gloo).  The hashes
+        travel through the rendezvous TCPStore, not a collective, so a diverged collective stream
+        cannot mask the check.  Called by the trainer at epoch end; raises on mismatch."""
+        if self.world <= 1:
+            return True
+        store = dist.distributed_c10d._get_default_store()
+        self._verify_calls = getattr(self, "_verify_calls", 0) + 1
+        prefix = f"hq_seq/{self._verify_calls}/"
+        store.set(prefix + str(self.rank), f"{self._seq_hash}:{self.stats['buckets_launched']}")
+        keys = [prefix + str(r) for r in range(self.world)]
+        store.wait(keys)
+        vals = [store.get(k).decode() for k in keys]
+        if len(set(vals)) != 1:
+            raise RuntimeError(f"gradient collective sequence diverged across ranks: {vals}")
+        return True
 
     def close(self):
         if self._native is not None:

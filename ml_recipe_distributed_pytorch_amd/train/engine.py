@@ -33,6 +33,43 @@ def to_device(data, device, non_blocking=True):
     return data
 
 
+class PhaseTimer:
+    """Per-phase step timer.  On GPU it records HIP events on the compute stream (no per-phase
+    synchronisation; ``resolve`` waits for the last event once per step, profiling runs only);
+    on CPU it reads the wall clock.  Phases repeated across micro-batches are summed."""
+
+    def __init__(self, enabled: bool, device):
+        self.enabled = enabled
+        self.cuda = torch.device(device).type == "cuda"
+        self.marks: List = []
+
+    def reset(self):
+        self.marks = []
+
+    def mark(self, name: str = "start"):
+        if not self.enabled:
+            return
+        if self.cuda:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self.marks.append((name, ev))
+        else:
+            self.marks.append((name, time.perf_counter()))
+
+    def resolve(self) -> Dict[str, float]:
+        if not self.enabled or len(self.marks) < 2:
+            return {}
+        if self.cuda:
+            self.marks[-1][1].synchronize()
+        out: Dict[str, float] = {}
+        for (_, a), (name, b) in zip(self.marks, self.marks[1:]):
+            if name == "start":
+                continue
+            ms = a.elapsed_time(b) if self.cuda else (b - a) * 1e3
+            out[name + "_ms"] = out.get(name + "_ms", 0.0) + ms
+        return out
+
+
 @dataclass
 class StepResult:
     losses: LossRecord
@@ -54,53 +91,46 @@ class TrainEngine:
         self.no_sync_accum = no_sync_accum
         self.profile = profile
         self.micro = 0
+        self._timer = PhaseTimer(profile, model.store.device)
 
     @property
     def device(self):
         return self.model.store.device
 
-    def _sync(self):
-        if self.profile and self.device.type == "cuda":
-            torch.cuda.synchronize()
-
     def micro_step(self, inputs, labels) -> Optional[StepResult]:
         """Forward+backward of one micro-batch; runs the optimizer on the accumulation boundary."""
-        t = {}
-        t0 = time.perf_counter()
+        timer = self._timer
+        if self.micro % self.batch_split == 0:
+            timer.reset()
+        timer.mark()
         boundary = (self.micro + 1) % self.batch_split == 0
         if self.reducer is not None:
             self.reducer.prepare(sync=boundary or not self.no_sync_accum)
         preds = self.model(**inputs)
         loss = self.loss_fn(preds, labels)
-        self._sync()
-        t1 = time.perf_counter()
+        timer.mark("fwd")
         (loss / self.batch_split).backward()
         if self.reducer is not None and not boundary and not self.no_sync_accum:
             self.reducer.finalize()
-        self._sync()
-        t2 = time.perf_counter()
+        timer.mark("bwd")
         self.micro += 1
-        t["fwd_ms"], t["bwd_ms"] = (t1 - t0) * 1e3, (t2 - t1) * 1e3
         if not boundary:
             return None
-        return self._apply(t)
+        return self._apply()
 
-    def _apply(self, t) -> StepResult:
-        t2 = time.perf_counter()
+    def _apply(self) -> StepResult:
+        timer = self._timer
         if self.reducer is not None:
             self.reducer.finalize()
-        self._sync()
-        t3 = time.perf_counter()
+        timer.mark("comm_wait")
         norm, coef = grad_norm_and_clip(self.model.store, self.max_grad_norm)
         lr = self.optimizer.param_groups[0]["lr"]
         self.optimizer.step(clip_coef=coef)
         self.optimizer.zero_grad()
         if self.scheduler is not None:
             self.scheduler.step()
-        self._sync()
-        t4 = time.perf_counter()
-        t["comm_wait_ms"], t["optim_ms"] = (t3 - t2) * 1e3, (t4 - t3) * 1e3
-        return StepResult(losses=self.loss_fn.last, grad_norm=norm, lr=lr, timings=t)
+        timer.mark("optim")
+        return StepResult(losses=self.loss_fn.last, grad_norm=norm, lr=lr, timings=timer.resolve())
 
     def step(self, micro_batches) -> StepResult:
         res = None

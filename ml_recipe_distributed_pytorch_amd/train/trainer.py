@@ -227,6 +227,8 @@ class Trainer:
         for epoch_i in range(self.start_epoch, self.n_epochs + 1):
             self.epoch = epoch_i
             self._train(epoch_i)
+            if self.reducer is not None:
+                self.reducer.verify_sequence()
             for func in after_epoch_funcs:
                 func(epoch_i)
 

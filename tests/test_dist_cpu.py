@@ -104,3 +104,29 @@ def test_bucket_layout_follows_backward_order():
         assert e0 == s1
     # first bucket (lowest offsets) holds the heads, which are ready first in backward
     assert "head" in buckets[0].groups
+
+
+def _seq_worker(rank, world, port, out_dir):
+    _setup(rank, world, port)
+    from ml_recipe_distributed_pytorch_amd.parallel import dist as hqdist
+    from ml_recipe_distributed_pytorch_amd.parallel.reducer import GradReducer
+    model, _, _ = _build(seed=0)
+    red = GradReducer(model, bucket_cap_mb=0.05)
+    red.prepare(True)
+    red.finalize()                    # every bucket, same order on both ranks
+    first = red.verify_sequence()
+    if rank == 1:                     # simulate a rank whose backward issued a different bucket sequence
+        red._seq_hash ^= 0x5A5A
+    try:
+        second = red.verify_sequence()
+    except RuntimeError:
+        second = False
+    torch.save(torch.tensor([first, second]), os.path.join(out_dir, f"seq{rank}.pt"))
+    hqdist.destroy()
+
+
+def test_collective_sequence_checker_detects_divergence(tmp_path):
+    mp.spawn(_seq_worker, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        first, second = torch.load(tmp_path / f"seq{r}.pt", weights_only=True).tolist()
+        assert first and not second
