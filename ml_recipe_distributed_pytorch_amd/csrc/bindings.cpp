@@ -124,6 +124,65 @@ std::vector<Tensor> ln_bwd(Tensor dy, c10::optional<Tensor> dy2, Tensor z, Tenso
 }
 
 // ------------------------------------------------------------------------------------------ GELU
+// ------------------------------------------------------------------------------------ MFMA GEMM
+// C[M,N] = A[M,K] · B[N,K]^T with epilogue `epi` (HQ_EPI_*).  bias f32[N] (BIAS/GELU); pre bf16[M,N]
+// (GELU: written, DGELU: read); resid bf16[M,N] (RESID); part f32[M/256, N] (DGELU column partials).
+int64_t gemm_nt_supported(int64_t M, int64_t N, int64_t K) { return hq_gemm_nt_supported((int)M, (int)N, (int)K); }
+
+Tensor gemm_nt(Tensor A, Tensor B, int64_t epi, c10::optional<Tensor> bias, c10::optional<Tensor> pre,
+               c10::optional<Tensor> resid, c10::optional<Tensor> part, c10::optional<Tensor> out) {
+  check(A, BF16, "A"); check(B, BF16, "B");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_nt: A[M,K], B[N,K] expected");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(M < (1ll << 31) / 4 && N * K < (1ll << 31) && M * N < (1ll << 40), "gemm_nt: shape too large");
+  const int bn = hq_gemm_nt_supported((int)M, (int)N, (int)K);
+  TORCH_CHECK(bn > 0, "gemm_nt: unsupported shape M=", M, " N=", N, " K=", K, " (need M%256, N%128, K%64 == 0)");
+  TORCH_CHECK(epi >= HQ_EPI_NONE && epi <= HQ_EPI_RESID, "gemm_nt: bad epilogue");
+  c10::DeviceGuard g(A.device());
+  Tensor C = (out.has_value() && out->defined()) ? *out : at::empty({M, N}, A.options());
+  check(C, BF16, "out");
+  TORCH_CHECK(C.size(0) == M && C.size(1) == N, "gemm_nt: out shape");
+  if (epi == HQ_EPI_BIAS || epi == HQ_EPI_GELU) {
+    TORCH_CHECK(bias.has_value() && bias->defined(), "gemm_nt: bias required");
+    check(*bias, F32, "bias");
+    TORCH_CHECK(bias->numel() == N, "gemm_nt: bias length");
+  }
+  if (epi == HQ_EPI_GELU || epi == HQ_EPI_DGELU) {
+    TORCH_CHECK(pre.has_value() && pre->defined(), "gemm_nt: pre required");
+    check(*pre, BF16, "pre");
+    TORCH_CHECK(pre->size(0) == M && pre->size(1) == N, "gemm_nt: pre shape");
+  }
+  if (epi == HQ_EPI_RESID) {
+    TORCH_CHECK(resid.has_value() && resid->defined(), "gemm_nt: resid required");
+    check(*resid, BF16, "resid");
+    TORCH_CHECK(resid->size(0) == M && resid->size(1) == N, "gemm_nt: resid shape");
+  }
+  if (epi == HQ_EPI_DGELU) {
+    TORCH_CHECK(part.has_value() && part->defined(), "gemm_nt: part required");
+    check(*part, F32, "part");
+    TORCH_CHECK(part->numel() == (M / 256) * N, "gemm_nt: part must hold [M/256, N]");
+  }
+  hq_gemm_nt(ptr<uint16_t>(A), ptr<uint16_t>(B), ptr<uint16_t>(C), optr<float>(bias), optr<uint16_t>(pre),
+             optr<uint16_t>(resid), optr<float>(part), (int)M, (int)N, (int)K, (int)K, (int)K, (int)N, (int)epi, bn,
+             cur_stream());
+  return C;
+}
+
+void transpose_tiles(Tensor src, Tensor dst, Tensor tiles) {
+  check(src, BF16, "src"); check(dst, BF16, "dst");
+  TORCH_CHECK(tiles.device().is_cuda() && tiles.scalar_type() == at::kInt && tiles.is_contiguous() && tiles.dim() == 2 &&
+              tiles.size(1) == 6, "tiles must be a contiguous int32 [n,6] GPU tensor");
+  c10::DeviceGuard g(src.device());
+  hq_transpose_tiles(ptr<uint16_t>(src), ptr<uint16_t>(dst), ptr<int>(tiles), (int)tiles.size(0), cur_stream());
+}
+
+void colsum_into(Tensor part, Tensor out, bool accumulate) {
+  check(part, F32, "part"); check(out, F32, "out");
+  TORCH_CHECK(part.dim() == 2 && part.size(1) == out.numel(), "colsum_into: part [P,N] / out [N]");
+  c10::DeviceGuard g(part.device());
+  hq_colsum(ptr<float>(part), (int)part.size(0), (int)part.size(1), ptr<float>(out), accumulate, cur_stream());
+}
+
 Tensor gelu_fwd(Tensor pre) {
   check(pre, BF16, "pre");
   TORCH_CHECK(pre.numel() % 8 == 0, "numel must be a multiple of 8");
@@ -266,6 +325,12 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
   m.def("gelu_fwd", &gelu_fwd);
+  m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("epi"), py::arg("bias") = py::none(),
+        py::arg("pre") = py::none(), py::arg("resid") = py::none(), py::arg("part") = py::none(),
+        py::arg("out") = py::none());
+  m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("transpose_tiles", &transpose_tiles);
+  m.def("colsum_into", &colsum_into);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("bias_grad", &bias_grad);
   m.def("attn_fwd", &attn_fwd);

@@ -61,3 +61,17 @@ void hq_adamod(float* master, uint16_t* compute, const float* grad, float* m, fl
                const float* clip_coef, hipStream_t s);
 void hq_cast_f32_bf16(const float* src, uint16_t* dst, int64_t n, float scale, hipStream_t s);
 void hq_cast_bf16_f32(const uint16_t* src, float* dst, int64_t n, float scale, hipStream_t s);
+
+// ------------------------------------------------------------------ MFMA GEMM (gemm.hip)
+enum { HQ_EPI_NONE = 0, HQ_EPI_BIAS = 1, HQ_EPI_GELU = 2, HQ_EPI_DGELU = 3, HQ_EPI_RESID = 4 };
+// returns the block N-width the kernel will use for this shape (256 / 128), 0 = unsupported
+int hq_gemm_nt_supported(int M, int N, int K);
+// C[M,N] = A[M,K]·B[N,K]^T (+epilogue); P = GELU pre-activation (out for EPI_GELU, in for EPI_DGELU);
+// R = residual (EPI_RESID); part = [M/256][N] column partial sums (EPI_DGELU)
+void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,
+                float* part, int M, int N, int K, int lda, int ldb, int ldc, int epi, int bn, hipStream_t s);
+
+// tiles: int32 [ntiles][6] = (src_off, dst_off, rows, cols, r0, c0); src [rows][cols] -> dst [cols][rows]
+void hq_transpose_tiles(const uint16_t* src, uint16_t* dst, const int* tiles, int ntiles, hipStream_t s);
+// out[c] (+)= sum_p part[p][c], part f32 [P][N]
+void hq_colsum(const float* part, int P, int N, float* out, bool accumulate, hipStream_t s);

@@ -1,0 +1,304 @@
+// bf16 "NT" GEMM for gfx950 with fused epilogues:  C[M,N] = A[M,K] · B[N,K]ᵀ  (+ epilogue)
+//
+// Both operands are K-contiguous row-major — the layout of every BERT projection in the forward
+// (x · Wᵀ) and, with the transposed bf16 weight copy kept by the ParamStore, of every dgrad
+// (dy · W = dy · (Wᵀ)ᵀ).  Epilogues fuse what used to be separate HBM passes:
+//   EPI_NONE   C = acc
+//   EPI_BIAS   C = acc + bias[n]
+//   EPI_GELU   P = acc + bias[n] (stored, needed by backward),  C = gelu_erf(P)
+//   EPI_DGELU  C = acc · gelu'(P[m,n])  and per-block column sums of C (the bias gradient of the
+//              producing Linear) into part[M/BM][N]  — replaces the separate gelu_bwd pass
+//   EPI_RESID  C = acc + R[m,n]  (residual-gradient add of dgrad)
+//
+// Structure (CDNA4 playbook §5):
+// * 256×BN block tile, BK = 64, 512 threads = 8 waves as 2 (M) × 4 (N); a wave owns 128 × BN/4.
+// * Operands reach LDS by LDS-DMA (global_load_lds, 16 B per lane): the image is lane-linear, so the
+//   bank-conflict XOR swizzle is applied to the per-lane global SOURCE address and undone on the
+//   ds_read_b128 fragment read (rule 21).  Rows are 128 B; slot' = slot ^ ((row >> 1) & 7) makes the
+//   16-lane fragment reads of 16 rows hit all 64 banks once.
+// * Double-buffered ring: tile t+1 is issued before tile t is consumed; a COUNTED s_waitcnt vmcnt
+//   (never 0 inside the loop) retires tile t, then a raw s_barrier (no __syncthreads: its fence would
+//   drain the DMA in flight).  One __shared__ array for everything (trap 4a).
+// * mfma_f32_16x16x32_bf16 with the operands SWAPPED (B fragment as the MFMA's A input) so the
+//   accumulator holds Cᵀ: each lane owns 4 consecutive n of one m → 8-byte row-contiguous stores,
+//   a float4 of bias per lane, and the column (bias-grad) sums reduce over lanes.
+// * XCD-aware bijective block remap: each XCD walks a contiguous range of tiles in M-major order,
+//   so the tiles that share an A row-panel share that XCD's L2.
+#include "hq_common.h"
+#include "hq_kernels.h"
+
+namespace {
+
+constexpr int BM = 256;
+constexpr int BK = 64;
+constexpr int kThreads = 512;
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) void g_void;
+
+__device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  return cdf + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
+// Issue the LDS-DMA of one [ROWS × 64] bf16 panel (rows of 128 B) into lds (+ byte offset).
+// Each wave-instruction moves 8 rows (64 lanes × 16 B); this wave handles `n_instr` of them
+// starting at panel row `row0`.
+template <int N_INSTR>
+__device__ __forceinline__ void stage_panel(const uint16_t* __restrict__ g, int ld, int row0, int k0, char* lds_base,
+                                            int lane) {
+  const int r_in = lane >> 3;          // 0..7 row within the 8-row piece
+  const int slot = lane & 7;           // 16-B slot in the 128-B LDS row (lane-linear destination)
+#pragma unroll
+  for (int i = 0; i < N_INSTR; ++i) {
+    const int row = row0 + i * 8 + r_in;
+    const int src_slot = slot ^ ((row >> 1) & 7);
+    const uint16_t* src = g + (size_t)row * ld + k0 + src_slot * 8;
+    char* dst = lds_base + (size_t)(row0 + i * 8) * 128;  // wave-uniform; lane L lands at dst + 16 L
+    __builtin_amdgcn_global_load_lds((g_void*)src, (lds_void*)dst, 16, 0, 0);
+  }
+}
+
+// 16-B fragment read of LDS row `row`, k-slot `slot` (8 bf16 = 16 B), undoing the source swizzle.
+__device__ __forceinline__ bf16x8_t frag(const char* panel, int row, int slot) {
+  const int off = row * 128 + ((slot ^ ((row >> 1) & 7)) << 4);
+  return *reinterpret_cast<const bf16x8_t*>(panel + off);
+}
+
+template <int EPI, int BN>
+__global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                                                              uint16_t* __restrict__ C, const float* __restrict__ bias,
+                                                              uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
+                                                              float* __restrict__ part, int M, int N, int K, int lda,
+                                                              int ldb, int ldc) {
+  constexpr int WN = BN / 4;            // columns per wave
+  constexpr int NJ = WN / 16;           // 16-wide n subtiles per wave
+  constexpr int MI = 8;                 // 16-high m subtiles per wave (128 rows)
+  constexpr int A_BYTES = BM * 128;     // one A panel (256 × 64 bf16)
+  constexpr int B_BYTES = BN * 128;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // ---- bijective XCD remap of the linear block id, then M-major tile order within an XCD
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tiles_n = N / BN;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const uint16_t* Ab = A + (size_t)m0 * lda;
+  const uint16_t* Bb = B + (size_t)n0 * ldb;
+  const int nt = K / BK;
+
+  // staging split: A panel = 32 pieces of 8 rows (4 per wave); B panel = BN/8 pieces (BN/64 per wave)
+  constexpr int A_INSTR = BM / 8 / 8;
+  constexpr int B_INSTR = BN / 8 / 8;
+  constexpr int LOADS_PER_TILE = A_INSTR + B_INSTR;
+
+  f32x4_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int t, int buf) {
+    char* base = smem + buf * STAGE;
+    stage_panel<A_INSTR>(Ab, lda, wave * (BM / 8), t * BK, base, lane);
+    stage_panel<B_INSTR>(Bb, ldb, wave * (BN / 8), t * BK, base + A_BYTES, lane);
+  };
+
+  const int fr = lane & 15;           // fragment row within a 16-row subtile
+  const int fq = lane >> 4;           // k-slot quarter (8 bf16 each) within a 32-wide k step
+  bf16x8_t bf[NJ], af[MI];
+  auto read_frags = [&](int t, int ks) {   // R phase: this wave's fragments of k-step ks of tile t
+    const char* pa = smem + (t & 1) * STAGE;
+    const char* pb = pa + A_BYTES;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bf[j] = frag(pb, wn * WN + j * 16 + fr, ks * 4 + fq);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) af[i] = frag(pa, wm * 128 + i * 16 + fr, ks * 4 + fq);
+  };
+  auto mfma_block = [&]() {               // M phase
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = []() { __builtin_amdgcn_s_barrier(); };
+  auto drain = []() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
+
+  // Two wave groups (wm = 0: waves 0-3, wm = 1: waves 4-7; a SIMD hosts one wave of each) run the
+  // same R/M phase sequence offset by one workgroup barrier, so on every SIMD one wave reads its
+  // LDS fragments while the other issues MFMAs.  Group 1 starts with an extra barrier, group 0 ends
+  // with one.  Barrier k of group 0 pairs with barrier k of group 1 (one phase later in its program):
+  //   RAW: every wave drains its LDS-DMA of tile t before the barrier that precedes the first read of
+  //   tile t by either group; WAR: a tile-(t+1) DMA into buffer (t+1)&1 is issued only after the
+  //   barrier that follows the other group's last read of tile t-1.
+  stage(0, 0);
+  drain();
+  bar();
+  if (__builtin_amdgcn_readfirstlane(wm) == 0) {
+    for (int t = 0; t < nt; ++t) {
+      if (t + 1 < nt) stage(t + 1, (t + 1) & 1);
+      read_frags(t, 0);
+      bar();
+      mfma_block();
+      bar();
+      read_frags(t, 1);
+      bar();
+      mfma_block();
+      drain();
+      bar();
+    }
+    bar();
+  } else {
+    bar();
+    for (int t = 0; t < nt; ++t) {
+      if (t + 1 < nt) stage(t + 1, (t + 1) & 1);
+      read_frags(t, 0);
+      bar();
+      mfma_block();
+      bar();
+      read_frags(t, 1);
+      drain();
+      bar();
+      mfma_block();
+      bar();
+    }
+  }
+  (void)LOADS_PER_TILE;
+
+  // ---- epilogue, phase 1: acc (+bias) -> bf16 into this wave's private LDS region [128][WN]
+  // (row stride WN*2+16 B keeps the 16-row ds_write_b64 groups at most 2-way and rows 16-B aligned).
+  // The last loop barrier guarantees every wave is done reading the A/B panels.
+  constexpr int RS = WN * 2 + 16;
+  char* wreg = smem + wave * (128 * RS);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int nl = j * 16 + fq * 4;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU) bv = *reinterpret_cast<const float4*>(bias + n0 + wn * WN + nl);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      float v[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
+      *reinterpret_cast<uint2*>(wreg + (i * 16 + fr) * RS + nl * 2) = hq_pack4(v);
+    }
+  }
+  // ---- phase 2: row-coalesced 16-B pieces (8 columns) -> epilogue math -> 16-B global stores
+  constexpr int SEGS = WN / 8;                  // 16-B pieces per row of the wave tile
+  constexpr int ROWS_PER_IT = 64 / SEGS;
+  const int seg = lane % SEGS, rsub = lane / SEGS;
+  const int mb = m0 + wm * 128, nb = n0 + wn * WN + seg * 8;
+  float csum[8];
+  if constexpr (EPI == HQ_EPI_DGELU) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+  }
+#pragma unroll 4
+  for (int it = 0; it < 128 / ROWS_PER_IT; ++it) {
+    const int row = it * ROWS_PER_IT + rsub;
+    uint4 piece = *reinterpret_cast<const uint4*>(wreg + row * RS + seg * 16);
+    const size_t goff = (size_t)(mb + row) * ldc + nb;
+    if constexpr (EPI == HQ_EPI_GELU) {
+      *reinterpret_cast<uint4*>(P + goff) = piece;   // pre-activation (bf16), kept for backward
+      float x[8];
+      hq_unpack8(piece, x);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = gelu_erf(x[e]);
+      piece = hq_pack8(x);
+    } else if constexpr (EPI == HQ_EPI_DGELU) {
+      float d[8], pr[8];
+      hq_unpack8(piece, d);
+      hq_unpack8(*reinterpret_cast<const uint4*>(P + goff), pr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { d[e] *= gelu_grad(pr[e]); csum[e] += d[e]; }
+      piece = hq_pack8(d);
+    } else if constexpr (EPI == HQ_EPI_RESID) {
+      float d[8], rr[8];
+      hq_unpack8(piece, d);
+      hq_unpack8(*reinterpret_cast<const uint4*>(R + goff), rr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] += rr[e];
+      piece = hq_pack8(d);
+    }
+    *reinterpret_cast<uint4*>(C + goff) = piece;
+  }
+  if constexpr (EPI == HQ_EPI_DGELU) {
+    // column sums: lanes with equal `seg` hold the same 8 columns -> xor-reduce over rsub, then the
+    // two M-waves through LDS (after everyone is done with its staging region)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      for (int o = SEGS; o < 64; o <<= 1) csum[e] += __shfl_xor(csum[e], o, 64);
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [2][BN]
+    if (rsub == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wm * BN + wn * WN + seg * 8 + e] = csum[e];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += kThreads) part[(size_t)tm * N + n0 + c] = red[c] + red[BN + c];
+  }
+}
+
+constexpr size_t epi_lds(int bn) {
+  const size_t stage = 2 * (size_t)(BM * 128 + bn * 128);
+  const size_t epi = 8 * 128 * (size_t)(bn / 4 * 2 + 16);
+  return stage > epi ? stage : epi;
+}
+
+template <int EPI>
+void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,
+                float* part, int M, int N, int K, int lda, int ldb, int ldc, int bn, hipStream_t s) {
+  const int grid = (M / BM) * (N / bn);
+  if (bn == 256) {
+    constexpr size_t lds = epi_lds(256);
+    static bool init = [] {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      return true;
+    }();
+    (void)init;
+    hipLaunchKernelGGL((gemm_nt_kernel<EPI, 256>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, R, part, M, N, K,
+                       lda, ldb, ldc);
+  } else {
+    constexpr size_t lds = epi_lds(128);
+    static bool init = [] {
+      (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      return true;
+    }();
+    (void)init;
+    hipLaunchKernelGGL((gemm_nt_kernel<EPI, 128>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, R, part, M, N, K,
+                       lda, ldb, ldc);
+  }
+}
+
+}  // namespace
+
+int hq_gemm_nt_supported(int M, int N, int K) {
+  if (M % BM || K % BK || K < BK) return 0;
+  if (N % 256 == 0) return 256;
+  if (N % 128 == 0) return 128;
+  return 0;
+}
+
+void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,
+                float* part, int M, int N, int K, int lda, int ldb, int ldc, int epi, int bn, hipStream_t s) {
+  switch (epi) {
+    case HQ_EPI_NONE: launch_epi<HQ_EPI_NONE>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
+    case HQ_EPI_BIAS: launch_epi<HQ_EPI_BIAS>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
+    case HQ_EPI_GELU: launch_epi<HQ_EPI_GELU>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
+    case HQ_EPI_DGELU: launch_epi<HQ_EPI_DGELU>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
+    case HQ_EPI_RESID: launch_epi<HQ_EPI_RESID>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
+  }
+}

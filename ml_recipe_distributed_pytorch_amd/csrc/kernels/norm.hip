@@ -537,3 +537,7 @@ void hq_bias_grad(const uint16_t* dy, float* part, HqOuts outs, int T, int N, bo
   hipLaunchKernelGGL(colpart_kernel, dim3((N + 2047) / 2048, nb), dim3(256), 0, s, dy, part, T, N);
   colsum(part, nb, N, outs, N, accumulate, s);
 }
+
+void hq_colsum(const float* part, int P, int N, float* out, bool accumulate, hipStream_t s) {
+  colsum(part, P, N, HqOuts{{out, nullptr, nullptr, nullptr}}, N, accumulate, s);
+}

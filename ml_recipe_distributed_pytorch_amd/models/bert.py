@@ -165,15 +165,18 @@ class _LayerFn(torch.autograd.Function):
         pa = cfg.attention_probs_dropout_prob if info.training else 0.0
         scale = 1.0 / math.sqrt(cfg.head_dim)
         op0 = 1 + 3 * idx
-        qkv = ops.linear_fwd(x, st.view(p + "qkv.weight"), st.view(p + "qkv.bias"))
+        Bm = lambda k: st.view(p + k, "master")  # noqa: E731  (fp32 bias for the MFMA epilogue)
+        qkv = ops.linear_fwd(x, st.view(p + "qkv.weight"), st.view(p + "qkv.bias"), Bm("qkv.bias"))
         ctxv, lse, bits = ops.attn_fwd(qkv, key_bias, B, L, nh, pa, info.seed, op0, scale)
-        a1 = ops.linear_fwd(ctxv, st.view(p + "attention.output.dense.weight"), st.view(p + "attention.output.dense.bias"))
+        a1 = ops.linear_fwd(ctxv, st.view(p + "attention.output.dense.weight"), st.view(p + "attention.output.dense.bias"),
+                            Bm("attention.output.dense.bias"))
         h1, z1, m1, r1 = ops.ln_fwd(a1, x, st.view(p + "attention.output.LayerNorm.weight", "master"),
                                     st.view(p + "attention.output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph,
                                     info.seed, op0 + 1)
-        pre = ops.linear_fwd(h1, st.view(p + "intermediate.dense.weight"), st.view(p + "intermediate.dense.bias"))
-        act = ops.gelu_fwd(pre)
-        a2 = ops.linear_fwd(act, st.view(p + "output.dense.weight"), st.view(p + "output.dense.bias"))
+        pre, act = ops.linear_gelu_fwd(h1, st.view(p + "intermediate.dense.weight"),
+                                       st.view(p + "intermediate.dense.bias"), Bm("intermediate.dense.bias"))
+        a2 = ops.linear_fwd(act, st.view(p + "output.dense.weight"), st.view(p + "output.dense.bias"),
+                            Bm("output.dense.bias"))
         h2, z2, m2, r2 = ops.ln_fwd(a2, h1, st.view(p + "output.LayerNorm.weight", "master"),
                                     st.view(p + "output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph,
                                     info.seed, op0 + 2)
@@ -198,6 +201,7 @@ class _LayerFn(torch.autograd.Function):
         acc = m._take_accumulate(grp) if trainable else False
         G = (lambda k: st.view(p + k, "grad")) if trainable else (lambda k: None)
         W = lambda k: st.view(p + k)  # noqa: E731
+        WT = lambda k: st.view_t(p + k)  # noqa: E731  (Wᵀ working copy, GPU only)
         Wm = lambda k: st.view(p + k, "master")  # noqa: E731
         dh2 = dh2.contiguous()
 
@@ -206,24 +210,24 @@ class _LayerFn(torch.autograd.Function):
                               G("output.LayerNorm.weight"), G("output.LayerNorm.bias"), G("output.dense.bias"), acc)
         if trainable:
             ops.linear_wgrad(da2, act, G("output.dense.weight"), None, acc)
-        dact = ops.linear_dgrad(da2, W("output.dense.weight"))
-        dpre = ops.gelu_bwd(dact, pre, G("intermediate.dense.bias"), acc)
+        dpre = ops.linear_dgrad_gelu(da2, W("output.dense.weight"), pre, G("intermediate.dense.bias"), acc,
+                                     wt=WT("output.dense.weight"))
         if trainable:
             ops.linear_wgrad(dpre, h1, G("intermediate.dense.weight"), None, acc)
-        dh1_ffn = ops.linear_dgrad(dpre, W("intermediate.dense.weight"))
+        dh1_ffn = ops.linear_dgrad(dpre, W("intermediate.dense.weight"), wt=WT("intermediate.dense.weight"))
         # --- attention block ------------------------------------------------------------------
         dz1, da1 = ops.ln_bwd(dz2, dh1_ffn, z1, Wm("attention.output.LayerNorm.weight"), m1, r1, ctx.ph, info.seed,
                               op0 + 1, G("attention.output.LayerNorm.weight"), G("attention.output.LayerNorm.bias"),
                               G("attention.output.dense.bias"), acc)
         if trainable:
             ops.linear_wgrad(da1, ctxv, G("attention.output.dense.weight"), None, acc)
-        dctx = ops.linear_dgrad(da1, W("attention.output.dense.weight"))
+        dctx = ops.linear_dgrad(da1, W("attention.output.dense.weight"), wt=WT("attention.output.dense.weight"))
         dqkv = ops.attn_bwd(dctx, qkv, ctxv, lse, key_bias, ctx.bits, B, L, nh, ctx.pa, info.seed, op0, ctx.scale)
         ctx.bits = None
         if trainable:
             ops.linear_wgrad(dqkv, x, G("qkv.weight"), G("qkv.bias"), acc)
             m._group_ready(grp)
-        dx = ops.linear_dgrad_add(dqkv, W("qkv.weight"), dz1)
+        dx = ops.linear_dgrad_add(dqkv, W("qkv.weight"), dz1, wt=WT("qkv.weight"))
         return dx, None, None, None, None
 
 
@@ -248,6 +252,9 @@ class BertForQuestionAnswering(nn.Module):
         gen = torch.Generator().manual_seed(seed) if seed is not None else None
         self.store = ParamStore(build_entries(config))
         _init_store(self.store, config, gen)
+        self.store.enable_transposed([f"transformer.encoder.layer.{i}.{k}" for i in range(config.num_hidden_layers)
+                                      for k in ("qkv.weight", "attention.output.dense.weight",
+                                                "intermediate.dense.weight", "output.dense.weight")])
         order = hf_param_order(config)
         assert sorted(order) == sorted(self.store.params), "param layout / HF order mismatch"
         for name in order:

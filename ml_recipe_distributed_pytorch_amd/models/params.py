@@ -64,6 +64,12 @@ class ParamStore:
         self.compute_dtype = torch.float32
         self.params: Dict[str, nn.Parameter] = {}
         self._dirty = True
+        # transposed bf16 working copies (Wᵀ) of selected 2-D weights, for NT-layout dgrad GEMMs
+        self._t_keys: List[str] = []
+        self._t_off: Dict[str, int] = {}
+        self.compute_t: Optional[torch.Tensor] = None
+        self._t_tiles: Optional[torch.Tensor] = None
+        self._t_dirty = True
 
     # ------------------------------------------------------------------ allocation
     def allocate(self, device, init_std: float, generator: Optional[torch.Generator] = None):
@@ -108,6 +114,52 @@ class ParamStore:
             self.compute = torch.empty(self.total, dtype=dtype, device=self.master.device)
             self.compute.copy_(self.master)
         self._dirty = False
+        self._t_dirty = True
+        self.compute_t = None
+        self._t_tiles = None
+
+    # ------------------------------------------------------------------ transposed copies
+    def enable_transposed(self, keys: Sequence[str]):
+        """Keep Wᵀ (bf16, [in, out] contiguous) for these 2-D entries on GPU, refreshed lazily after
+        every change of the working copy (optimizer step, load, sync)."""
+        self._t_keys = [k for k in keys if len(self.by_key[k].shape) == 2]
+        off = 0
+        for k in self._t_keys:
+            self._t_off[k] = off
+            off += (self.by_key[k].numel + _ALIGN - 1) // _ALIGN * _ALIGN
+        self._t_total = off
+        self._t_dirty = True
+
+    def _transposable(self) -> bool:
+        return (bool(self._t_keys) and self.compute is not None and self.compute.is_cuda
+                and self.compute.dtype == torch.bfloat16)
+
+    def refresh_transposed(self):
+        from .._native import kernels
+        if self.compute_t is None:
+            self.compute_t = torch.empty(self._t_total, dtype=torch.bfloat16, device=self.compute.device)
+        if self._t_tiles is None:
+            rows = []
+            for k in self._t_keys:
+                e = self.by_key[k]
+                R, Cc = e.shape
+                assert R % 64 == 0 and Cc % 64 == 0, f"{k}: transposed copy needs 64-multiples, got {e.shape}"
+                for r0 in range(0, R, 64):
+                    for c0 in range(0, Cc, 64):
+                        rows.append([e.offset, self._t_off[k], R, Cc, r0, c0])
+            self._t_tiles = torch.tensor(rows, dtype=torch.int32).to(self.compute.device)
+        kernels().transpose_tiles(self.compute, self.compute_t, self._t_tiles)
+        self._t_dirty = False
+
+    def view_t(self, key: str) -> Optional[torch.Tensor]:
+        """Wᵀ of a registered weight, or None when unavailable (CPU / fp32 / not registered)."""
+        if key not in self._t_off or not self._transposable():
+            return None
+        if self._t_dirty:
+            self.refresh_transposed()
+        e = self.by_key[key]
+        o = self._t_off[key]
+        return self.compute_t[o:o + e.numel].view(e.shape[1], e.shape[0])
 
     def to(self, device):
         device = torch.device(device)
@@ -136,10 +188,13 @@ class ParamStore:
         """Refresh the bf16 working copy after host-side edits of master (load, init)."""
         if self._dirty and self.compute is not None and self.compute.data_ptr() != self.master.data_ptr():
             self.compute.copy_(self.master)
+            self._t_dirty = True
         self._dirty = False
 
     def mark_clean(self):
+        """The optimizer rewrote master AND the working copy."""
         self._dirty = False
+        self._t_dirty = True
 
     # ------------------------------------------------------------------ layout queries
     def segments(self, names: Optional[Iterable[str]] = None) -> List[Tuple[int, int, str]]:

@@ -6,6 +6,7 @@
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -83,24 +84,68 @@ def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale
 
 
 # --------------------------------------------------------------------------------------- linear
-def linear_fwd(x, w, b):
-    """y = x·Wᵀ + b — hipBLASLt GEMM with its bias epilogue on GPU."""
+# Which projection GEMMs run on the hand-written MFMA kernel (gemm.hip) instead of hipBLASLt:
+#   HQ_GEMM=blas   none;  fused (default)  the ones whose epilogue fuses an elementwise pass
+#   (FFN1 + GELU, FFN2-dgrad + dGELU + bias-grad);  mfma  every supported shape.
+_EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID = range(5)
+_GEMM_MODE = os.environ.get("HQ_GEMM", "fused").lower()
+
+
+def _mfma(M: int, N: int, K: int, fused: bool) -> bool:
+    if _GEMM_MODE == "blas" or (_GEMM_MODE == "fused" and not fused):
+        return False
+    return _k().gemm_nt_supported(int(M), int(N), int(K)) > 0
+
+
+def linear_fwd(x, w, b, b32=None):
+    """y = x·Wᵀ + b.  GPU: hipBLASLt (bias epilogue) or the MFMA NT kernel (fp32 ``b32`` bias)."""
     if x.is_cuda:
+        if b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1], False):
+            return _k().gemm_nt(x, w, _EPI_BIAS, bias=b32)
         return torch.addmm(b, x, w.t()) if b is not None else torch.mm(x, w.t())
     return ref.linear_fwd(x, w, b)
 
 
-def linear_dgrad(dy, w):
+def linear_gelu_fwd(x, w, b, b32=None):
+    """(pre, act) with pre = x·Wᵀ + b, act = gelu(pre).  GPU: one MFMA GEMM with the GELU epilogue
+    (pre stored for the backward) when the shape allows, else GEMM + gelu kernel."""
+    if x.is_cuda and b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1], True):
+        pre = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+        act = _k().gemm_nt(x, w, _EPI_GELU, bias=b32, pre=pre)
+        return pre, act
+    pre = linear_fwd(x, w, b, b32)
+    return pre, gelu_fwd(pre)
+
+
+def linear_dgrad(dy, w, wt=None):
+    """dy·W.  ``wt`` = Wᵀ working copy (ParamStore.view_t) enables the NT MFMA kernel."""
     if dy.is_cuda:
+        if wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1], False):
+            return _k().gemm_nt(dy, wt, _EPI_NONE)
         return torch.mm(dy, w)
     return ref.linear_dgrad(dy, w)
 
 
-def linear_dgrad_add(dy, w, resid):
-    """resid + dy·W (hipBLASLt beta=1 accumulate; fuses the residual-gradient add)."""
+def linear_dgrad_add(dy, w, resid, wt=None):
+    """resid + dy·W (fuses the residual-gradient add)."""
     if dy.is_cuda:
+        if wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1], False):
+            return _k().gemm_nt(dy, wt, _EPI_RESID, resid=resid)
         return torch.addmm(resid, dy, w)
     return ref.linear_dgrad_add(dy, w, resid)
+
+
+def linear_dgrad_gelu(dy, w, pre, g_bias, accumulate, wt=None):
+    """dpre = (dy·W) ⊙ gelu'(pre) and g_bias (+)= Σ_rows dpre — the dgrad of the layer after GELU
+    fused with the GELU backward and the bias gradient of the layer before it."""
+    if dy.is_cuda and wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1], True):
+        M, N = dy.shape[0], w.shape[1]
+        part = torch.empty(M // 256, N, dtype=torch.float32, device=dy.device)
+        dpre = _k().gemm_nt(dy, wt, _EPI_DGELU, pre=pre, part=part)
+        if g_bias is not None:
+            _k().colsum_into(part, g_bias, bool(accumulate))
+        return dpre
+    return gelu_bwd(linear_dgrad(dy, w, wt), pre, g_bias, accumulate)
 
 
 def _wgrad_splits(T: int, N: int, K: int) -> int:

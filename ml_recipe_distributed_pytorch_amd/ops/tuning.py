@@ -23,6 +23,19 @@ SHIPPED = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 _DONE = False
 
 
+def _dump_results(path: str):
+    """Backup of the tuned table in TunableOp's CSV format (torch also writes its own file at exit)."""
+    from torch.cuda import tunable
+    try:
+        with open(path, "w") as f:
+            for k, v in tunable.get_validators():
+                f.write(f"Validator,{k},{v}\n")
+            for row in tunable.get_results():
+                f.write(",".join(str(x) for x in row) + "\n")
+    except Exception as e:  # pragma: no cover
+        logger.warning(f"could not dump TunableOp results: {e}")
+
+
 def enable_tuned_gemms(mode: str | None = None) -> bool:
     """Idempotently switch TunableOp on for this process. Returns True if shipped results were loaded."""
     global _DONE
@@ -41,7 +54,7 @@ def enable_tuned_gemms(mode: str | None = None) -> bool:
         if out:
             tunable.set_filename(out)
             import atexit
-            atexit.register(tunable.write_file)
+            atexit.register(_dump_results, out + ".dump.csv")
     ok = False
     if os.path.exists(SHIPPED):
         try:

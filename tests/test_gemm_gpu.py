@@ -1,0 +1,76 @@
+"""MFMA NT GEMM (gemm.hip) vs an fp32 torch reference, every epilogue."""
+import pytest
+import torch
+
+from ml_recipe_distributed_pytorch_amd import _native
+
+EPI_NONE, EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID = range(5)
+SHAPES = [(256, 256, 64), (512, 384, 192), (1024, 768, 768), (768, 2304, 128), (512, 128, 3072)]
+
+
+def _ref(A, B):
+    return A.float() @ B.float().t()
+
+
+def _close(got, exp, tol=2e-2):
+    err = (got.float() - exp).abs().max().item()
+    scale = exp.abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err} vs scale {scale}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_gemm_nt_plain_and_bias(cuda, M, N, K):
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(M + N + K)
+    A = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+    B = torch.randn(N, K, device=cuda, generator=g).bfloat16()
+    bias = torch.randn(N, device=cuda, generator=g)
+    assert k.gemm_nt_supported(M, N, K) in (128, 256)
+    _close(k.gemm_nt(A, B, EPI_NONE), _ref(A, B))
+    _close(k.gemm_nt(A, B, EPI_BIAS, bias=bias), _ref(A, B) + bias)
+
+
+@pytest.mark.gpu
+def test_gemm_nt_asymmetric_layout(cuda):
+    """A = I (padded) with an asymmetric B: catches a transposed C write."""
+    k = _native.kernels()
+    M, N, K = 256, 256, 256
+    A = torch.eye(M, K, device=cuda).bfloat16()
+    B = (torch.arange(N * K, device=cuda).reshape(N, K) % 251).float().bfloat16()
+    C = k.gemm_nt(A, B, EPI_NONE)
+    assert torch.equal(C.float(), B.float().t()[:M, :N].contiguous())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(512, 768, 256), (256, 3072, 768)])
+def test_gemm_nt_gelu_dgelu_resid(cuda, M, N, K):
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(7)
+    A = (torch.randn(M, K, device=cuda, generator=g) * 0.5).bfloat16()
+    B = (torch.randn(N, K, device=cuda, generator=g) * 0.1).bfloat16()
+    bias = torch.randn(N, device=cuda, generator=g) * 0.1
+    pre = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    act = k.gemm_nt(A, B, EPI_GELU, bias=bias, pre=pre)
+    ref_pre = _ref(A, B) + bias
+    _close(pre, ref_pre)
+    _close(act, torch.nn.functional.gelu(pre.float()))
+    # dgelu: C = (A·Bᵀ) * gelu'(pre), part = column sums per 256-row block
+    part = torch.empty(M // 256, N, device=cuda)
+    d = k.gemm_nt(A, B, EPI_DGELU, pre=pre, part=part)
+    x = pre.float().requires_grad_(True)
+    torch.nn.functional.gelu(x).backward(_ref(A, B).bfloat16().float())
+    _close(d, x.grad)
+    torch.testing.assert_close(part.sum(0), d.float().sum(0), atol=5e-2 * (1 + d.float().abs().sum(0).max().item() / M), rtol=2e-2)
+    resid = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+    _close(k.gemm_nt(A, B, EPI_RESID, resid=resid), _ref(A, B) + resid.float())
+
+
+@pytest.mark.gpu
+def test_gemm_nt_rejects_bad_shapes(cuda):
+    k = _native.kernels()
+    A = torch.randn(100, 64, device=cuda).bfloat16()
+    B = torch.randn(128, 64, device=cuda).bfloat16()
+    assert k.gemm_nt_supported(100, 128, 64) == 0
+    with pytest.raises(RuntimeError):
+        k.gemm_nt(A, B, EPI_NONE)
