@@ -40,11 +40,8 @@ __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-__device__ __forceinline__ float gelu_grad(float x) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  return cdf + x * 0.3989422804014327f * __expf(-0.5f * x * x);
-}
+__device__ __forceinline__ float gelu_erf(float x) { return hq_gelu(x); }
+__device__ __forceinline__ float gelu_grad(float x) { return hq_gelu_grad(x); }
 
 // Issue the LDS-DMA of one [ROWS × 64] bf16 panel (rows of 128 B) into lds (+ byte offset).
 // Each wave-instruction moves 8 rows (64 lanes × 16 B); this wave handles `n_instr` of them

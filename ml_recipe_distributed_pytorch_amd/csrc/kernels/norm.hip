@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const uint16_t* __restric
     float x[8], o[8];
     hq_unpack8(reinterpret_cast<const uint4*>(pre)[i], x);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = 0.5f * x[k] * (1.f + erff(x[k] * 0.70710678118654752f));
+    for (int k = 0; k < 8; ++k) o[k] = hq_gelu(x[k]);
     reinterpret_cast<uint4*>(out)[i] = hq_pack8(o);
   }
 }
@@ -380,8 +380,8 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const uint16_t* __restric
       hq_unpack8(*reinterpret_cast<const uint4*>(pre + off), x);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        const float cdf = 0.5f * (1.f + erff(x[k] * 0.70710678118654752f));
-        const float pdf = __expf(-0.5f * x[k] * x[k]) * 0.3989422804014327f;
+        float cdf, pdf;
+        hq_normal_cdf_pdf(x[k], cdf, pdf);
         o[k] = d[k] * (cdf + x[k] * pdf);
         acc[k] += o[k];
       }

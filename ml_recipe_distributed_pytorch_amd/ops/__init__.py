@@ -84,23 +84,36 @@ def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale
 
 
 # --------------------------------------------------------------------------------------- linear
-# Which projection GEMMs run on the hand-written MFMA kernel (gemm.hip) instead of hipBLASLt:
-#   HQ_GEMM=blas   none;  fused (default)  the ones whose epilogue fuses an elementwise pass
-#   (FFN1 + GELU, FFN2-dgrad + dGELU + bias-grad);  mfma  every supported shape.
+# Which projection GEMMs run on the hand-written MFMA NT kernel (gemm.hip) instead of hipBLASLt.
+#   HQ_GEMM=auto (default): where it measured faster on MI355X (tools/gemm_nt_bench.py,
+#     profiles/): the long-K shapes (K >= 2048: FFN2 forward, QKV / FFN1 dgrad), the fused
+#     FFN2-dgrad + dGELU + bias-grad, and FFN1 + GELU; only when the 256-row tile grid fills the
+#     256 CUs to >= 85 % (small batches fall back to hipBLASLt's narrower tiles);
+#   HQ_GEMM=mfma: every supported shape;  HQ_GEMM=blas: none.
 _EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID = range(5)
-_GEMM_MODE = os.environ.get("HQ_GEMM", "fused").lower()
+_GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
+_CUS = 256
 
 
-def _mfma(M: int, N: int, K: int, fused: bool) -> bool:
-    if _GEMM_MODE == "blas" or (_GEMM_MODE == "fused" and not fused):
+def _mfma(M: int, N: int, K: int, kind: str = "plain") -> bool:
+    if _GEMM_MODE == "blas":
         return False
-    return _k().gemm_nt_supported(int(M), int(N), int(K)) > 0
+    bn = _k().gemm_nt_supported(int(M), int(N), int(K))
+    if bn <= 0:
+        return False
+    if _GEMM_MODE == "mfma":
+        return True
+    tiles = (M // 256) * (N // bn)
+    fill = tiles / (-(-tiles // _CUS) * _CUS)
+    if fill < 0.85:
+        return False
+    return kind in ("dgelu", "gelu") or K >= 2048
 
 
 def linear_fwd(x, w, b, b32=None):
     """y = x·Wᵀ + b.  GPU: hipBLASLt (bias epilogue) or the MFMA NT kernel (fp32 ``b32`` bias)."""
     if x.is_cuda:
-        if b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1], False):
+        if b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1]):
             return _k().gemm_nt(x, w, _EPI_BIAS, bias=b32)
         return torch.addmm(b, x, w.t()) if b is not None else torch.mm(x, w.t())
     return ref.linear_fwd(x, w, b)
@@ -109,7 +122,7 @@ def linear_fwd(x, w, b, b32=None):
 def linear_gelu_fwd(x, w, b, b32=None):
     """(pre, act) with pre = x·Wᵀ + b, act = gelu(pre).  GPU: one MFMA GEMM with the GELU epilogue
     (pre stored for the backward) when the shape allows, else GEMM + gelu kernel."""
-    if x.is_cuda and b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1], True):
+    if x.is_cuda and b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1], "gelu"):
         pre = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
         act = _k().gemm_nt(x, w, _EPI_GELU, bias=b32, pre=pre)
         return pre, act
@@ -120,7 +133,7 @@ def linear_gelu_fwd(x, w, b, b32=None):
 def linear_dgrad(dy, w, wt=None):
     """dy·W.  ``wt`` = Wᵀ working copy (ParamStore.view_t) enables the NT MFMA kernel."""
     if dy.is_cuda:
-        if wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1], False):
+        if wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1]):
             return _k().gemm_nt(dy, wt, _EPI_NONE)
         return torch.mm(dy, w)
     return ref.linear_dgrad(dy, w)
@@ -129,7 +142,7 @@ def linear_dgrad(dy, w, wt=None):
 def linear_dgrad_add(dy, w, resid, wt=None):
     """resid + dy·W (fuses the residual-gradient add)."""
     if dy.is_cuda:
-        if wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1], False):
+        if wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1]):
             return _k().gemm_nt(dy, wt, _EPI_RESID, resid=resid)
         return torch.addmm(resid, dy, w)
     return ref.linear_dgrad_add(dy, w, resid)
@@ -138,7 +151,7 @@ def linear_dgrad_add(dy, w, resid, wt=None):
 def linear_dgrad_gelu(dy, w, pre, g_bias, accumulate, wt=None):
     """dpre = (dy·W) ⊙ gelu'(pre) and g_bias (+)= Σ_rows dpre — the dgrad of the layer after GELU
     fused with the GELU backward and the bias gradient of the layer before it."""
-    if dy.is_cuda and wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1], True):
+    if dy.is_cuda and wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1], "dgelu"):
         M, N = dy.shape[0], w.shape[1]
         part = torch.empty(M // 256, N, dtype=torch.float32, device=dy.device)
         dpre = _k().gemm_nt(dy, wt, _EPI_DGELU, pre=pre, part=part)
