@@ -111,12 +111,25 @@ __device__ __forceinline__ bf16x8_t pack_b(const float* v, int s) {
   return __builtin_bit_cast(bf16x8_t, u);
 }
 
+// Q fragment pre-multiplied by c = softmax_scale·log2(e) (rounded to bf16): the score MFMA then
+// yields log2-domain scores directly, and its accumulator is initialised with the per-key mask bias
+// (and, in the backward, minus the per-query LSE), so no per-element scale/bias/LSE VALU remains.
+// The forward and both backward kernels use the identical rounded Q·c, so P is recomputed exactly.
+__device__ __forceinline__ bf16x8_t prescale8(const bf16x8_t& q, float c) {
+  float f[8];
+  hq_unpack8(__builtin_bit_cast(uint4, q), f);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] *= c;
+  return __builtin_bit_cast(bf16x8_t, hq_pack8(f));
+}
+
 __device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
 
 // Cooperative copy of rows [0, Lp) of a [*, ld] bf16 matrix (64 columns starting at src) into a
 // [Lp][64] LDS image; rows >= L are zero.  Each thread issues all its 16-B loads before any store.
-template <int NT>
-__device__ __forceinline__ void load_head(uint16_t* dst, const uint16_t* src, size_t ld, int L, int Lp) {
+template <int NT, bool SCALE = false>
+__device__ __forceinline__ void load_head(uint16_t* dst, const uint16_t* src, size_t ld, int L, int Lp,
+                                          float c = 1.f) {
   constexpr int kMax = 8;  // up to 512 rows × 8 chunks / (NT threads)
   uint4 buf[kMax];
   const int n = Lp * 8;
@@ -132,7 +145,17 @@ __device__ __forceinline__ void load_head(uint16_t* dst, const uint16_t* src, si
 #pragma unroll
   for (int i = 0; i < kMax; ++i) {
     const int t = threadIdx.x + i * NT;
-    if (t < n) *reinterpret_cast<uint4*>(dst + lds_off(t >> 3, (t & 7) * 8)) = buf[i];
+    if (t < n) {
+      uint4 v = buf[i];
+      if constexpr (SCALE) {
+        float f[8];
+        hq_unpack8(v, f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] *= c;
+        v = hq_pack8(f);
+      }
+      *reinterpret_cast<uint4*>(dst + lds_off(t >> 3, (t & 7) * 8)) = v;
+    }
   }
 }
 
@@ -158,7 +181,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
   bf16x8_t qf[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s)
-    qf[s] = (qi < L) ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)qi * ld + 16 * s + 8 * hh)
+    qf[s] = (qi < L) ? prescale8(*reinterpret_cast<const bf16x8_t*>(base + (size_t)qi * ld + 16 * s + 8 * hh), c_scale)
                      : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
   load_head<NWB * 64>(sK, base + H, ld, L, Lp);
   load_head<NWB * 64>(sV, base + 2 * H, ld, L, Lp);
@@ -180,19 +203,16 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
   for (int kt = 0; kt < n32; ++kt) {
     f32x16_t acc;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int g = 0; g < 4; ++g) {  // accumulator starts at the key-mask bias (log2 domain)
+      const float4 bb = *reinterpret_cast<const float4*>(sB + kt * 32 + 8 * g + 4 * hh);
+      acc[4 * g + 0] = bb.x; acc[4 * g + 1] = bb.y; acc[4 * g + 2] = bb.z; acc[4 * g + 3] = bb.w;
+    }
 #pragma unroll
     for (int s = 0; s < 4; ++s) acc = mfma32(row8(sK, kt * 32, lo_, s), qf[s], acc);
     float sc[16];
     float mx = -INFINITY;
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float4 bb = *reinterpret_cast<const float4*>(sB + kt * 32 + 8 * g + 4 * hh);
-      sc[4 * g + 0] = fmaf(acc[4 * g + 0], c_scale, bb.x);
-      sc[4 * g + 1] = fmaf(acc[4 * g + 1], c_scale, bb.y);
-      sc[4 * g + 2] = fmaf(acc[4 * g + 2], c_scale, bb.z);
-      sc[4 * g + 3] = fmaf(acc[4 * g + 3], c_scale, bb.w);
-    }
+    for (int r = 0; r < 16; ++r) sc[r] = acc[r];
 #pragma unroll
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
@@ -283,7 +303,8 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
   float dpart = 0.f;
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    qf[s] = qok ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)qi * ld + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    qf[s] = qok ? prescale8(*reinterpret_cast<const bf16x8_t*>(base + (size_t)qi * ld + 16 * s + 8 * hh), c_scale)
+                : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
     of[s] = qok ? *reinterpret_cast<const bf16x8_t*>(dctx + orow + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
     if (qok) {
       float x[8], y[8];
@@ -314,7 +335,13 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
   for (int kt = 0; kt < n32; ++kt) {
     f32x16_t s_acc, p_acc;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { s_acc[r] = 0.f; p_acc[r] = 0.f; }
+    for (int g = 0; g < 4; ++g) {  // S' = c·q·k + bias − lse (log2 domain) straight out of the MFMA
+      const float4 bb = *reinterpret_cast<const float4*>(sB + kt * 32 + 8 * g + 4 * hh);
+      s_acc[4 * g + 0] = bb.x - lq; s_acc[4 * g + 1] = bb.y - lq;
+      s_acc[4 * g + 2] = bb.z - lq; s_acc[4 * g + 3] = bb.w - lq;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) p_acc[r] = 0.f;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       s_acc = mfma32(row8(sK, kt * 32, lo_, s), qf[s], s_acc);
@@ -328,16 +355,10 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
     }
     float ds[16];
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float4 bb = *reinterpret_cast<const float4*>(sB + kt * 32 + 8 * g + 4 * hh);
-      const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int r = 4 * g + i;
-        const float P = __builtin_amdgcn_exp2f(fmaf(s_acc[r], c_scale, bv[i]) - lq);
-        const float mk = ((bits >> r) & 1u) ? ks : 0.f;
-        ds[r] = P * fmaf(p_acc[r], mk, -dlt);
-      }
+    for (int r = 0; r < 16; ++r) {
+      const float P = __builtin_amdgcn_exp2f(s_acc[r]);
+      const float mk = ((bits >> r) & 1u) ? ks : 0.f;
+      ds[r] = P * fmaf(p_acc[r], mk, -dlt);
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -389,7 +410,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
     vf[s] = kok ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)kj * ld + 2 * H + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
   }
   const float kb = kok ? key_bias[(size_t)b * L + kj] * LOG2E : -INFINITY;
-  load_head<NWB * 64>(sQ, base, ld, L, Lp);
+  load_head<NWB * 64, true>(sQ, base, ld, L, Lp, c_scale);  // Q·c, exactly as the forward's
   load_head<NWB * 64>(sO, dctx + (size_t)b * L * H + h * D, H, L, Lp);
   for (int t = threadIdx.x; t < Lp; t += NWB * 64) {
     sL[t] = t < L ? lse[(size_t)bh * L + t] * LOG2E : INFINITY;
@@ -420,7 +441,11 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
     for (int qt = 0; qt < n32; ++qt) {
       f32x16_t s_acc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s_acc[r] = 0.f;
+      for (int g = 0; g < 4; ++g) {  // S' = c·q·k + bias − lse (key on the lane, query in the register)
+        const float4 l4 = *reinterpret_cast<const float4*>(sL + qt * 32 + 8 * g + 4 * hh);
+        s_acc[4 * g + 0] = kb - l4.x; s_acc[4 * g + 1] = kb - l4.y;
+        s_acc[4 * g + 2] = kb - l4.z; s_acc[4 * g + 3] = kb - l4.w;
+      }
 #pragma unroll
       for (int s = 0; s < 4; ++s) s_acc = mfma32(row8(sQ, qt * 32, lo_, s), kf[s], s_acc);
       const uint32_t word = DROP ? (uint32_t)mbits[(((size_t)bh * n32 + qt) * n32 + ks_idx) * 64 + lane] : 0xFFFFu;
@@ -430,14 +455,12 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
 #pragma unroll
         for (int gg = 0; gg < 2; ++gg) {
           const int g = 2 * s + gg;
-          const float4 l4 = *reinterpret_cast<const float4*>(sL + qt * 32 + 8 * g + 4 * hh);
-          const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int r = 4 * g + i;
             const uint32_t w = DROP ? (uint32_t)__shfl((int)word, acc_row(r, hh) + 32 * hh_f, 64) : 0xFFFFu;
             const float mk = ((w >> r_f) & 1u) ? ksc : 0.f;
-            pd[4 * gg + i] = __builtin_amdgcn_exp2f(fmaf(s_acc[r], c_scale, kb) - lv[i]) * mk;
+            pd[4 * gg + i] = __builtin_amdgcn_exp2f(s_acc[r]) * mk;
           }
         }
         const bf16x8_t pb = pack_b(pd, 0);
@@ -465,7 +488,13 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
     for (int qt = 0; qt < n32; ++qt) {
       f32x16_t s_acc, p_acc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) { s_acc[r] = 0.f; p_acc[r] = 0.f; }
+      for (int g = 0; g < 4; ++g) {
+        const float4 l4 = *reinterpret_cast<const float4*>(sL + qt * 32 + 8 * g + 4 * hh);
+        s_acc[4 * g + 0] = kb - l4.x; s_acc[4 * g + 1] = kb - l4.y;
+        s_acc[4 * g + 2] = kb - l4.z; s_acc[4 * g + 3] = kb - l4.w;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) p_acc[r] = 0.f;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         s_acc = mfma32(row8(sQ, qt * 32, lo_, s), kf[s], s_acc);
@@ -478,16 +507,14 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
 #pragma unroll
         for (int gg = 0; gg < 2; ++gg) {
           const int g = 2 * s + gg;
-          const float4 l4 = *reinterpret_cast<const float4*>(sL + qt * 32 + 8 * g + 4 * hh);
           const float4 d4 = *reinterpret_cast<const float4*>(sD + qt * 32 + 8 * g + 4 * hh);
-          const float lv[4] = {l4.x, l4.y, l4.z, l4.w};
           const float dl[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int r = 4 * g + i;
             const uint32_t w = DROP ? (uint32_t)__shfl((int)word, acc_row(r, hh) + 32 * hh_f, 64) : 0xFFFFu;
             const float mk = ((w >> r_f) & 1u) ? ksc : 0.f;
-            const float P = __builtin_amdgcn_exp2f(fmaf(s_acc[r], c_scale, kb) - lv[i]);
+            const float P = __builtin_amdgcn_exp2f(s_acc[r]);
             ds[4 * gg + i] = P * fmaf(p_acc[r], mk, -dl[i]);
           }
         }
@@ -501,7 +528,8 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
       for (int d = 0; d < 2; ++d)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          float k4[4] = {dk[d][4 * g] * scale, dk[d][4 * g + 1] * scale, dk[d][4 * g + 2] * scale, dk[d][4 * g + 3] * scale};
+          // sQ holds Q·c (c = scale·log2e): dK = scale·Σ dS·q = Σ dS·(q·c) / log2e
+          float k4[4] = {dk[d][4 * g] * LN2, dk[d][4 * g + 1] * LN2, dk[d][4 * g + 2] * LN2, dk[d][4 * g + 3] * LN2};
           *reinterpret_cast<uint2*>(out + H + d * 32 + 8 * g + 4 * hh) = hq_pack4(k4);
         }
     }

@@ -85,10 +85,10 @@ def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale
 
 # --------------------------------------------------------------------------------------- linear
 # Which projection GEMMs run on the hand-written MFMA NT kernel (gemm.hip) instead of hipBLASLt.
-#   HQ_GEMM=auto (default): where it measured faster on MI355X (tools/gemm_nt_bench.py,
-#     profiles/): the long-K shapes (K >= 2048: FFN2 forward, QKV / FFN1 dgrad), the fused
-#     FFN2-dgrad + dGELU + bias-grad, and FFN1 + GELU; only when the 256-row tile grid fills the
-#     256 CUs to >= 85 % (small batches fall back to hipBLASLt's narrower tiles);
+#   HQ_GEMM=auto (default): the GEMMs whose epilogue fuses an elementwise pass — FFN1 + GELU and
+#     FFN2-dgrad + dGELU + FFN1 bias-grad (1.04x / 1.34x vs hipBLASLt + separate kernel at b256,
+#     profiles/) — when the 256-row tile grid fills the 256 CUs to >= 85 %.  Plain projections stay
+#     on hipBLASLt with the shipped TunableOp picks, which measured 3-15 % faster than this kernel;
 #   HQ_GEMM=mfma: every supported shape;  HQ_GEMM=blas: none.
 _EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID = range(5)
 _GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
@@ -105,9 +105,7 @@ def _mfma(M: int, N: int, K: int, kind: str = "plain") -> bool:
         return True
     tiles = (M // 256) * (N // bn)
     fill = tiles / (-(-tiles // _CUS) * _CUS)
-    if fill < 0.85:
-        return False
-    return kind in ("dgelu", "gelu") or K >= 2048
+    return fill >= 0.85 and kind in ("dgelu", "gelu")
 
 
 def linear_fwd(x, w, b, b32=None):
