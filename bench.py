@@ -36,6 +36,8 @@ def parse():
     ap.add_argument("--seq", type=int, default=384)
     ap.add_argument("--model", default="bert-base-uncased")
     ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
+                    help="compute precision; fp8 = OCP e4m3 forward projections (BASELINE config #5)")
     ap.add_argument("--bucket_cap_mb", type=float, default=32.0)
     ap.add_argument("--profile", action="store_true", help="per-phase timers (adds syncs; not for the headline)")
     ap.add_argument("--json_out", default=None)
@@ -69,7 +71,7 @@ def main():
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
 
     cfg = get_config(args.model)
-    model = BertForQuestionAnswering(cfg, seed=1234).to(device).train()
+    model = BertForQuestionAnswering(cfg, seed=1234, precision=args.precision).to(device).train()
     # config/test_bert.cfg: loss=smooth(0.01), all five loss weights 1, lr 1e-5, wd 1e-4, clip 1
     lp = SimpleNamespace(loss="smooth", smooth_alpha=0.01, focal_alpha=1, focal_gamma=2, w_start=1, w_end=1,
                          w_start_reg=1, w_end_reg=1, w_cls=1)
@@ -134,7 +136,7 @@ def main():
     flops_per_sample = 6 * 85.0e6 * L + 12 * L * L * cfg.hidden_size * cfg.num_hidden_layers  # SURVEY §6.2 model
     out = {"metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None), "dtype": "bf16",
+           "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None), "dtype": args.precision,
            "data": "synthetic (dummy-QA generator, random-init weights)",
            "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": L,
                       "parallelism": f"dp{world}", "allreduce_dtype": args.allreduce_dtype,

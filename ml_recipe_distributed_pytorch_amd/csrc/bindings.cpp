@@ -183,6 +183,19 @@ void colsum_into(Tensor part, Tensor out, bool accumulate) {
   hq_colsum(ptr<float>(part), (int)part.size(0), (int)part.size(1), ptr<float>(out), accumulate, cur_stream());
 }
 
+// x (bf16, numel % 8 == 0) -> (x8 float8_e4m3fn, scale f32[1]) with x ≈ x8 · scale (current scaling)
+std::vector<Tensor> fp8_quantize(Tensor x) {
+  check(x, BF16, "x");
+  TORCH_CHECK(x.numel() % 8 == 0, "fp8_quantize: numel must be a multiple of 8");
+  c10::DeviceGuard g(x.device());
+  auto y = at::empty(x.sizes(), x.options().dtype(at::kFloat8_e4m3fn));
+  auto amax = at::empty({1}, x.options().dtype(at::kInt));
+  auto scale = at::empty({1}, x.options().dtype(F32));
+  hq_amax_bf16(ptr<uint16_t>(x), x.numel(), ptr<unsigned>(amax), cur_stream());
+  hq_fp8_quant(ptr<uint16_t>(x), ptr<uint8_t>(y), x.numel(), ptr<unsigned>(amax), ptr<float>(scale), cur_stream());
+  return {y, scale.view({})};
+}
+
 Tensor gelu_fwd(Tensor pre) {
   check(pre, BF16, "pre");
   TORCH_CHECK(pre.numel() % 8 == 0, "numel must be a multiple of 8");
@@ -331,6 +344,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("transpose_tiles", &transpose_tiles);
   m.def("colsum_into", &colsum_into);
+  m.def("fp8_quantize", &fp8_quantize);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("bias_grad", &bias_grad);
   m.def("attn_fwd", &attn_fwd);

@@ -75,3 +75,7 @@ void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
 void hq_transpose_tiles(const uint16_t* src, uint16_t* dst, const int* tiles, int ntiles, hipStream_t s);
 // out[c] (+)= sum_p part[p][c], part f32 [P][N]
 void hq_colsum(const float* part, int P, int N, float* out, bool accumulate, hipStream_t s);
+
+// ------------------------------------------------------------------ fp8 (fp8.hip); n % 8 == 0
+void hq_amax_bf16(const uint16_t* x, size_t n, unsigned* amax, hipStream_t s);
+void hq_fp8_quant(const uint16_t* x, uint8_t* y, size_t n, const unsigned* amax, float* scale, hipStream_t s);

@@ -234,21 +234,33 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
     }
     l_run += rs;
     if constexpr (DROP) {
+      // keep bits straight from the integer compares; the 1/(1-p) scale is applied once to O at the end
       uint32_t bits = 0;
+      if constexpr (EVEN) {
+        // L % 32 == 0: the tile's 16 pair indices are pbase | (4g + 2hh + ip) with pbase % 16 == 0, so
+        // (pair ^ key) = pk ^ (4g + ip): ONE xor per hash instead of index arithmetic.
+        const uint32_t pk = (((row_idx >> 1) + (uint32_t)kt * 16u) ^ key) ^ (2u * (uint32_t)hh);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint32_t idx0 = row_idx + kt * 32 + 8 * g + 4 * hh;
-        float mk[4];
-        if constexpr (EVEN) {
-          hq_keep4(idx0, key, thr, kscale, mk);
-        } else {
+        for (int g = 0; g < 4; ++g)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) mk[i] = hq_keep(idx0 + i, key, thr) ? kscale : 0.f;
-        }
+          for (int ip = 0; ip < 2; ++ip) {
+            const uint32_t h = hq_mix24(pk ^ (uint32_t)(4 * g + ip));
+            const int r = 4 * g + 2 * ip;
+            const bool k0 = (h & 0xFFFFu) >= thr, k1 = (h >> 16) >= thr;
+            sc[r] = k0 ? sc[r] : 0.f;
+            sc[r + 1] = k1 ? sc[r + 1] : 0.f;
+            bits |= ((uint32_t)k0 << r) | ((uint32_t)k1 << (r + 1));
+          }
+      } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          sc[4 * g + i] *= mk[i];
-          bits |= (mk[i] != 0.f ? 1u : 0u) << (4 * g + i);
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t idx0 = row_idx + kt * 32 + 8 * g + 4 * hh;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bool k = hq_keep(idx0 + i, key, thr);
+            sc[4 * g + i] = k ? sc[4 * g + i] : 0.f;
+            bits |= (uint32_t)k << (4 * g + i);
+          }
         }
       }
       my_bits[(size_t)kt * 64] = (uint16_t)bits;
@@ -261,7 +273,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
     }
   }
   const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  const float inv = 1.f / l_tot;
+  const float inv = (DROP ? kscale : 1.f) / l_tot;
   if (qi < L) {
     uint16_t* out = ctx + ((size_t)b * L + qi) * H + h * D;
 #pragma unroll
@@ -589,7 +601,7 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
                          thr ? mbits : nullptr, L, nh, scale * LOG2E, key, thr, hq_keep_scale(thr));
     };
     if (!thr) launch(attn_fwd_kernel<NW, false, true>);
-    else if ((L & 1) == 0) launch(attn_fwd_kernel<NW, true, true>);
+    else if ((L & 31) == 0) launch(attn_fwd_kernel<NW, true, true>);
     else launch(attn_fwd_kernel<NW, true, false>);
   });
 }

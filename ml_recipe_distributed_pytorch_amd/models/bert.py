@@ -166,17 +166,26 @@ class _LayerFn(torch.autograd.Function):
         scale = 1.0 / math.sqrt(cfg.head_dim)
         op0 = 1 + 3 * idx
         Bm = lambda k: st.view(p + k, "master")  # noqa: E731  (fp32 bias for the MFMA epilogue)
-        qkv = ops.linear_fwd(x, st.view(p + "qkv.weight"), st.view(p + "qkv.bias"), Bm("qkv.bias"))
+        fp8 = m.precision == "fp8" and x.is_cuda
+
+        def proj(inp, name):  # forward projection: fp8 (--precision fp8) or bf16
+            if fp8:
+                return ops.linear_fwd_fp8(inp, st.view_fp8(p + name + ".weight"), st.view(p + name + ".bias"))
+            return ops.linear_fwd(inp, st.view(p + name + ".weight"), st.view(p + name + ".bias"), Bm(name + ".bias"))
+
+        qkv = proj(x, "qkv")
         ctxv, lse, bits = ops.attn_fwd(qkv, key_bias, B, L, nh, pa, info.seed, op0, scale)
-        a1 = ops.linear_fwd(ctxv, st.view(p + "attention.output.dense.weight"), st.view(p + "attention.output.dense.bias"),
-                            Bm("attention.output.dense.bias"))
+        a1 = proj(ctxv, "attention.output.dense")
         h1, z1, m1, r1 = ops.ln_fwd(a1, x, st.view(p + "attention.output.LayerNorm.weight", "master"),
                                     st.view(p + "attention.output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph,
                                     info.seed, op0 + 1)
-        pre, act = ops.linear_gelu_fwd(h1, st.view(p + "intermediate.dense.weight"),
-                                       st.view(p + "intermediate.dense.bias"), Bm("intermediate.dense.bias"))
-        a2 = ops.linear_fwd(act, st.view(p + "output.dense.weight"), st.view(p + "output.dense.bias"),
-                            Bm("output.dense.bias"))
+        if fp8:
+            pre = proj(h1, "intermediate.dense")
+            act = ops.gelu_fwd(pre)
+        else:
+            pre, act = ops.linear_gelu_fwd(h1, st.view(p + "intermediate.dense.weight"),
+                                           st.view(p + "intermediate.dense.bias"), Bm("intermediate.dense.bias"))
+        a2 = proj(act, "output.dense")
         h2, z2, m2, r2 = ops.ln_fwd(a2, h1, st.view(p + "output.LayerNorm.weight", "master"),
                                     st.view(p + "output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph,
                                     info.seed, op0 + 2)

@@ -70,6 +70,8 @@ class ParamStore:
         self.compute_t: Optional[torch.Tensor] = None
         self._t_tiles: Optional[torch.Tensor] = None
         self._t_dirty = True
+        self._fp8: Dict[str, Tuple[torch.Tensor, torch.Tensor]] = {}
+        self._fp8_dirty = True
 
     # ------------------------------------------------------------------ allocation
     def allocate(self, device, init_std: float, generator: Optional[torch.Generator] = None):
@@ -115,6 +117,8 @@ class ParamStore:
             self.compute.copy_(self.master)
         self._dirty = False
         self._t_dirty = True
+        self._fp8_dirty = True
+        self._fp8_dirty = True
         self.compute_t = None
         self._t_tiles = None
 
@@ -150,6 +154,18 @@ class ParamStore:
             self._t_tiles = torch.tensor(rows, dtype=torch.int32).to(self.compute.device)
         kernels().transpose_tiles(self.compute, self.compute_t, self._t_tiles)
         self._t_dirty = False
+
+    def view_fp8(self, key: str):
+        """(W as float8_e4m3fn, dequant scale) of a registered weight for the fp8 forward GEMMs,
+        re-quantised (current per-tensor scaling) after every change of the working copy."""
+        if key not in self._t_off or not self._transposable():
+            return None
+        if self._fp8_dirty:
+            from .._native import kernels
+            k = kernels()
+            self._fp8 = {kk: tuple(k.fp8_quantize(self.view(kk))) for kk in self._t_keys}
+            self._fp8_dirty = False
+        return self._fp8[key]
 
     def view_t(self, key: str) -> Optional[torch.Tensor]:
         """Wᵀ of a registered weight, or None when unavailable (CPU / fp32 / not registered)."""
@@ -189,12 +205,14 @@ class ParamStore:
         if self._dirty and self.compute is not None and self.compute.data_ptr() != self.master.data_ptr():
             self.compute.copy_(self.master)
             self._t_dirty = True
+            self._fp8_dirty = True
         self._dirty = False
 
     def mark_clean(self):
         """The optimizer rewrote master AND the working copy."""
         self._dirty = False
         self._t_dirty = True
+        self._fp8_dirty = True
 
     # ------------------------------------------------------------------ layout queries
     def segments(self, names: Optional[Iterable[str]] = None) -> List[Tuple[int, int, str]]:

@@ -117,6 +117,14 @@ def linear_fwd(x, w, b, b32=None):
     return ref.linear_fwd(x, w, b)
 
 
+def linear_fwd_fp8(x, w8s, b):
+    """y = x·Wᵀ + b with both operands in OCP fp8 e4m3 (per-tensor current scaling) on hipBLASLt's
+    fp8 MFMA path (torch._scaled_mm), bf16 out.  ``w8s`` = (W fp8 [N,K], scale) from ParamStore.view_fp8."""
+    x8, sx = _k().fp8_quantize(x)
+    w8, sw = w8s
+    return torch._scaled_mm(x8, w8.t(), scale_a=sx, scale_b=sw, bias=b, out_dtype=torch.bfloat16)
+
+
 def linear_gelu_fwd(x, w, b, b32=None):
     """(pre, act) with pre = x·Wᵀ + b, act = gelu(pre).  GPU: one MFMA GEMM with the GELU epilogue
     (pre stored for the backward) when the shape allows, else GEMM + gelu kernel."""
@@ -160,12 +168,16 @@ def linear_dgrad_gelu(dy, w, pre, g_bias, accumulate, wt=None):
 
 
 def _wgrad_splits(T: int, N: int, K: int) -> int:
-    """Split-K factor for dW = dyᵀ·x (reduction over T tokens, output only N×K).  hipBLASLt runs these
-    long-K/small-MN GEMMs at 220-500 TF on MI355X (a 768×768 output is 9 tiles of 256² for 256 CUs);
-    a batched split over T restores occupancy (measured 410-880 TF, tools/gemm_bench.py)."""
+    """Split-K factor for dW = dyᵀ·x (reduction over T tokens, output only N×K): hipBLASLt runs these
+    long-K / small-MN GEMMs far below peak (a 768×768 output is 9 tiles of 256² for 256 CUs), so the
+    T axis is split into a batched GEMM with fp32 partials.  Factors from the MI355X sweep
+    (tools/wgrad_bench.py, profiles/): ~6k tokens per split for >= 32 output tiles, ~3k for 10-31,
+    ~1.5k for <= 9, at most 16 splits (T = 98304: 16 everywhere, 430-480 µs → 0.8-1.0 PF)."""
     tiles = max(1, (N * K) // (256 * 256))
+    per = 6144 if tiles >= 32 else (3072 if tiles > 9 else 1536)
+    target = max(1, min(16, T // per))
     s = 1
-    while s < 8 and tiles * s * 2 <= 220 and T % (s * 2) == 0 and T // (s * 2) >= 2048:
+    while s * 2 <= target and T % (s * 2) == 0 and T // (s * 2) >= 1024:
         s *= 2
     return s
 

@@ -60,3 +60,23 @@ def test_bert_base_step_runs(cuda):
     torch.cuda.synchronize()
     assert torch.isfinite(m.store.grad).all()
     assert m.store.grad.abs().sum().item() > 0
+
+
+def test_bert_base_fp8_forward_close_to_bf16(cuda):
+    """--precision fp8: forward projections on fp8 e4m3 operands stay close to the bf16 model."""
+    cfg = get_config("bert-base-uncased", hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    m = BertForQuestionAnswering(cfg, seed=0).to(cuda).eval()
+    ids, mask, tt = _inputs(4, 256, cfg.vocab_size)
+    ids, mask, tt = ids.to(cuda), mask.to(cuda), tt.to(cuda)
+    with torch.no_grad():
+        ref = m(ids, mask, tt)
+        m.set_precision("fp8")
+        out = m(ids, mask, tt)
+    for k in ("start_class", "end_class", "cls"):
+        rel = ((out[k].float() - ref[k].float()).norm() / ref[k].float().norm()).item()
+        assert rel < 0.1, (k, rel)
+    m.train()
+    loss = sum(v.float().mean() for v in m(ids, mask, tt).values())
+    m.zero_grad()
+    loss.backward()
+    assert torch.isfinite(m.store.grad).all()
