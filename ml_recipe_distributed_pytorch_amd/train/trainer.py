@@ -35,6 +35,7 @@ from ..parallel import dist as hqdist
 from ..parallel.reducer import GradReducer
 from ..utils.tb import SummaryWriter
 from .callbacks import TestCallback
+from .amp import apex_to_precision, resolve_precision  # noqa: F401  (apex_to_precision re-exported)
 from .engine import TrainEngine, to_device
 from .meters import AverageMeter
 from .optim import get_linear_schedule_with_warmup
@@ -58,12 +59,6 @@ def time_profiler(fun):
         finally:
             logger.info(f"Execution of {fun.__name__} took {time.perf_counter() - start:.3f} sec.")
     return wrapped
-
-
-def apex_to_precision(apex_level: Optional[str], device: torch.device) -> str:
-    if device.type != "cuda":
-        return "fp32"
-    return "fp32" if apex_level == "O0" else "bf16"
 
 
 def _fault_hook(rank: int, step: int):
@@ -120,7 +115,7 @@ class Trainer:
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         if self.sync_bn and self.local_rank != -1:
             logger.info("sync_bn: the BERT encoder has no BatchNorm layers; nothing to convert.")
-        prec = self.precision or apex_to_precision(self.apex_level, self.device)
+        prec = resolve_precision(self.precision, self.apex_level, self.device, self.apex_loss_scale)
         if hasattr(self.model, "set_precision"):
             self.model.set_precision(prec)
         self.model = self.model.to(self.device)
