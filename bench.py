@@ -133,7 +133,9 @@ def main():
     final_loss = res.losses.to_floats().get("loss", float("nan"))
     ms = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
-    flops_per_sample = 6 * 85.0e6 * L + 12 * L * L * cfg.hidden_size * cfg.num_hidden_layers  # SURVEY §6.2 model
+    H, F, NL = cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers
+    enc_linear = NL * (4 * H * H + 2 * H * F)  # 85.0 M (base), 302 M (large)
+    flops_per_sample = 6 * enc_linear * L + 12 * L * L * H * NL  # SURVEY §6.2 model
     out = {"metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None), "dtype": args.precision,

@@ -193,7 +193,7 @@ std::vector<Tensor> fp8_quantize(Tensor x) {
   auto scale = at::empty({1}, x.options().dtype(F32));
   hq_amax_bf16(ptr<uint16_t>(x), x.numel(), ptr<unsigned>(amax), cur_stream());
   hq_fp8_quant(ptr<uint16_t>(x), ptr<uint8_t>(y), x.numel(), ptr<unsigned>(amax), ptr<float>(scale), cur_stream());
-  return {y, scale.view({})};
+  return {y, scale.squeeze(0)};
 }
 
 Tensor gelu_fwd(Tensor pre) {

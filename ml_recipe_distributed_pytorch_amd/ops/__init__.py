@@ -95,6 +95,13 @@ _GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
 _CUS = 256
 
 
+def set_gemm_mode(mode: str) -> str:
+    """Switch the projection-GEMM policy at runtime (auto | mfma | blas); returns the previous mode."""
+    global _GEMM_MODE
+    prev, _GEMM_MODE = _GEMM_MODE, mode.lower()
+    return prev
+
+
 def _mfma(M: int, N: int, K: int, kind: str = "plain") -> bool:
     if _GEMM_MODE == "blas":
         return False

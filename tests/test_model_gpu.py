@@ -20,14 +20,25 @@ def _inputs(B, L, V):
     return ids, ids > 0, tt
 
 
-@pytest.mark.parametrize("train", [False, True])
-def test_tiny_model_gpu_matches_cpu(cuda, train):
+@pytest.mark.parametrize("train,gemm", [(False, "auto"), (True, "auto"), (True, "mfma")])
+def test_tiny_model_gpu_matches_cpu(cuda, train, gemm):
+    """gemm="mfma" routes every projection (fwd + GELU epilogue, dgrad, residual and dGELU
+    epilogues on the transposed weight copies) through the hand-written MFMA GEMM."""
+    from ml_recipe_distributed_pytorch_amd import ops
+    prev = ops.set_gemm_mode(gemm)
+    try:
+        _tiny_parity(cuda, train, B=4 if gemm == "mfma" else 3)
+    finally:
+        ops.set_gemm_mode(prev)
+
+
+def _tiny_parity(cuda, train, B):
     cfg = get_config("bert-tiny-test")
     cpu = BertForQuestionAnswering(cfg, seed=0)
     gpu = copy.deepcopy(cpu).to(cuda)
     cpu.train(train)
     gpu.train(train)
-    ids, mask, tt = _inputs(3, 64, cfg.vocab_size)
+    ids, mask, tt = _inputs(B, 64, cfg.vocab_size)
     torch.manual_seed(11)
     oc = cpu(ids, mask, tt)
     torch.manual_seed(11)

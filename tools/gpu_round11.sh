@@ -10,3 +10,4 @@ tail -2 $O/pytest_gpu.log
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > $O/bench.log 2>&1 && tail -1 $O/bench.log
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --precision fp8 > $O/bench_fp8.log 2>&1 && tail -1 $O/bench_fp8.log
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 --batch 64 > $O/bench_b64.log 2>&1 && tail -1 $O/bench_b64.log
+timeout -k 10 600 python bench.py --model bert-large-uncased --seq 512 --batch 64 --steps 10 --warmup 3 > $O/bench_large512.log 2>&1 && tail -1 $O/bench_large512.log
