@@ -196,6 +196,31 @@ std::vector<Tensor> fp8_quantize(Tensor x) {
   return {y, scale.squeeze(0)};
 }
 
+// QA span head: logits [T,2] fp32 = seq[T,H] (bf16) · w[2,H]^T + b
+Tensor span_fwd(Tensor seq, Tensor w, Tensor b) {
+  check(seq, BF16, "seq"); check(w, F32, "w"); check(b, F32, "b");
+  const int64_t H = seq.size(-1), T = seq.numel() / H;
+  TORCH_CHECK(w.numel() == 2 * H && b.numel() == 2, "span_fwd: w [2,H], b [2]");
+  TORCH_CHECK(H % 4 == 0 && H <= 2048, "span_fwd: hidden size");
+  c10::DeviceGuard g(seq.device());
+  auto logits = at::empty({T, 2}, w.options());
+  hq_span_fwd(ptr<uint16_t>(seq), ptr<float>(w), ptr<float>(b), ptr<float>(logits), (int)T, (int)H, cur_stream());
+  return logits;
+}
+
+// returns dseq (bf16, seq's shape); dw [2,H] f32 written (or accumulated)
+Tensor span_bwd(Tensor seq, Tensor w, Tensor glog, Tensor dw, bool accumulate) {
+  check(seq, BF16, "seq"); check(w, F32, "w"); check(glog, F32, "grad_logits"); check(dw, F32, "dw");
+  const int64_t H = seq.size(-1), T = seq.numel() / H;
+  TORCH_CHECK(w.numel() == 2 * H && dw.numel() == 2 * H && glog.numel() == 2 * T, "span_bwd: shapes");
+  c10::DeviceGuard g(seq.device());
+  auto dseq = at::empty_like(seq);
+  auto part = at::empty({(int64_t)hq_ln_bwd_partials((int)T), 2 * H}, w.options());
+  hq_span_bwd(ptr<uint16_t>(seq), ptr<float>(w), ptr<float>(glog), ptr<uint16_t>(dseq), ptr<float>(part), ptr<float>(dw),
+              (int)T, (int)H, accumulate, cur_stream());
+  return dseq;
+}
+
 Tensor gelu_fwd(Tensor pre) {
   check(pre, BF16, "pre");
   TORCH_CHECK(pre.numel() % 8 == 0, "numel must be a multiple of 8");
@@ -345,6 +370,8 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("transpose_tiles", &transpose_tiles);
   m.def("colsum_into", &colsum_into);
   m.def("fp8_quantize", &fp8_quantize);
+  m.def("span_fwd", &span_fwd);
+  m.def("span_bwd", &span_bwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("bias_grad", &bias_grad);
   m.def("attn_fwd", &attn_fwd);

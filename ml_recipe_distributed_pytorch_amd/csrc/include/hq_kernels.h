@@ -79,3 +79,9 @@ void hq_colsum(const float* part, int P, int N, float* out, bool accumulate, hip
 // ------------------------------------------------------------------ fp8 (fp8.hip); n % 8 == 0
 void hq_amax_bf16(const uint16_t* x, size_t n, unsigned* amax, hipStream_t s);
 void hq_fp8_quant(const uint16_t* x, uint8_t* y, size_t n, const unsigned* amax, float* scale, hipStream_t s);
+
+// ------------------------------------------------------------------ QA span head (norm.hip)
+void hq_span_fwd(const uint16_t* seq, const float* w, const float* b, float* logits, int T, int H, hipStream_t s);
+// part: [hq_ln_bwd_partials(T)][2][H] scratch; dw: [2][H] (+)=
+void hq_span_bwd(const uint16_t* seq, const float* w, const float* g, uint16_t* dseq, float* part, float* dw, int T,
+                 int H, bool accumulate, hipStream_t s);

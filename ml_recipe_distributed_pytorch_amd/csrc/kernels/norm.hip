@@ -209,6 +209,77 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
   block_partials<NCH, 3>(acc, lds, part, H);
 }
 
+// QA span head (reference model.py:30,54-58: position_outputs = Linear(H, 2) over the sequence
+// output): fwd logits[t] = (seq[t]·w0 + b0, seq[t]·w1 + b1) in fp32 straight from the bf16 sequence
+// (no fp32 copy of the [T, H] activations); bwd dseq[t] = g[t,0]·w0 + g[t,1]·w1 (bf16) plus
+// deterministic per-block partials of dW = Σ_t g[t]ᵀ·seq[t].
+template <int NCH>
+__global__ __launch_bounds__(256) void span_fwd_kernel(const uint16_t* __restrict__ seq, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, float* __restrict__ logits, int T,
+                                                       int H) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kWaves + wave;
+  if (row >= T) return;
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    if (col < H) {
+      float x[4];
+      hq_unpack4(*reinterpret_cast<const uint2*>(seq + (size_t)row * H + col), x);
+      const float4 a = *reinterpret_cast<const float4*>(w + col);
+      const float4 b = *reinterpret_cast<const float4*>(w + H + col);
+      s0 += x[0] * a.x + x[1] * a.y + x[2] * a.z + x[3] * a.w;
+      s1 += x[0] * b.x + x[1] * b.y + x[2] * b.z + x[3] * b.w;
+    }
+  }
+  s0 = hq_wave_sum(s0);
+  s1 = hq_wave_sum(s1);
+  if (lane == 0) *reinterpret_cast<float2*>(logits + 2 * (size_t)row) = make_float2(s0 + bias[0], s1 + bias[1]);
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void span_bwd_kernel(const uint16_t* __restrict__ seq, const float* __restrict__ w,
+                                                       const float* __restrict__ g, uint16_t* __restrict__ dseq,
+                                                       float* __restrict__ part, int T, int H) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float acc[2][NCH][4];
+  float w0[NCH][4], w1[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    const float4 a = col < H ? *reinterpret_cast<const float4*>(w + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 b = col < H ? *reinterpret_cast<const float4*>(w + H + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+    w0[c][0] = a.x; w0[c][1] = a.y; w0[c][2] = a.z; w0[c][3] = a.w;
+    w1[c][0] = b.x; w1[c][1] = b.y; w1[c][2] = b.z; w1[c][3] = b.w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { acc[0][c][i] = 0.f; acc[1][c][i] = 0.f; }
+  }
+  const int row0 = blockIdx.x * kWaves * kRowsPerWave;
+  for (int r = 0; r < kRowsPerWave; ++r) {
+    const int row = row0 + r * kWaves + wave;
+    if (row >= T) break;
+    const float2 gg = *reinterpret_cast<const float2*>(g + 2 * (size_t)row);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 256 + lane * 4;
+      if (col < H) {
+        float x[4], d[4];
+        hq_unpack4(*reinterpret_cast<const uint2*>(seq + (size_t)row * H + col), x);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[0][c][i] += gg.x * x[i];
+          acc[1][c][i] += gg.y * x[i];
+          d[i] = gg.x * w0[c][i] + gg.y * w1[c][i];
+        }
+        *reinterpret_cast<uint2*>(dseq + (size_t)row * H + col) = hq_pack4(d);
+      }
+    }
+  }
+  block_partials<NCH, 2>(acc, lds, part, H);
+}
+
 template <int NCH>
 __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ pids,
                                                         const int64_t* __restrict__ tids, const uint16_t* __restrict__ ww,
@@ -540,4 +611,21 @@ void hq_bias_grad(const uint16_t* dy, float* part, HqOuts outs, int T, int N, bo
 
 void hq_colsum(const float* part, int P, int N, float* out, bool accumulate, hipStream_t s) {
   colsum(part, P, N, HqOuts{{out, nullptr, nullptr, nullptr}}, N, accumulate, s);
+}
+
+void hq_span_fwd(const uint16_t* seq, const float* w, const float* b, float* logits, int T, int H, hipStream_t s) {
+  dispatch_nch(H, [&](auto nch) {
+    hipLaunchKernelGGL(span_fwd_kernel<decltype(nch)::value>, dim3((T + kWaves - 1) / kWaves), dim3(256), 0, s, seq, w, b,
+                       logits, T, H);
+  });
+}
+
+void hq_span_bwd(const uint16_t* seq, const float* w, const float* g, uint16_t* dseq, float* part, float* dw, int T,
+                 int H, bool accumulate, hipStream_t s) {
+  const int nb = hq_ln_bwd_partials(T);
+  dispatch_nch(H, [&](auto nch) {
+    hipLaunchKernelGGL(span_bwd_kernel<decltype(nch)::value>, dim3(nb), dim3(256), 4 * H * sizeof(float), s, seq, w, g,
+                       dseq, part, T, H);
+  });
+  colsum(part, nb, 2 * H, HqOuts{{dw, dw + H, nullptr, nullptr}}, H, accumulate, s);
 }

@@ -240,6 +240,29 @@ class _LayerFn(torch.autograd.Function):
         return dx, None, None, None, None
 
 
+class _SpanHeadFn(torch.autograd.Function):
+    """position_outputs (Linear(H, 2) over the sequence, reference ``model.py:30,54-58``) as one HIP
+    kernel each way: fp32 logits from the bf16 sequence; backward writes the bf16 sequence gradient
+    (rank-2 outer product) and dW partials (deterministic), db = Σ g."""
+
+    @staticmethod
+    def forward(ctx, seq, w, b):
+        from .._native import kernels
+        B, L, H = seq.shape
+        seq = seq.contiguous()
+        ctx.save_for_backward(seq, w)
+        return kernels().span_fwd(seq, w.detach().contiguous(), b.detach().contiguous()).view(B, L, 2)
+
+    @staticmethod
+    def backward(ctx, g):
+        from .._native import kernels
+        seq, w = ctx.saved_tensors
+        g = g.float().contiguous()
+        dw = torch.empty_like(w)
+        dseq = kernels().span_bwd(seq, w.detach().contiguous(), g, dw, False)
+        return dseq, dw, g.sum((0, 1))
+
+
 # ============================================================================================ model
 def _ensure_module(root: nn.Module, path: List[str]) -> nn.Module:
     mod = root
@@ -403,9 +426,12 @@ class BertForQuestionAnswering(nn.Module):
             raise NotImplementedError("head_mask is not supported by the fused encoder")
         seq = self.encode(input_ids, attention_mask, token_type_ids, position_ids)
         P = self.store.params
-        seq32 = seq.float()
-        pooled = torch.tanh(F.linear(seq32[:, 0], P["transformer.pooler.dense.weight"], P["transformer.pooler.dense.bias"]))
-        pos_logits = F.linear(seq32, P["position_outputs.weight"], P["position_outputs.bias"])
+        pooled = torch.tanh(F.linear(seq[:, 0].float(), P["transformer.pooler.dense.weight"],
+                                     P["transformer.pooler.dense.bias"]))
+        if seq.is_cuda and seq.dtype == torch.bfloat16:  # fused span head straight from bf16 (no fp32 copy)
+            pos_logits = _SpanHeadFn.apply(seq, P["position_outputs.weight"], P["position_outputs.bias"])
+        else:
+            pos_logits = F.linear(seq.float(), P["position_outputs.weight"], P["position_outputs.bias"])
         start_logits, end_logits = pos_logits.split(1, dim=-1)
         cls_in = F.dropout(pooled, self.config.hidden_dropout_prob, self.training)
         cls = F.linear(cls_in, P["classifier.1.weight"], P["classifier.1.bias"])

@@ -85,10 +85,11 @@ def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale
 
 # --------------------------------------------------------------------------------------- linear
 # Which projection GEMMs run on the hand-written MFMA NT kernel (gemm.hip) instead of hipBLASLt.
-#   HQ_GEMM=auto (default): the GEMMs whose epilogue fuses an elementwise pass — FFN1 + GELU and
+#   HQ_GEMM=auto (default): the GEMMs whose epilogue fuses an elementwise pass — FFN1 + GELU,
 #     FFN2-dgrad + dGELU + FFN1 bias-grad (1.04x / 1.34x vs hipBLASLt + separate kernel at b256,
-#     profiles/) — when the 256-row tile grid fills the 256 CUs to >= 85 %.  Plain projections stay
-#     on hipBLASLt with the shipped TunableOp picks, which measured 3-15 % faster than this kernel;
+#     profiles/) and the QKV dgrad + residual-gradient add (torch.addmm first copies the residual
+#     into the output: +56 µs at b256) — when the 256-row tile grid fills the 256 CUs to >= 85 %.
+#     Plain projections stay on hipBLASLt with the shipped TunableOp picks (3-15 % faster here);
 #   HQ_GEMM=mfma: every supported shape;  HQ_GEMM=blas: none.
 _EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID = range(5)
 _GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
@@ -112,7 +113,7 @@ def _mfma(M: int, N: int, K: int, kind: str = "plain") -> bool:
         return True
     tiles = (M // 256) * (N // bn)
     fill = tiles / (-(-tiles // _CUS) * _CUS)
-    return fill >= 0.85 and kind in ("dgelu", "gelu")
+    return fill >= 0.85 and kind in ("dgelu", "gelu", "resid")
 
 
 def linear_fwd(x, w, b, b32=None):
@@ -155,7 +156,7 @@ def linear_dgrad(dy, w, wt=None):
 def linear_dgrad_add(dy, w, resid, wt=None):
     """resid + dy·W (fuses the residual-gradient add)."""
     if dy.is_cuda:
-        if wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1]):
+        if wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1], "resid"):
             return _k().gemm_nt(dy, wt, _EPI_RESID, resid=resid)
         return torch.addmm(resid, dy, w)
     return ref.linear_dgrad_add(dy, w, resid)

@@ -197,3 +197,22 @@ def test_fp8_quantize_and_linear(cuda):
     ref = x.float() @ w.float().t() + b.float()
     rel = ((y.float() - ref).norm() / ref.norm()).item()
     assert rel < 0.06, rel
+
+
+@pytest.mark.gpu
+def test_span_head_fwd_bwd(cuda):
+    k = _native.kernels()
+    T, H = 1000, 768
+    seq = torch.randn(T, H, device=cuda).bfloat16()
+    w = torch.randn(2, H, device=cuda) * 0.05
+    b = torch.randn(2, device=cuda)
+    logits = k.span_fwd(seq, w, b)
+    ref = seq.float() @ w.t() + b
+    torch.testing.assert_close(logits, ref, atol=2e-3, rtol=2e-3)
+    g = torch.randn(T, 2, device=cuda)
+    dw = torch.zeros(2, H, device=cuda)
+    dseq = k.span_bwd(seq, w, g, dw, False)
+    torch.testing.assert_close(dseq.float(), g @ w, atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(dw, g.t() @ seq.float(), atol=2e-2, rtol=1e-3)
+    k.span_bwd(seq, w, g, dw, True)
+    torch.testing.assert_close(dw, 2 * (g.t() @ seq.float()), atol=4e-2, rtol=1e-3)
