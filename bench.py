@@ -22,7 +22,7 @@ METRIC = "samples/sec (whole node) BERT-base QA fine-tune seq=384 at 1/2/4/8 MI3
 # The reference publishes no numbers; BASELINE.md's "baseline to beat" is the reference recipe re-run
 # on the same MI355X (HF BertModel + its QA heads/loss, autocast bf16 for apex O1, AdamW, clip):
 # tools/ref_recipe_bench.py --batch 256 --attn sdpa (the faster of its two attention paths) = 1611.65.
-BASELINE_VALUE = 1611.65
+BASELINE_VALUE = 1611.65  # per GPU; for N GPUs the baseline is taken as N x this (ideal reference scaling)
 
 
 def parse():
@@ -138,7 +138,7 @@ def main():
     flops_per_sample = 6 * enc_linear * L + 12 * L * L * H * NL  # SURVEY §6.2 model
     out = {"metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": (round(value / BASELINE_VALUE, 4) if BASELINE_VALUE else None), "dtype": args.precision,
+           "vs_baseline": (round(value / (BASELINE_VALUE * world), 4) if BASELINE_VALUE else None), "dtype": args.precision,
            "data": "synthetic (dummy-QA generator, random-init weights)",
            "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": L,
                       "parallelism": f"dp{world}", "allreduce_dtype": args.allreduce_dtype,

@@ -389,6 +389,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
       .def("allreduce_bf16", &HqReducer::allreduce_bf16, py::call_guard<py::gil_scoped_release>())
       .def("broadcast", &HqReducer::broadcast, py::call_guard<py::gil_scoped_release>())
       .def("wait", &HqReducer::wait)
+      .def("fence_from", &HqReducer::fence_from)
       .def("synchronize", &HqReducer::synchronize, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("comm_stream", &HqReducer::comm_stream)
       .def_property_readonly("rank", &HqReducer::rank)

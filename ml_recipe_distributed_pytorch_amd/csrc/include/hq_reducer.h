@@ -18,6 +18,8 @@ class HqReducer {
   void allreduce_bf16(int64_t ptr_f32, int64_t scratch_bf16, int64_t count, int64_t compute_stream);
   void broadcast(int64_t ptr, int64_t count, int dtype, int root, int64_t compute_stream);
   void wait(int64_t compute_stream);
+  // comm stream waits for all work issued so far on `stream` (e.g. a side stream computing grads)
+  void fence_from(int64_t stream);
   void synchronize();
   int64_t comm_stream() const { return (int64_t)stream_; }
   int rank() const { return rank_; }
@@ -26,7 +28,6 @@ class HqReducer {
  private:
   static constexpr int kEvents = 64;
   void* next_event();
-  void fence_from(int64_t compute_stream);
   int rank_, world_, device_;
   void* comm_ = nullptr;
   void* stream_ = nullptr;

@@ -19,6 +19,7 @@ Capability parity with the reference model (``modules/model/model/model.py:13-73
 from __future__ import annotations
 
 import math
+import os
 from typing import Callable, Dict, List, Optional
 
 import torch
@@ -211,30 +212,40 @@ class _LayerFn(torch.autograd.Function):
         G = (lambda k: st.view(p + k, "grad")) if trainable else (lambda k: None)
         W = lambda k: st.view(p + k)  # noqa: E731
         WT = lambda k: st.view_t(p + k)  # noqa: E731  (Wᵀ working copy, GPU only)
+        side = m.grad_side_stream if dh2.is_cuda else None
+
+        def wgrad(dy, xin, gw, gb):  # dW (+db) — on the side stream when enabled (overlaps the dgrad chain)
+            if not trainable:
+                return
+            if side is None:
+                ops.linear_wgrad(dy, xin, gw, gb, acc)
+                return
+            side.wait_stream(torch.cuda.current_stream())
+            dy.record_stream(side)
+            xin.record_stream(side)
+            with torch.cuda.stream(side):
+                ops.linear_wgrad(dy, xin, gw, gb, acc)
         Wm = lambda k: st.view(p + k, "master")  # noqa: E731
         dh2 = dh2.contiguous()
 
         # --- FFN block ------------------------------------------------------------------------
         dz2, da2 = ops.ln_bwd(dh2, None, z2, Wm("output.LayerNorm.weight"), m2, r2, ctx.ph, info.seed, op0 + 2,
                               G("output.LayerNorm.weight"), G("output.LayerNorm.bias"), G("output.dense.bias"), acc)
-        if trainable:
-            ops.linear_wgrad(da2, act, G("output.dense.weight"), None, acc)
+        wgrad(da2, act, G("output.dense.weight"), None)
         dpre = ops.linear_dgrad_gelu(da2, W("output.dense.weight"), pre, G("intermediate.dense.bias"), acc,
                                      wt=WT("output.dense.weight"))
-        if trainable:
-            ops.linear_wgrad(dpre, h1, G("intermediate.dense.weight"), None, acc)
+        wgrad(dpre, h1, G("intermediate.dense.weight"), None)
         dh1_ffn = ops.linear_dgrad(dpre, W("intermediate.dense.weight"), wt=WT("intermediate.dense.weight"))
         # --- attention block ------------------------------------------------------------------
         dz1, da1 = ops.ln_bwd(dz2, dh1_ffn, z1, Wm("attention.output.LayerNorm.weight"), m1, r1, ctx.ph, info.seed,
                               op0 + 1, G("attention.output.LayerNorm.weight"), G("attention.output.LayerNorm.bias"),
                               G("attention.output.dense.bias"), acc)
-        if trainable:
-            ops.linear_wgrad(da1, ctxv, G("attention.output.dense.weight"), None, acc)
+        wgrad(da1, ctxv, G("attention.output.dense.weight"), None)
         dctx = ops.linear_dgrad(da1, W("attention.output.dense.weight"), wt=WT("attention.output.dense.weight"))
         dqkv = ops.attn_bwd(dctx, qkv, ctxv, lse, key_bias, ctx.bits, B, L, nh, ctx.pa, info.seed, op0, ctx.scale)
         ctx.bits = None
+        wgrad(dqkv, x, G("qkv.weight"), G("qkv.bias"))
         if trainable:
-            ops.linear_wgrad(dqkv, x, G("qkv.weight"), G("qkv.bias"), acc)
             m._group_ready(grp)
         dx = ops.linear_dgrad_add(dqkv, W("qkv.weight"), dz1, wt=WT("qkv.weight"))
         return dx, None, None, None, None
@@ -295,6 +306,9 @@ class BertForQuestionAnswering(nn.Module):
             _ensure_module(self, path).register_parameter(leaf, prm)
         emb = _ensure_module(self, ["transformer", "embeddings"])
         emb.register_buffer("position_ids", torch.arange(config.max_position_embeddings).unsqueeze(0))
+        # HQ_WGRAD_STREAM=1: weight-gradient GEMMs on a side stream, overlapping the dgrad/attention chain
+        self.grad_side_stream = None
+        self._want_side_stream = os.environ.get("HQ_WGRAD_STREAM", "0") == "1"
         self._head_params = [prm for n, prm in self.store.params.items() if not n.startswith("transformer.encoder")
                              and not n.startswith("transformer.embeddings")]
         self._fresh: Dict[str, bool] = {}
@@ -330,6 +344,10 @@ class BertForQuestionAnswering(nn.Module):
         if probe.device.type == "cuda":
             from ..ops.tuning import enable_tuned_gemms
             enable_tuned_gemms()
+            if self._want_side_stream and self.grad_side_stream is None:
+                self.grad_side_stream = torch.cuda.Stream(device=probe.device)
+        else:
+            self.grad_side_stream = None
         for mod in self.modules():
             for k, b in list(mod._buffers.items()):
                 if b is not None:

@@ -148,13 +148,18 @@ class GradReducer:
         self.stats["buckets_launched"] += 1
         self.stats["bytes"] += b.numel * (2 if self.allreduce_dtype == "bf16" else 4)
         self._seq_hash = (self._seq_hash * 1_000_003 + b.index * 65_537 + b.numel) & 0x7FFFFFFFFFFFFFFF
+        side = getattr(self.model, "grad_side_stream", None)
         if self._native is not None:
             stream = torch.cuda.current_stream().cuda_stream
+            if side is not None:  # weight grads computed on the side stream
+                self._native.fence_from(side.cuda_stream)
             if self.allreduce_dtype == "bf16":
                 self._native.allreduce_bf16(view.data_ptr(), self._scratch[b.start:b.end].data_ptr(), b.numel, stream)
             else:
                 self._native.allreduce_f32(view.data_ptr(), b.numel, stream)
         else:
+            if side is not None:
+                torch.cuda.current_stream().wait_stream(side)
             backend = dist.get_backend(self.group)
             if backend == "nccl":
                 b.work = dist.all_reduce(view, op=dist.ReduceOp.AVG, group=self.group, async_op=True)

@@ -120,6 +120,9 @@ class TrainEngine:
 
     def _apply(self) -> StepResult:
         timer = self._timer
+        side = getattr(self.model, "grad_side_stream", None)
+        if side is not None:  # weight grads from the side stream must be complete
+            torch.cuda.current_stream().wait_stream(side)
         if self.reducer is not None:
             self.reducer.finalize()
         timer.mark("comm_wait")

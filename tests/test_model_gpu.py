@@ -20,22 +20,25 @@ def _inputs(B, L, V):
     return ids, ids > 0, tt
 
 
-@pytest.mark.parametrize("train,gemm", [(False, "auto"), (True, "auto"), (True, "mfma")])
-def test_tiny_model_gpu_matches_cpu(cuda, train, gemm):
+@pytest.mark.parametrize("train,gemm,side", [(False, "auto", False), (True, "auto", False), (True, "mfma", False),
+                                             (True, "auto", True)])
+def test_tiny_model_gpu_matches_cpu(cuda, train, gemm, side):
     """gemm="mfma" routes every projection (fwd + GELU epilogue, dgrad, residual and dGELU
     epilogues on the transposed weight copies) through the hand-written MFMA GEMM."""
     from ml_recipe_distributed_pytorch_amd import ops
     prev = ops.set_gemm_mode(gemm)
     try:
-        _tiny_parity(cuda, train, B=4 if gemm == "mfma" else 3)
+        _tiny_parity(cuda, train, B=4 if gemm == "mfma" else 3, side=side)
     finally:
         ops.set_gemm_mode(prev)
 
 
-def _tiny_parity(cuda, train, B):
+def _tiny_parity(cuda, train, B, side=False):
     cfg = get_config("bert-tiny-test")
     cpu = BertForQuestionAnswering(cfg, seed=0)
     gpu = copy.deepcopy(cpu).to(cuda)
+    if side:  # weight-grad GEMMs on the side stream (HQ_WGRAD_STREAM=1)
+        gpu.grad_side_stream = torch.cuda.Stream(device=cuda)
     cpu.train(train)
     gpu.train(train)
     ids, mask, tt = _inputs(B, 64, cfg.vocab_size)
@@ -55,6 +58,8 @@ def _tiny_parity(cuda, train, B):
     gpu.zero_grad()
     lc.backward()
     lg.backward()
+    if side:
+        torch.cuda.current_stream().wait_stream(gpu.grad_side_stream)
     gc, gg = cpu.store.grad, gpu.store.grad.cpu()
     rel = (gc - gg).norm() / gc.norm()
     assert rel.item() < 5e-2, f"grad arena rel err {rel.item():.3e}"
