@@ -21,23 +21,61 @@ _lock = threading.Lock()
 _cache = {}
 
 
-def _load(name: str):
+_DEBUG_DIR = os.path.join(_PKG_DIR, "csrc", "build", "debug")
+
+
+def _load(name: str, directory: str = _PKG_DIR):
     with _lock:
-        if name in _cache:
-            return _cache[name]
-        hits = sorted(glob.glob(os.path.join(_PKG_DIR, name + "*.so")))
+        ck = (name, directory)
+        if ck in _cache:
+            return _cache[ck]
+        hits = sorted(glob.glob(os.path.join(directory, name + "*.so")))
         if not hits:
-            _cache[name] = None
+            _cache[ck] = None
             return None
         import torch  # noqa: F401  (kernels lib resolves libamdhip64/librccl/libtorch from torch's lib dir)
         spec = importlib.util.spec_from_file_location(name, hits[0])
         mod = importlib.util.module_from_spec(spec)
         spec.loader.exec_module(mod)
-        _cache[name] = mod
+        _cache[ck] = mod
         return mod
 
 
+class _SyncedKernels:
+    """Debug-build proxy: every kernel entry point is followed by a device synchronisation, so an
+    ``HQ_DASSERT`` trap or a memory fault is reported against the op that caused it."""
+
+    def __init__(self, mod):
+        self._mod = mod
+
+    def __getattr__(self, name):
+        attr = getattr(self._mod, name)
+        if type(attr).__name__ != "builtin_function_or_method":
+            return attr
+
+        def call(*args, **kwargs):
+            import torch
+            out = attr(*args, **kwargs)
+            try:
+                torch.cuda.synchronize()
+            except RuntimeError as e:
+                raise RuntimeError(f"HIP kernel op {name!r} failed in the debug build: {e}") from e
+            return out
+
+        return call
+
+
+def debug_enabled() -> bool:
+    return os.environ.get("HQ_KERNELS_DEBUG", "0") == "1"
+
+
 def kernels():
+    if debug_enabled():
+        mod = _load("_hq_kernels", _DEBUG_DIR)
+        if mod is None:
+            raise RuntimeError("HQ_KERNELS_DEBUG=1 but the debug kernel library is not built. Run "
+                               "`python -m ml_recipe_distributed_pytorch_amd.csrc.build --kernels --debug`.")
+        return _SyncedKernels(mod)
     mod = _load("_hq_kernels")
     if mod is None:
         raise RuntimeError(

@@ -53,7 +53,8 @@ std::vector<Tensor> embed_fwd(Tensor ids, Tensor pids, Tensor tids, Tensor ww, T
   auto rstd = at::empty({T}, gamma.options());
   hq_embed_fwd(ptr<int64_t>(ids), ptr<int64_t>(pids), ptr<int64_t>(tids), ptr<uint16_t>(ww), ptr<uint16_t>(wp),
                ptr<uint16_t>(wt), ptr<float>(gamma), ptr<float>(beta), ptr<uint16_t>(y), ptr<float>(mean), ptr<float>(rstd),
-               (int)T, (int)H, (float)eps, (float)p, u32(seed), u32(opid), cur_stream());
+               (int)T, (int)H, (float)eps, (float)p, u32(seed), u32(opid), (int)ww.size(0), (int)wp.size(0),
+               (int)wt.size(0), cur_stream());
   return {y, mean, rstd};
 }
 
@@ -84,7 +85,7 @@ void embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tenso
   hq_embed_bwd(ptr<uint16_t>(dy), ptr<int64_t>(ids), ptr<int64_t>(pids), ptr<int64_t>(tids), ptr<uint16_t>(ww),
                ptr<uint16_t>(wp), ptr<uint16_t>(wt), ptr<float>(gamma), ptr<float>(mean), ptr<float>(rstd),
                ptr<float>(g_word), ptr<float>(g_pos), t0, ptr<float>(part), o, (int)T, (int)H, n_types, (int)pad_word,
-               (int)pad_pos, (float)p, u32(seed), u32(opid), accumulate, s);
+               (int)pad_pos, (float)p, u32(seed), u32(opid), accumulate, (int)ww.size(0), (int)wp.size(0), s);
 }
 
 // ------------------------------------------------------------------ residual + dropout + LayerNorm

@@ -4,7 +4,7 @@
   ``hipcc --offload-arch=gfx950`` and linked against torch + librccl.
 * ``_hq_host<ext>.so``    — ``host/*.cpp`` (pure C++17 + pybind11, g++), no GPU dependency.
 
-Usage: ``python -m ml_recipe_distributed_pytorch_amd.csrc.build [--host] [--kernels] [-j N] [--force]``
+Usage: ``python -m ml_recipe_distributed_pytorch_amd.csrc.build [--host] [--kernels] [-j N] [--force] [--debug]``
 """
 from __future__ import annotations
 
@@ -21,6 +21,7 @@ from typing import List
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 BUILD = os.path.join(HERE, "build")
+DEBUG_DIR = os.path.join(BUILD, "debug")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
@@ -66,11 +67,16 @@ def _torch_paths():
     return incs, libdir
 
 
-def build_kernels(jobs: int = 8, force: bool = False, verbose: bool = True) -> str:
+def build_kernels(jobs: int = 8, force: bool = False, verbose: bool = True, debug: bool = False) -> str:
+    """Release build → ``<pkg>/_hq_kernels<ext>``.  ``debug=True`` adds ``-DHQ_DEBUG`` (device-side
+    ``HQ_DASSERT`` bounds checks, host line info) and writes ``csrc/build/debug/_hq_kernels<ext>``,
+    which ``_native`` loads instead when ``HQ_KERNELS_DEBUG=1``."""
     incs, torch_lib = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I" + os.path.join(HERE, "include"),
               "-D__HIP_PLATFORM_AMD__=1", "-Wno-unused-result"]
+    if debug:
+        common += ["-DHQ_DEBUG=1", "-g1"]
     kernel_srcs = sorted(os.path.join(HERE, "kernels", f) for f in os.listdir(os.path.join(HERE, "kernels"))
                          if f.endswith(".hip"))
     runtime_srcs = sorted(os.path.join(HERE, "runtime", f) for f in os.listdir(os.path.join(HERE, "runtime"))
@@ -86,6 +92,9 @@ def build_kernels(jobs: int = 8, force: bool = False, verbose: bool = True) -> s
     with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(lambda a: _compile(a[0], a[1], a[2], force), jobs_list))
     out = os.path.join(PKG, "_hq_kernels" + EXT)
+    if debug:
+        os.makedirs(DEBUG_DIR, exist_ok=True)
+        out = os.path.join(DEBUG_DIR, "_hq_kernels" + EXT)
     link = [HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out + ".tmp"] + objs + [
         "-L" + torch_lib, "-Wl,-rpath," + torch_lib, "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
         "-ltorch_python", "-L" + os.path.join(ROCM, "lib"), "-lamdhip64", "-lrccl"]
@@ -131,12 +140,13 @@ def main(argv=None):
     ap.add_argument("--kernels", action="store_true")
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--force", action="store_true")
+    ap.add_argument("--debug", action="store_true", help="kernels with HQ_DASSERT checks into csrc/build/debug/")
     a = ap.parse_args(argv)
     both = not a.host and not a.kernels
     if a.host or both:
         build_host(a.j, a.force)
     if a.kernels or both:
-        build_kernels(a.j, a.force)
+        build_kernels(a.j, a.force, debug=a.debug)
 
 
 if __name__ == "__main__":

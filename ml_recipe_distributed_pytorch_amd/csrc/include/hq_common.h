@@ -132,6 +132,22 @@ __device__ __forceinline__ void hq_keep4(uint32_t idx0, uint32_t key, uint32_t t
   }
 }
 
+// Device-side assertions for the debug build only (`python -m ...csrc.build --debug` defines
+// HQ_DEBUG); the release build compiles them to nothing.  A failing assertion prints its site and
+// traps, so the faulting kernel is named by the runtime instead of corrupting memory silently.
+#ifdef HQ_DEBUG
+#define HQ_DASSERT(cond)                                                                       \
+  do {                                                                                         \
+    if (!(cond)) {                                                                             \
+      printf("HQ_DASSERT %s:%d block (%d,%d) thread %d: %s\n", __FILE__, __LINE__, (int)blockIdx.x, \
+             (int)blockIdx.y, (int)threadIdx.x, #cond);                                        \
+      __builtin_trap();                                                                        \
+    }                                                                                          \
+  } while (0)
+#else
+#define HQ_DASSERT(cond) ((void)0)
+#endif
+
 #define HQ_CHECK(x)                                                                       \
   do {                                                                                    \
     hipError_t e_ = (x);                                                                  \

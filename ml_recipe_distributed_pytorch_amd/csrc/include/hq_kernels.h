@@ -21,11 +21,12 @@ void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const
                uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s);
 void hq_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww, const uint16_t* wp,
                   const uint16_t* wt, const float* gamma, const float* beta, uint16_t* y, float* mean, float* rstd, int T,
-                  int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s);
+                  int H, float eps, float p, uint32_t seed, uint32_t opid, int V, int P, int NTY, hipStream_t s);
 void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww,
                   const uint16_t* wp, const uint16_t* wt, const float* gamma, const float* mean, const float* rstd,
                   float* g_word, float* g_pos, float* g_type, float* part, HqOuts outs, int T, int H, int n_types,
-                  int pad_word, int pad_pos, float p, uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s);
+                  int pad_word, int pad_pos, float p, uint32_t seed, uint32_t opid, bool accumulate, int V, int P,
+                  hipStream_t s);
 void hq_gelu_fwd(const uint16_t* pre, uint16_t* out, size_t n, hipStream_t s);
 void hq_gelu_bwd(const uint16_t* dout, const uint16_t* pre, uint16_t* dpre, float* part, HqOuts outs, int T, int N,
                  bool accumulate, hipStream_t s);

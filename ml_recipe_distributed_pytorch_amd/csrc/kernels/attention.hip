@@ -125,6 +125,26 @@ __device__ __forceinline__ bf16x8_t prescale8(const bf16x8_t& q, float c) {
 
 __device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
 
+// Packed-f32 pair (v_pk_add/mul/fma_f32 on gfx950: two lanes' worth of f32 work per VALU issue).
+typedef float f2_t __attribute__((ext_vector_type(2)));
+
+// lane ^ 32 exchange without LDS: v_permlane32_swap hands each half the other half's value.
+__device__ __forceinline__ float xor32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// max over the 16 accumulator registers as a v_max3 chain
+__device__ __forceinline__ float max16(const f32x16_t& a) {
+  float m = fmaxf(fmaxf(a[0], a[1]), a[2]);
+#pragma unroll
+  for (int r = 3; r < 15; r += 2) m = fmaxf(fmaxf(m, a[r]), a[r + 1]);
+  return fmaxf(m, a[15]);
+}
+
 // Cooperative copy of rows [0, Lp) of a [*, ld] bf16 matrix (64 columns starting at src) into a
 // [Lp][64] LDS image; rows >= L are zero.  Each thread issues all its 16-B loads before any store.
 template <int NT, bool SCALE = false>
@@ -160,19 +180,23 @@ __device__ __forceinline__ void load_head(uint16_t* dst, const uint16_t* src, si
 }
 
 // ============================================================================ forward
-template <int NWB, bool DROP, bool EVEN>
+// NT > 0: compile-time count of 32-key tiles (L = 32·NT, the common BERT lengths): the key loop is
+// fully unrolled so every LDS address is base + immediate.  NT = 0: runtime count, rolled loop.
+template <int NWB, bool DROP, bool EVEN, int NT>
 __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __restrict__ qkv,
                                                             const float* __restrict__ key_bias,
                                                             uint16_t* __restrict__ ctx, float* __restrict__ lse,
                                                             uint16_t* __restrict__ mbits, int L, int nh, float c_scale,
                                                             uint32_t key, uint32_t thr, float kscale) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int Lp = (L + 31) & ~31, n32 = Lp >> 5;
+  constexpr int UNR = NT > 0 ? NT : 1;
+  const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
   uint16_t* sK = reinterpret_cast<uint16_t*>(smem);
   uint16_t* sV = sK + Lp * D;
   float* sB = reinterpret_cast<float*>(sV + Lp * D);
   const int H = nh * D, ld = 3 * H;
   const int bh = blockIdx.x, b = bh / nh, h = bh % nh;
+  HQ_DASSERT(L > 0 && L <= 512 && (NT == 0 || L == NT * 32));
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, hh = lane >> 5;
   const int qs = blockIdx.y * NWB + wave;  // 32-query subtile
   const int qi = qs * 32 + (lane & 31);
@@ -196,10 +220,12 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
   for (int d = 0; d < 2; ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
+  float m_run = -INFINITY;
+  f2_t l2 = {0.f, 0.f};  // running row sum, two partial sums (packed adds)
   const uint32_t row_idx = ((uint32_t)bh * L + (uint32_t)min(qi, L - 1)) * (uint32_t)L;
   uint16_t* my_bits = mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane;
 
+#pragma unroll UNR
   for (int kt = 0; kt < n32; ++kt) {
     f32x16_t acc;
 #pragma unroll
@@ -209,30 +235,33 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) acc = mfma32(row8(sK, kt * 32, lo_, s), qf[s], acc);
-    float sc[16];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sc[r] = acc[r];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[r]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mx = xor32_max(max16(acc));
     if (__any(mx > m_run)) {  // exact rescale skip: α = 1 for every lane whose max did not grow
       const float m_new = fmaxf(m_run, mx);
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
       m_run = m_new;
-      l_run *= alpha;
+      const f2_t a2 = {alpha, alpha};
+      l2 *= a2;
 #pragma unroll
       for (int d = 0; d < 2; ++d)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+        for (int r = 0; r < 16; r += 2) {
+          f2_t v = {o[d][r], o[d][r + 1]};
+          v *= a2;
+          o[d][r] = v.x; o[d][r + 1] = v.y;
+        }
     }
-    float rs = 0.f;
+    float sc[16];
+    const f2_t m2 = {m_run, m_run};
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      sc[r] = __builtin_amdgcn_exp2f(sc[r] - m_run);
-      rs += sc[r];
+    for (int r = 0; r < 16; r += 2) {
+      f2_t v = {acc[r], acc[r + 1]};
+      v -= m2;
+      sc[r] = __builtin_amdgcn_exp2f(v.x);
+      sc[r + 1] = __builtin_amdgcn_exp2f(v.y);
+      const f2_t e = {sc[r], sc[r + 1]};
+      l2 += e;  // the softmax denominator counts every key; dropout only thins the P·V product
     }
-    l_run += rs;
     if constexpr (DROP) {
       // keep bits straight from the integer compares; the 1/(1-p) scale is applied once to O at the end
       uint32_t bits = 0;
@@ -244,9 +273,9 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
         for (int g = 0; g < 4; ++g)
 #pragma unroll
           for (int ip = 0; ip < 2; ++ip) {
-            const uint32_t h = hq_mix24(pk ^ (uint32_t)(4 * g + ip));
+            const uint32_t hsh = hq_mix24(pk ^ (uint32_t)(4 * g + ip));
             const int r = 4 * g + 2 * ip;
-            const bool k0 = (h & 0xFFFFu) >= thr, k1 = (h >> 16) >= thr;
+            const bool k0 = (hsh & 0xFFFFu) >= thr, k1 = (hsh >> 16) >= thr;
             sc[r] = k0 ? sc[r] : 0.f;
             sc[r + 1] = k1 ? sc[r + 1] : 0.f;
             bits |= ((uint32_t)k0 << r) | ((uint32_t)k1 << (r + 1));
@@ -272,7 +301,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
       for (int d = 0; d < 2; ++d) o[d] = mfma32(tr8(sV, kt * 32, lo_, s, d), pb, o[d]);
     }
   }
-  const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  const float l_tot = xor32_sum(l2.x + l2.y);
   const float inv = (DROP ? kscale : 1.f) / l_tot;
   if (qi < L) {
     uint16_t* out = ctx + ((size_t)b * L + qi) * H + h * D;
@@ -288,7 +317,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
 }
 
 // ============================================================================ backward: dQ (+ δ)
-template <int NWB, bool DROP>
+template <int NWB, bool DROP, int NT>
 __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv,
                                                                const uint16_t* __restrict__ dctx,
                                                                const uint16_t* __restrict__ ctx,
@@ -298,12 +327,14 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
                                                                float* __restrict__ delta, uint16_t* __restrict__ dqkv,
                                                                int L, int nh, float c_scale, float scale, float kscale) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int Lp = (L + 31) & ~31, n32 = Lp >> 5;
+  constexpr int UNR = NT > 0 ? NT : 1;
+  const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
   uint16_t* sK = reinterpret_cast<uint16_t*>(smem);
   uint16_t* sV = sK + Lp * D;
   float* sB = reinterpret_cast<float*>(sV + Lp * D);
   const int H = nh * D, ld = 3 * H;
   const int bh = blockIdx.x, b = bh / nh, h = bh % nh;
+  HQ_DASSERT(L > 0 && L <= 512);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, hh = lane >> 5;
   const int qs = blockIdx.y * NWB + wave;
   const int qi = qs * 32 + (lane & 31);
@@ -329,7 +360,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
   load_head<NWB * 64>(sK, base + H, ld, L, Lp);
   load_head<NWB * 64>(sV, base + 2 * H, ld, L, Lp);
   for (int t = threadIdx.x; t < Lp; t += NWB * 64) sB[t] = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -INFINITY;
-  const float dlt = dpart + __shfl_xor(dpart, 32, 64);  // δ = rowsum(dO·O) over all 64 dims
+  const float dlt = xor32_sum(dpart);  // δ = rowsum(dO·O) over all 64 dims
   const float lq = qok ? lse[(size_t)bh * L + qi] * LOG2E : INFINITY;
   if (qok && hh == 0) delta[(size_t)bh * L + qi] = dlt;
   __syncthreads();
@@ -344,6 +375,8 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
     for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
   const uint16_t* my_bits = mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane;
 
+  const f2_t dl2 = {dlt, dlt};
+#pragma unroll UNR
   for (int kt = 0; kt < n32; ++kt) {
     f32x16_t s_acc, p_acc;
 #pragma unroll
@@ -367,10 +400,12 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
     }
     float ds[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float P = __builtin_amdgcn_exp2f(s_acc[r]);
-      const float mk = ((bits >> r) & 1u) ? ks : 0.f;
-      ds[r] = P * fmaf(p_acc[r], mk, -dlt);
+    for (int r = 0; r < 16; r += 2) {  // dS = P·(dP·mask − δ), two elements per packed FMA / multiply
+      const f2_t P = {__builtin_amdgcn_exp2f(s_acc[r]), __builtin_amdgcn_exp2f(s_acc[r + 1])};
+      const f2_t mk = {((bits >> r) & 1u) ? ks : 0.f, ((bits >> (r + 1)) & 1u) ? ks : 0.f};
+      const f2_t dp = {p_acc[r], p_acc[r + 1]};
+      const f2_t v = (dp * mk - dl2) * P;
+      ds[r] = v.x; ds[r + 1] = v.y;
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -392,7 +427,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
 }
 
 // ============================================================================ backward: dK, dV
-template <int NWB, bool DROP>
+template <int NWB, bool DROP, int NT>
 __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv,
                                                                  const uint16_t* __restrict__ dctx,
                                                                  const float* __restrict__ lse,
@@ -402,14 +437,17 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
                                                                  uint16_t* __restrict__ dqkv, int L, int nh,
                                                                  float c_scale, float scale, float kscale) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int Lp = (L + 31) & ~31, n32 = Lp >> 5;
+  constexpr int UNR = NT > 0 ? (NWB >= 12 ? 4 : NT) : 1;  // full unroll spills at 12 waves
+  const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
   uint16_t* sQ = reinterpret_cast<uint16_t*>(smem);
   uint16_t* sO = sQ + Lp * D;  // dO
   float* sL = reinterpret_cast<float*>(sO + Lp * D);  // lse·log2e (+inf past L)
   float* sD = sL + Lp;                                // δ
   const int H = nh * D, ld = 3 * H;
   const int bh = blockIdx.x, b = bh / nh, h = bh % nh;
+  HQ_DASSERT(L > 0 && L <= 512 && (NT == 0 || L == NT * 32));
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, hh = lane >> 5;
+  uint16_t* sW = reinterpret_cast<uint16_t*>(sD + Lp) + wave * 64;  // this wave's keep-bit words of one tile
   const int ks_idx = blockIdx.y * NWB + wave;  // 32-key subtile
   const int kj = ks_idx * 32 + (lane & 31);
   const bool kok = kj < L;
@@ -436,11 +474,39 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
   // Two passes over the queries (dV, then dK with S recomputed): +25 % MFMA, but the live set of a
   // single pass (K/V fragments + dV/dK accumulators + S/dP tiles ≈ 200 VGPRs) spills at the 168-VGPR
   // budget of 12 waves per workgroup.
-  // forward bit layout: word of fwd-lane l' = q + 32·hh', bit r' with acc_row(r', hh') = key-in-subtile
+  // Forward bit layout: the word of fwd-lane l' = q + 32·hh' holds bit r' for key acc_row(r', hh').  This
+  // lane (key krel) needs, for its 16 query rows acc_row(r, hh) = 8g + 4hh + i, bit r_f of the words of
+  // fwd-lanes 8g + 4hh + i + 32·hh_f: four consecutive words per g, i.e. one 8-byte LDS read per g.
   const int krel = lane & 31;
   const int hh_f = (krel >> 2) & 1;
   const int r_f = (krel & 3) + 4 * (krel >> 3);
   const float ksc = DROP ? kscale : 1.f;
+  const uint16_t* wsrc = sW + 4 * hh + 32 * hh_f;
+  auto tile_mask = [&](int qt, f2_t* mk) {  // mk[r/2] = {mask(r), mask(r+1)} ∈ {0, 1/(1-p)}
+    if constexpr (DROP) {
+      sW[lane] = mbits[(((size_t)bh * n32 + qt) * n32 + ks_idx) * 64 + lane];
+      asm volatile("" ::: "memory");  // the u64 reads below alias these u16 stores (no TBAA reordering)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const uint64_t w = *reinterpret_cast<const uint64_t*>(wsrc + 8 * g);
+        const uint32_t lo = (uint32_t)w >> r_f, hi = (uint32_t)(w >> 32) >> r_f;
+        mk[2 * g] = f2_t{(lo & 1u) ? ksc : 0.f, ((lo >> 16) & 1u) ? ksc : 0.f};
+        mk[2 * g + 1] = f2_t{(hi & 1u) ? ksc : 0.f, ((hi >> 16) & 1u) ? ksc : 0.f};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mk[i] = f2_t{1.f, 1.f};
+    }
+  };
+  const f2_t kb2 = {kb, kb};
+  auto score_init = [&](int qt, f32x16_t& s_acc) {  // S' = c·q·k + bias − lse (key on the lane)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float4 l4 = *reinterpret_cast<const float4*>(sL + qt * 32 + 8 * g + 4 * hh);
+      const f2_t a = kb2 - f2_t{l4.x, l4.y}, c = kb2 - f2_t{l4.z, l4.w};
+      s_acc[4 * g + 0] = a.x; s_acc[4 * g + 1] = a.y; s_acc[4 * g + 2] = c.x; s_acc[4 * g + 3] = c.y;
+    }
+  };
   uint16_t* out = dqkv + ((size_t)b * L + min(kj, L - 1)) * ld + h * D;
 
   // ------------------------------------------------------------------ pass 1: dVᵀ += dOᵀ·Pd
@@ -450,30 +516,23 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
     for (int d = 0; d < 2; ++d)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dv[d][r] = 0.f;
+#pragma unroll UNR
     for (int qt = 0; qt < n32; ++qt) {
       f32x16_t s_acc;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {  // S' = c·q·k + bias − lse (key on the lane, query in the register)
-        const float4 l4 = *reinterpret_cast<const float4*>(sL + qt * 32 + 8 * g + 4 * hh);
-        s_acc[4 * g + 0] = kb - l4.x; s_acc[4 * g + 1] = kb - l4.y;
-        s_acc[4 * g + 2] = kb - l4.z; s_acc[4 * g + 3] = kb - l4.w;
-      }
+      score_init(qt, s_acc);
 #pragma unroll
       for (int s = 0; s < 4; ++s) s_acc = mfma32(row8(sQ, qt * 32, lo_, s), kf[s], s_acc);
-      const uint32_t word = DROP ? (uint32_t)mbits[(((size_t)bh * n32 + qt) * n32 + ks_idx) * 64 + lane] : 0xFFFFu;
+      f2_t mk[8];
+      tile_mask(qt, mk);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         float pd[8];
 #pragma unroll
-        for (int gg = 0; gg < 2; ++gg) {
-          const int g = 2 * s + gg;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int r = 4 * g + i;
-            const uint32_t w = DROP ? (uint32_t)__shfl((int)word, acc_row(r, hh) + 32 * hh_f, 64) : 0xFFFFu;
-            const float mk = ((w >> r_f) & 1u) ? ksc : 0.f;
-            pd[4 * gg + i] = __builtin_amdgcn_exp2f(s_acc[r]) * mk;
-          }
+        for (int j = 0; j < 8; j += 2) {
+          const int r = 8 * s + j;
+          const f2_t P = {__builtin_amdgcn_exp2f(s_acc[r]), __builtin_amdgcn_exp2f(s_acc[r + 1])};
+          const f2_t v = P * mk[r >> 1];
+          pd[j] = v.x; pd[j + 1] = v.y;
         }
         const bf16x8_t pb = pack_b(pd, 0);
 #pragma unroll
@@ -497,14 +556,10 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
     for (int d = 0; d < 2; ++d)
 #pragma unroll
       for (int r = 0; r < 16; ++r) dk[d][r] = 0.f;
+#pragma unroll UNR
     for (int qt = 0; qt < n32; ++qt) {
       f32x16_t s_acc, p_acc;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 l4 = *reinterpret_cast<const float4*>(sL + qt * 32 + 8 * g + 4 * hh);
-        s_acc[4 * g + 0] = kb - l4.x; s_acc[4 * g + 1] = kb - l4.y;
-        s_acc[4 * g + 2] = kb - l4.z; s_acc[4 * g + 3] = kb - l4.w;
-      }
+      score_init(qt, s_acc);
 #pragma unroll
       for (int r = 0; r < 16; ++r) p_acc[r] = 0.f;
 #pragma unroll
@@ -512,7 +567,8 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
         s_acc = mfma32(row8(sQ, qt * 32, lo_, s), kf[s], s_acc);
         p_acc = mfma32(row8(sO, qt * 32, lo_, s), vf[s], p_acc);
       }
-      const uint32_t word = DROP ? (uint32_t)mbits[(((size_t)bh * n32 + qt) * n32 + ks_idx) * 64 + lane] : 0xFFFFu;
+      f2_t mk[8];
+      tile_mask(qt, mk);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         float ds[8];
@@ -520,14 +576,14 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
         for (int gg = 0; gg < 2; ++gg) {
           const int g = 2 * s + gg;
           const float4 d4 = *reinterpret_cast<const float4*>(sD + qt * 32 + 8 * g + 4 * hh);
-          const float dl[4] = {d4.x, d4.y, d4.z, d4.w};
+          const f2_t dl[2] = {f2_t{d4.x, d4.y}, f2_t{d4.z, d4.w}};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) {
+          for (int i = 0; i < 4; i += 2) {
             const int r = 4 * g + i;
-            const uint32_t w = DROP ? (uint32_t)__shfl((int)word, acc_row(r, hh) + 32 * hh_f, 64) : 0xFFFFu;
-            const float mk = ((w >> r_f) & 1u) ? ksc : 0.f;
-            const float P = __builtin_amdgcn_exp2f(s_acc[r]);
-            ds[4 * gg + i] = P * fmaf(p_acc[r], mk, -dl[i]);
+            const f2_t P = {__builtin_amdgcn_exp2f(s_acc[r]), __builtin_amdgcn_exp2f(s_acc[r + 1])};
+            const f2_t dp = {p_acc[r], p_acc[r + 1]};
+            const f2_t v = (dp * mk[r >> 1] - dl[i >> 1]) * P;
+            ds[4 * gg + i] = v.x; ds[4 * gg + i + 1] = v.y;
           }
         }
         const bf16x8_t sb = pack_b(ds, 0);
@@ -591,8 +647,8 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
   const int Lp = (L + 31) & ~31, n32 = Lp / 32;
   const int nw = waves_for(L);
   const size_t lds = (size_t)Lp * D * 2 * 2 + Lp * sizeof(float);
-  dispatch_waves<FwdTag>(nw, [&](auto c) {
-    constexpr int NW = decltype(c)::value;
+  auto run = [&](auto cw, auto cn) {
+    constexpr int NW = decltype(cw)::value, NT = decltype(cn)::value;
     auto launch = [&](auto kern) {
       static bool attr =
           (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess);
@@ -600,10 +656,17 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
       hipLaunchKernelGGL(kern, dim3(B * nh, (n32 + NW - 1) / NW), dim3(NW * 64), lds, s, qkv, key_bias, ctx, lse,
                          thr ? mbits : nullptr, L, nh, scale * LOG2E, key, thr, hq_keep_scale(thr));
     };
-    if (!thr) launch(attn_fwd_kernel<NW, false, true>);
-    else if ((L & 31) == 0) launch(attn_fwd_kernel<NW, true, true>);
-    else launch(attn_fwd_kernel<NW, true, false>);
-  });
+    if (!thr) launch(attn_fwd_kernel<NW, false, true, NT>);
+    else if constexpr (NT > 0) launch(attn_fwd_kernel<NW, true, true, NT>);  // L = 32·NT is always even
+    else if ((L & 31) == 0) launch(attn_fwd_kernel<NW, true, true, NT>);
+    else launch(attn_fwd_kernel<NW, true, false, NT>);
+  };
+  // unrolled specialisations for L = 128 / 256 / 384 / 512, rolled loop otherwise
+  if (L == 384) run(std::integral_constant<int, 12>{}, std::integral_constant<int, 12>{});
+  else if (L == 512) run(std::integral_constant<int, 8>{}, std::integral_constant<int, 16>{});
+  else if (L == 256) run(std::integral_constant<int, 8>{}, std::integral_constant<int, 8>{});
+  else if (L == 128) run(std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{});
+  else dispatch_waves<FwdTag>(nw, [&](auto c) { run(c, std::integral_constant<int, 0>{}); });
 }
 
 void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx, const float* lse, const float* key_bias,
@@ -616,9 +679,9 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
   const int Lp = (L + 31) & ~31, n32 = Lp / 32;
   const int nw = waves_for(L);
   const size_t lds_dq = (size_t)Lp * D * 2 * 2 + Lp * sizeof(float);
-  const size_t lds_kv = (size_t)Lp * D * 2 * 2 + 2 * Lp * sizeof(float);
-  dispatch_waves<FwdTag>(nw, [&](auto c) {
-    constexpr int NW = decltype(c)::value;
+  const size_t lds_kv = (size_t)Lp * D * 2 * 2 + 2 * Lp * sizeof(float) + (size_t)nw * 64 * sizeof(uint16_t);
+  auto run = [&](auto cw, auto cn) {
+    constexpr int NW = decltype(cw)::value, NT = decltype(cn)::value;
     const dim3 grid(B * nh, (n32 + NW - 1) / NW);
     auto launch = [&](auto kdq, auto kkv) {
       static bool attr =
@@ -630,7 +693,12 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
       hipLaunchKernelGGL(kkv, grid, dim3(NW * 64), lds_kv, s, qkv, dctx, lse, delta, key_bias, bits, dqkv, L, nh,
                          scale * LOG2E, scale, ks);
     };
-    if (bits) launch(attn_bwd_dq_kernel<NW, true>, attn_bwd_dkdv_kernel<NW, true>);
-    else launch(attn_bwd_dq_kernel<NW, false>, attn_bwd_dkdv_kernel<NW, false>);
-  });
+    if (bits) launch(attn_bwd_dq_kernel<NW, true, NT>, attn_bwd_dkdv_kernel<NW, true, NT>);
+    else launch(attn_bwd_dq_kernel<NW, false, NT>, attn_bwd_dkdv_kernel<NW, false, NT>);
+  };
+  if (L == 384) run(std::integral_constant<int, 12>{}, std::integral_constant<int, 12>{});
+  else if (L == 512) run(std::integral_constant<int, 8>{}, std::integral_constant<int, 16>{});
+  else if (L == 256) run(std::integral_constant<int, 8>{}, std::integral_constant<int, 8>{});
+  else if (L == 128) run(std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{});
+  else dispatch_waves<FwdTag>(nw, [&](auto c) { run(c, std::integral_constant<int, 0>{}); });
 }

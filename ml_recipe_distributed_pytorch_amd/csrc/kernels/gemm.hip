@@ -92,6 +92,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   const int tiles_n = N / BN;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
+  HQ_DASSERT(m0 + BM <= M && n0 + BN <= N && K % BK == 0);
 
   const uint16_t* Ab = A + (size_t)m0 * lda;
   const uint16_t* Bb = B + (size_t)n0 * ldb;

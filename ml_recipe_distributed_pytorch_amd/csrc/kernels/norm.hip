@@ -287,10 +287,11 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
                                                         uint16_t* __restrict__ y, float* __restrict__ mean_out,
                                                         float* __restrict__ rstd_out, int T, int H, float eps, uint32_t key,
-                                                        uint32_t thr, float kscale) {
+                                                        uint32_t thr, float kscale, int V, int P, int NTY) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * kWaves + wave;
   if (row >= T) return;
+  HQ_DASSERT(ids[row] >= 0 && ids[row] < V && pids[row] >= 0 && pids[row] < P && tids[row] >= 0 && tids[row] < NTY);
   const size_t rw = (size_t)ids[row] * H, rp = (size_t)pids[row] * H, rt = (size_t)tids[row] * H;
   float v[NCH][4];
   float sum = 0.f;
@@ -342,7 +343,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
     const uint16_t* __restrict__ wt, const float* __restrict__ gamma, const float* __restrict__ mean,
     const float* __restrict__ rstd, float* __restrict__ g_word, float* __restrict__ g_pos, float* __restrict__ g_type,
     float* __restrict__ part, int T, int H, int n_types, int pad_word, int pad_pos, uint32_t key, uint32_t thr,
-    float kscale) {
+    float kscale, int V, int P) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][H] reduction scratch, reused as dx rows
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float acc[4][NCH][4];
@@ -365,6 +366,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
     const int row = row0 + r * kWaves + wave;
     if (row >= T) break;
     const int64_t id = ids[row], pid = pids[row], tid = tids[row];
+    HQ_DASSERT(id >= 0 && id < V && pid >= 0 && pid < P && tid >= 0 && tid < n_types);
     const size_t base = (size_t)row * H;
     const float mu = mean[row], rs = rstd[row];
     float g[NCH][4], xh[NCH][4];
@@ -560,13 +562,13 @@ void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const
 
 void hq_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww, const uint16_t* wp,
                   const uint16_t* wt, const float* gamma, const float* beta, uint16_t* y, float* mean, float* rstd, int T,
-                  int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s) {
+                  int H, float eps, float p, uint32_t seed, uint32_t opid, int V, int P, int NTY, hipStream_t s) {
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const uint32_t key = hq_op_key(seed, opid);
   const float ks = hq_keep_scale(thr);
   dispatch_nch(H, [&](auto nch) {
     hipLaunchKernelGGL(embed_fwd_kernel<decltype(nch)::value>, dim3((T + kWaves - 1) / kWaves), dim3(256), 0, s, ids,
-                       pids, tids, ww, wp, wt, gamma, beta, y, mean, rstd, T, H, eps, key, thr, ks);
+                       pids, tids, ww, wp, wt, gamma, beta, y, mean, rstd, T, H, eps, key, thr, ks, V, P, NTY);
   });
 }
 
@@ -574,7 +576,7 @@ void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, c
                   const uint16_t* wp, const uint16_t* wt, const float* gamma, const float* mean, const float* rstd,
                   float* g_word, float* g_pos, float* g_type, float* part, HqOuts outs, int T, int H,
                   int n_types, int pad_word, int pad_pos, float p, uint32_t seed, uint32_t opid, bool accumulate,
-                  hipStream_t s) {
+                  int V, int P, hipStream_t s) {
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const uint32_t key = hq_op_key(seed, opid);
   const float ks = hq_keep_scale(thr);
@@ -582,7 +584,7 @@ void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, c
   dispatch_nch(H, [&](auto nch) {
     hipLaunchKernelGGL(embed_bwd_kernel<decltype(nch)::value>, dim3(nb), dim3(256), 4 * H * sizeof(float), s, dy, ids,
                        pids, tids, ww, wp, wt, gamma, mean, rstd, g_word, g_pos, g_type, part, T, H, n_types, pad_word,
-                       pad_pos, key, thr, ks);
+                       pad_pos, key, thr, ks, V, P);
   });
   // outs: gamma, beta, type0, type1 (type rows only when n_types <= 2)
   colsum(part, nb, 4 * H, outs, H, accumulate, s);

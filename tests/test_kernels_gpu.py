@@ -121,7 +121,7 @@ def _attn_case(cuda, B, L, nh, p, masked):
     _close(dq, dqr, 3e-2, 3e-2, "dqkv")
 
 
-@pytest.mark.parametrize("L", [384, 512, 128, 100, 24, 7])
+@pytest.mark.parametrize("L", [384, 512, 256, 128, 100, 24, 7])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_attention(cuda, L, p):
     _attn_case(cuda, 2, L, 2, p, masked=True)

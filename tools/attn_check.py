@@ -1,0 +1,24 @@
+"""Per-part (dQ / dK / dV) error of the attention backward vs the torch oracle."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ml_recipe_distributed_pytorch_amd import _native  # noqa: E402
+from ml_recipe_distributed_pytorch_amd.ops import reference as ref  # noqa: E402
+
+k = _native.kernels()
+for L, p in ((128, 0.1), (100, 0.1), (128, 0.0)):
+    B, nh = 2, 2
+    H = nh * 64
+    torch.manual_seed(3)
+    qkv = torch.randn(B * L, 3 * H).bfloat16()
+    kb = torch.zeros(B, L)
+    ctx, lse, bits = k.attn_fwd(qkv.cuda(), kb.cuda(), B, L, nh, p, 555, 3, 0.125)
+    dctx = torch.randn(B * L, H).bfloat16()
+    dq = k.attn_bwd(dctx.cuda(), qkv.cuda(), ctx, lse, kb.cuda(), bits, B, L, nh, p, 0.125).float().cpu()
+    dqr = ref.attn_bwd(dctx, qkv, ctx.cpu(), lse.cpu(), kb, B, L, nh, p, 555, 3, 0.125).float()
+    for i, nm in enumerate("QKV"):
+        a, b = dq[:, i * H:(i + 1) * H], dqr[:, i * H:(i + 1) * H]
+        print(L, p, "d" + nm, "max err %.3e" % (a - b).abs().max().item(), "ref max %.3e" % b.abs().max().item())

@@ -35,6 +35,10 @@ def main():
                     print(f"   {c + ' / MFMA':28s} {m[c] / mf:14.3f}")
         if "SQ_WAVE_CYCLES" in m and "SQ_WAIT_INST_ANY" in m:
             print(f"   {'wait_inst / wave_cycles':28s} {m['SQ_WAIT_INST_ANY'] / m['SQ_WAVE_CYCLES']:14.3f}")
+        if "SQ_VALU_MFMA_BUSY_CYCLES" in m and m.get("GRBM_GUI_ACTIVE"):
+            # MFMA busy cycles summed over SIMDs vs (GPU-active cycles per XCD x 1024 SIMDs)
+            util = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8 * 1024)
+            print(f"   {'mfma_busy / simd_cycles':28s} {util:14.3f}")
         if "SQ_LDS_BANK_CONFLICT" in m and "SQ_LDS_IDX_ACTIVE" in m and m["SQ_LDS_IDX_ACTIVE"]:
             print(f"   {'lds_conflict / lds_active':28s} {m['SQ_LDS_BANK_CONFLICT'] / m['SQ_LDS_IDX_ACTIVE']:14.3f}")
 
