@@ -62,6 +62,9 @@ def init_model(model_params, *, checkpoint=None, device=torch.device("cpu"), bpe
     prec = precision or ("bf16" if torch.device(device).type == "cuda" else "fp32")
     model = BertForQuestionAnswering(cfg, precision=prec, seed=seed)
     pre = getattr(model_params, "pretrained_path", None)
+    if pre and getattr(model_params, "random_init", False):
+        logger.warning(f"--random_init: ignoring --pretrained_path {pre}.")
+        pre = None
     if pre:
         missing = load_pretrained(model, pre)
         logger.info(f"Pretrained encoder weights loaded from {pre} ({len(missing)} tensors left at init).")

@@ -107,6 +107,8 @@ class Trainer:
     profile: bool = False
     eval_shard: bool = False
     precision: Optional[str] = None
+    torch_profile_dir: Optional[str] = None
+    torch_profile_steps: str = "3:5"
     extra_state: dict = field(default_factory=dict)
 
     def __post_init__(self):
@@ -246,6 +248,7 @@ class Trainer:
             if res is None:
                 continue
             self.global_step += 1
+            self._torch_profiler_step()
             _fault_hook(self.rank, self.global_step)
             if self.global_step % max(1, self.log_every) == 0 or self.debug:
                 avg = res.losses.to_floats()  # the one device→host sync per log step
@@ -265,10 +268,39 @@ class Trainer:
                     if self.profile:
                         for k, v in res.timings.items():
                             self.writer.add_scalar(f"perf/{k}", v, global_step=self.global_step)
+                        if "comm_wait_ms" in res.timings:  # SURVEY §5.5 tag name
+                            self.writer.add_scalar("perf/comm_ms", res.timings["comm_wait_ms"],
+                                                   global_step=self.global_step)
                 data.set_postfix_str(self._console_str({k: v for k, v in avg.items() if not k.startswith("perf")}))
             if self.debug:
                 logger.info("Training was interrupted because of debug mode.")
                 break
+
+    # ------------------------------------------------------------------ torch.profiler export
+    def _torch_profiler_step(self):
+        """SURVEY §5.1 optional torch.profiler trace: optimizer steps ``first..last`` (1-based) of this
+        run are captured with CPU + HIP activities and written as a Chrome trace per rank."""
+        if not self.torch_profile_dir:
+            return
+        first, last = (int(x) for x in str(self.torch_profile_steps).split(":"))
+        prof = getattr(self, "_tprof", None)
+        if prof is False:
+            return
+        if prof is None and first - 1 <= self.global_step < last:  # armed after step first-1 (>= step 1)
+            acts = [torch.profiler.ProfilerActivity.CPU]
+            if self.device.type == "cuda":
+                acts.append(torch.profiler.ProfilerActivity.CUDA)
+            self._tprof = torch.profiler.profile(activities=acts, record_shapes=True)
+            self._tprof.__enter__()
+        elif prof is not None and self.global_step >= last:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            prof.__exit__(None, None, None)
+            os.makedirs(self.torch_profile_dir, exist_ok=True)
+            path = os.path.join(self.torch_profile_dir, f"trace_rank{self.rank}_steps{first}-{last}.json")
+            prof.export_chrome_trace(path)
+            logger.info(f"torch.profiler trace written to {path}")
+            self._tprof = False  # done; never re-arm
 
     # ------------------------------------------------------------------ evaluation
     def test(self, epoch_i, *, callbacks=None):

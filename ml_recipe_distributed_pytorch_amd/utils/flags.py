@@ -73,6 +73,8 @@ def get_model_parser() -> ArgumentParser:
     parser.add_argument("--handle_chinese_chars", action="store_true",
                         help="Do not replace chinese symbols with UNK tokens.")
     # --- MI355X additions -------------------------------------------------------------------
+    parser.add_argument("--random_init", action="store_true",
+                        help="Ignore --pretrained_path and start from random weights (what happens anyway without it).")
     parser.add_argument("--pretrained_path", type=cast2(str), default=None,
                         help="Local dir/file with HF-named weights (safetensors or weights-only torch). "
                              "Random init when absent (no network in this environment).")
@@ -168,6 +170,10 @@ def get_trainer_parser() -> ArgumentParser:
                         help="1: all-reduce only at the accumulation boundary (fix of D1); 0: every micro-batch.")
     parser.add_argument("--dist_timeout", type=float, default=1800.0, help="Process-group timeout in seconds.")
     parser.add_argument("--profile", action="store_true", help="Per-phase step timers + perf/* TB scalars.")
+    parser.add_argument("--torch_profile_dir", type=cast2(str), default=None,
+                        help="Export a torch.profiler Chrome trace of optimizer steps --torch_profile_steps here.")
+    parser.add_argument("--torch_profile_steps", type=str, default="3:5",
+                        help="first:last optimizer steps (1-based, inclusive) captured by --torch_profile_dir.")
     parser.add_argument("--log_every", type=int, default=1, help="Device→host loss sync cadence (steps).")
     parser.add_argument("--checkpoint", type=cast2(str), default=None,
                         help="Checkpoint for train_metrics evaluation (fix of D9).")

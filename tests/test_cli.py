@@ -74,6 +74,24 @@ def test_train_resume_and_interrupt(tmp_path, monkeypatch):
     assert st3["global_step"] == 3
 
 
+def test_profiling_outputs(tmp_path):
+    """--profile writes perf/* phase timers (incl. perf/comm_ms) and
+    --torch_profile_dir exports a torch.profiler Chrome trace of the chosen optimizer steps."""
+    cfg = _cfg(tmp_path, debug="False", n_epochs="1", train_batch_size="8", batch_split="1",
+               dummy_dataset_len="48", experiment_name="prof")
+    tdir = tmp_path / "trace"
+    _train(["-c", cfg, "--dump_dir", str(tmp_path), "--profile", "--torch_profile_dir", str(tdir),
+            "--torch_profile_steps", "2:4", "--random_init"] + TINY)
+    traces = list(tdir.glob("trace_rank0_steps2-4.json"))
+    assert traces and traces[0].stat().st_size > 0
+    import json
+    assert "traceEvents" in json.load(open(traces[0]))
+    from ml_recipe_distributed_pytorch_amd.utils.tb import read_events
+    ev = list((tmp_path / "board" / "prof").glob("events.out.tfevents.*"))
+    tags = {t for _, t, _ in read_events(str(ev[0]))}
+    assert {"perf/samples_per_sec", "perf/step_ms", "perf/fwd_ms", "perf/bwd_ms", "perf/comm_ms"} <= tags
+
+
 @pytest.mark.slow
 def test_train_two_rank_gloo_spawn(tmp_path):
     cfg = _cfg(tmp_path, debug="False", n_epochs="1", train_batch_size="4", batch_split="1",
