@@ -368,6 +368,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
         py::arg("pre") = py::none(), py::arg("resid") = py::none(), py::arg("part") = py::none(),
         py::arg("out") = py::none());
   m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_set_variant", [](int64_t v) { hq_gemm_set_variant((int)v); });
   m.def("transpose_tiles", &transpose_tiles);
   m.def("colsum_into", &colsum_into);
   m.def("fp8_quantize", &fp8_quantize);

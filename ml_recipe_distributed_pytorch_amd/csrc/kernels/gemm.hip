@@ -250,6 +250,269 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   }
 }
 
+
+// ============================================================================================
+// v2 — deep LDS-DMA pipeline (CDNA4 playbook §5 "8-phase" structure, re-derived for this tile).
+//
+// Same 256×256×64 tile, 8 waves, swizzle and swapped-operand MFMA as v1, but the K-tile is split
+// into FOUR phases of 16 MFMAs per wave and the staging into four 16 KiB "halves" (128 rows of
+// the A or B panel, 2 LDS-DMA instructions per thread), ONE half issued per phase, so three
+// halves stay in flight across every barrier (counted vmcnt(6), never 0 in the steady state)
+// instead of v1's whole-tile issue + vmcnt(0) drain per K-tile.
+//
+// Wave (wm, wn) owns four 64×32 quadrants (mh, nh): rows mh·128 + wm·64 + [0,64),
+// cols nh·128 + wn·32 + [0,32) — so quadrant (mh, nh) reads exactly A-half mh and B-half nh.
+//   phase  quadrant  LDS reads (ds_read_b128)   stage issued          wait (vmcnt 6) retires
+//   P0     (0,0)     A0 (8) + B0 (4)            B1(t+1)               B1(t)
+//   P1     (0,1)     B1 (4)                     A1(t+1)               A1(t)
+//   P2     (1,1)     A1 (8)                     A0(t+2)               —
+//   P3     (1,0)     — (B0 kept in registers)   B0(t+2)               A0(t+1), B0(t+1)
+// Hazards (two wave groups staggered by one barrier, two barriers per phase): a slot is
+// restaged ≥ 2 phases after its last read (WAR) and read ≥ 1 phase after the wait that retires
+// it (RAW); the table satisfies both (3/3/2/3 phases and 4-5 phases of load latency hiding).
+// Tail tiles skip the stages past the end and use the exact smaller vmcnt.
+// ABL (tools/gemm_lab only; production = 0): bit0 skip the in-loop LDS-DMA stages, bit1 skip the
+// in-loop fragment reads, bit2 run both wave groups in lockstep (no stagger barrier), bit3 stage
+// with buffer_load … lds (SRD + precomputed per-lane offsets) instead of global_load_lds, bit4
+// grouped tile order (8 row panels × all column panels per group).
+template <int EPI, int ABL = 0>
+__global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                                                               uint16_t* __restrict__ C, const float* __restrict__ bias,
+                                                               uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
+                                                               float* __restrict__ part, int M, int N, int K, int lda,
+                                                               int ldb, int ldc) {
+  constexpr int BN = 256;
+  constexpr int PANEL = 256 * 128;      // one A or B panel (256 rows × 64 bf16)
+  constexpr int HALF = 128 * 128;       // 128 rows of a panel
+  constexpr int STAGE = 2 * PANEL;      // A panel then B panel
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tiles_n = N / BN;
+  int tm = tile / tiles_n, tn = tile % tiles_n;
+  if constexpr ((ABL & 16) != 0) {
+    constexpr int GM = 8;
+    const int tiles_m = M / BM, per = GM * tiles_n;
+    const int first = (tile / per) * GM, gsz = min(tiles_m - first, GM), in = tile % per;
+    tm = first + in % gsz;
+    tn = in / gsz;
+  }
+  const int m0 = tm * BM, n0 = tn * BN;
+  HQ_DASSERT(m0 + BM <= M && n0 + BN <= N && K % BK == 0 && K >= 2 * BK);
+
+  const uint16_t* Ab = A + (size_t)m0 * lda;
+  const uint16_t* Bb = B + (size_t)n0 * ldb;
+  const int nt = K / BK;
+
+  // one half = 16 pieces of 8 rows; wave w stages rows w·16 .. w·16+15 of it (2 instructions)
+  auto stage_half = [&](const uint16_t* g, int ld, int half, int t, char* panel) {
+    stage_panel<2>(g, ld, half * 128 + wave * 16, t * BK, panel, lane);
+  };
+  // buffer-load staging: SRDs over the block's A / B row panels; the per-lane byte offsets of the two
+  // 8-row pieces a wave stages are the same for every half and K-tile (the swizzle depends on row
+  // bits 1..3 only), so the K-tile and half advance lives in the scalar soffset.
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, BM * lda * 2, 0x00020000);
+  __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, BN * ldb * 2, 0x00020000);
+  int voA[2], voB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * 16 + i * 8 + (lane >> 3);
+    const int src_slot = (lane & 7) ^ ((row >> 1) & 7);
+    voA[i] = (row * lda + src_slot * 8) * 2;
+    voB[i] = (row * ldb + src_slot * 8) * 2;
+  }
+  auto buf_half = [&](__amdgpu_buffer_rsrc_t rs, const int (&vo)[2], int ld, int half, int t, char* panel) {
+    char* dst = panel + (half * 128 + wave_u * 16) * 128;
+    const int so = half * 128 * ld * 2 + t * BK * 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + i * 8 * 128), 16, vo[i], so, 0, 0);
+  };
+  auto stA = [&](int half, int t) {
+    if constexpr ((ABL & 1) != 0) return;
+    if constexpr ((ABL & 8) != 0) buf_half(rA, voA, lda, half, t, smem + (t & 1) * STAGE);
+    else stage_half(Ab, lda, half, t, smem + (t & 1) * STAGE);
+  };
+  auto stB = [&](int half, int t) {
+    if constexpr ((ABL & 1) != 0) return;
+    if constexpr ((ABL & 8) != 0) buf_half(rB, voB, ldb, half, t, smem + (t & 1) * STAGE + PANEL);
+    else stage_half(Bb, ldb, half, t, smem + (t & 1) * STAGE + PANEL);
+  };
+
+  f32x4_t acc[8][4];   // [mh·4 + i][nh·2 + j]
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8_t af[2][4];        // [ks][i] of the current m-half
+  bf16x8_t bf0[2][2], bf1[2][2];   // [ks][j] of n-half 0 / 1
+  auto readA = [&](int t, int mh) {
+    if constexpr ((ABL & 2) != 0) { if (t > 0) return; }
+    const char* pa = smem + (t & 1) * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[ks][i] = frag(pa, mh * 128 + wm * 64 + i * 16 + fr, ks * 4 + fq);
+  };
+  auto readB = [&](int t, int nh, bf16x8_t (&bf)[2][2]) {
+    if constexpr ((ABL & 2) != 0) { if (t > 0) return; }
+    const char* pb = smem + (t & 1) * STAGE + PANEL;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[ks][j] = frag(pb, nh * 128 + wn * 32 + j * 16 + fr, ks * 4 + fq);
+  };
+  auto mma = [&](int mh, int nh, const bf16x8_t (&bf)[2][2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mh * 4 + i][nh * 2 + j] = mfma16(bf[ks][j], af[ks][i], acc[mh * 4 + i][nh * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = []() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // prologue: tile 0 (A0 B0 B1 A1) and the first two halves of tile 1; retire A0(0), B0(0)
+  stage_half(Ab, lda, 0, 0, smem); stage_half(Bb, ldb, 0, 0, smem + PANEL);
+  stage_half(Bb, ldb, 1, 0, smem + PANEL); stage_half(Ab, lda, 1, 0, smem);
+  stage_half(Ab, lda, 0, 1, smem + STAGE); stage_half(Bb, ldb, 0, 1, smem + STAGE + PANEL);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  bar();
+
+  // One K-tile = 4 phases; `G1` = the staggered group (one barrier behind).
+  auto ktile = [&](int t) {
+    const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
+    // P0 (0,0)
+    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    readB(t, 0, bf0);
+    readA(t, 0);
+    if (more1) stB(1, t + 1);
+    bar();
+    mma(0, 0, bf0);
+    bar();
+    // P1 (0,1)
+    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    readB(t, 1, bf1);
+    if (more1) stA(1, t + 1);
+    bar();
+    mma(0, 1, bf1);
+    bar();
+    // P2 (1,1)
+    readA(t, 1);
+    if (more2) stA(0, t + 2);
+    bar();
+    mma(1, 1, bf1);
+    bar();
+    // P3 (1,0)
+    if (more1) {
+      if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    if (more2) stB(0, t + 2);
+    bar();
+    mma(1, 0, bf0);
+    bar();
+  };
+  if (ABL & 4) {
+    for (int t = 0; t < nt; ++t) ktile(t);
+  } else if (__builtin_amdgcn_readfirstlane(wm) == 0) {
+    for (int t = 0; t < nt; ++t) ktile(t);
+    bar();
+  } else {
+    bar();
+    for (int t = 0; t < nt; ++t) ktile(t);
+  }
+
+  // ---- epilogue (as v1, with the quadrant → tile mapping): acc (+bias) -> bf16 into this wave's
+  // private LDS region [128 local rows][64 local cols], local row lr = mh·64 + i·16 + ..,
+  // local col lc = nh·32 + j·16 + ..; then row-coalesced 16-B pieces -> epilogue math -> global.
+  constexpr int WN = 64;
+  constexpr int RS = WN * 2 + 16;
+  char* wreg = smem + wave * (128 * RS);
+#pragma unroll
+  for (int J = 0; J < 4; ++J) {
+    const int nh = J >> 1, j = J & 1;
+    const int lc = nh * 32 + j * 16 + fq * 4;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU)
+      bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
+#pragma unroll
+    for (int I = 0; I < 8; ++I) {
+      float v[4] = {acc[I][J][0] + bv.x, acc[I][J][1] + bv.y, acc[I][J][2] + bv.z, acc[I][J][3] + bv.w};
+      *reinterpret_cast<uint2*>(wreg + (I * 16 + fr) * RS + lc * 2) = hq_pack4(v);
+    }
+  }
+  constexpr int SEGS = WN / 8;                  // 8 pieces of 16 B per local row
+  constexpr int ROWS_PER_IT = 64 / SEGS;        // 8
+  const int seg = lane % SEGS, rsub = lane / SEGS;
+  const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;   // 4 pieces per 32-col chunk
+  float csum[8];
+  if constexpr (EPI == HQ_EPI_DGELU) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+  }
+#pragma unroll 4
+  for (int it = 0; it < 128 / ROWS_PER_IT; ++it) {
+    const int lr = it * ROWS_PER_IT + rsub;
+    const int grow = m0 + (lr >> 6) * 128 + wm * 64 + (lr & 63);
+    uint4 piece = *reinterpret_cast<const uint4*>(wreg + lr * RS + seg * 16);
+    const size_t goff = (size_t)grow * ldc + gcol;
+    if constexpr (EPI == HQ_EPI_GELU) {
+      *reinterpret_cast<uint4*>(P + goff) = piece;
+      float x[8];
+      hq_unpack8(piece, x);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = gelu_erf(x[e]);
+      piece = hq_pack8(x);
+    } else if constexpr (EPI == HQ_EPI_DGELU) {
+      float d[8], pr[8];
+      hq_unpack8(piece, d);
+      hq_unpack8(*reinterpret_cast<const uint4*>(P + goff), pr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { d[e] *= gelu_grad(pr[e]); csum[e] += d[e]; }
+      piece = hq_pack8(d);
+    } else if constexpr (EPI == HQ_EPI_RESID) {
+      float d[8], rr[8];
+      hq_unpack8(piece, d);
+      hq_unpack8(*reinterpret_cast<const uint4*>(R + goff), rr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] += rr[e];
+      piece = hq_pack8(d);
+    }
+    *reinterpret_cast<uint4*>(C + goff) = piece;
+  }
+  if constexpr (EPI == HQ_EPI_DGELU) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      for (int o = SEGS; o < 64; o <<= 1) csum[e] += __shfl_xor(csum[e], o, 64);
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [2][BN], indexed by tile column
+    if (rsub == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wm * BN + (gcol - n0) + e] = csum[e];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += kThreads) part[(size_t)tm * N + n0 + c] = red[c] + red[BN + c];
+  }
+}
+
+int g_gemm_variant = 0;   // 0 = auto (v2 where supported), 1 = force v1
+
 constexpr size_t epi_lds(int bn) {
   const size_t stage = 2 * (size_t)(BM * 128 + bn * 128);
   const size_t epi = 8 * 128 * (size_t)(bn / 4 * 2 + 16);
@@ -260,7 +523,25 @@ template <int EPI>
 void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,
                 float* part, int M, int N, int K, int lda, int ldb, int ldc, int bn, hipStream_t s) {
   const int grid = (M / BM) * (N / bn);
-  if (bn == 256) {
+  if (bn == 256 && g_gemm_variant == 0 && K >= 2 * BK && (size_t)BM * lda * 2 < (1ull << 31) &&
+      (size_t)256 * ldb * 2 < (1ull << 31)) {
+    // production v2: buffer_load…lds staging (+8-12 % over global_load_lds on the BERT shapes,
+    // tools/gemm_lab); grouped 8-row-panel tile order only for wide N (+15 % at 8192², neutral at
+    // N <= 3072 where an XCD's co-resident tiles already share few panels).
+    constexpr size_t lds = epi_lds(256);
+    static bool init = [] {
+      (void)hipFuncSetAttribute((const void*)gemm_nt2_kernel<EPI, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (void)hipFuncSetAttribute((const void*)gemm_nt2_kernel<EPI, 24>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      return true;
+    }();
+    (void)init;
+    if (N / 256 >= 16)
+      hipLaunchKernelGGL((gemm_nt2_kernel<EPI, 24>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, R, part, M, N, K,
+                         lda, ldb, ldc);
+    else
+      hipLaunchKernelGGL((gemm_nt2_kernel<EPI, 8>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, R, part, M, N, K,
+                         lda, ldb, ldc);
+  } else if (bn == 256) {
     constexpr size_t lds = epi_lds(256);
     static bool init = [] {
       (void)hipFuncSetAttribute((const void*)gemm_nt_kernel<EPI, 256>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -282,6 +563,8 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
 }
 
 }  // namespace
+
+void hq_gemm_set_variant(int v) { g_gemm_variant = v; }
 
 int hq_gemm_nt_supported(int M, int N, int K) {
   if (M % BM || K % BK || K < BK) return 0;

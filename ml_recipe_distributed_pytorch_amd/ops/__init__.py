@@ -86,10 +86,11 @@ def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale
 # --------------------------------------------------------------------------------------- linear
 # Which projection GEMMs run on the hand-written MFMA NT kernel (gemm.hip) instead of hipBLASLt.
 #   HQ_GEMM=auto (default): the GEMMs whose epilogue fuses an elementwise pass — FFN1 + GELU,
-#     FFN2-dgrad + dGELU + FFN1 bias-grad (1.04x / 1.34x vs hipBLASLt + separate kernel at b256,
+#     FFN2-dgrad + dGELU + FFN1 bias-grad (1.08x / 1.40x vs hipBLASLt + separate kernel at b256,
 #     profiles/) and the QKV dgrad + residual-gradient add (torch.addmm first copies the residual
-#     into the output: +56 µs at b256) — when the 256-row tile grid fills the 256 CUs to >= 85 %.
-#     Plain projections stay on hipBLASLt with the shipped TunableOp picks (3-15 % faster here);
+#     into the output: +56 µs at b256), plus the plain long-K (K >= 2048) dgrads where the v2 kernel
+#     is 1.04x hipBLASLt — when the 256-row tile grid fills the 256 CUs to >= 85 %.
+#     Plain forward projections stay on hipBLASLt with the shipped TunableOp picks (2-13 % faster);
 #   HQ_GEMM=mfma: every supported shape;  HQ_GEMM=blas: none.
 _EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID = range(5)
 _GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
@@ -113,6 +114,8 @@ def _mfma(M: int, N: int, K: int, kind: str = "plain") -> bool:
         return True
     tiles = (M // 256) * (N // bn)
     fill = tiles / (-(-tiles // _CUS) * _CUS)
+    if kind == "dgrad":  # plain long-K dgrad: v2 kernel 1.03-1.04x hipBLASLt at b256 (profiles/)
+        return fill >= 0.85 and K >= 2048
     return fill >= 0.85 and kind in ("dgelu", "gelu", "resid")
 
 
@@ -147,7 +150,7 @@ def linear_gelu_fwd(x, w, b, b32=None):
 def linear_dgrad(dy, w, wt=None):
     """dy·W.  ``wt`` = Wᵀ working copy (ParamStore.view_t) enables the NT MFMA kernel."""
     if dy.is_cuda:
-        if wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1]):
+        if wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1], "dgrad"):
             return _k().gemm_nt(dy, wt, _EPI_NONE)
         return torch.mm(dy, w)
     return ref.linear_dgrad(dy, w)

@@ -1,11 +1,24 @@
-"""MFMA NT GEMM (gemm.hip) vs an fp32 torch reference, every epilogue."""
+"""MFMA NT GEMM (gemm.hip) vs an fp32 torch reference, every epilogue, both kernel variants
+(v2 = deep LDS-DMA pipeline, the default for 256-wide tiles with K >= 128; v1 = whole-tile staging)."""
 import pytest
 import torch
 
 from ml_recipe_distributed_pytorch_amd import _native
 
+
+@pytest.fixture(params=[0, 1], ids=["v2", "v1"], autouse=True)
+def variant(request):
+    if not torch.cuda.is_available():
+        yield request.param
+        return
+    k = _native.kernels()
+    k.gemm_set_variant(request.param)
+    yield request.param
+    k.gemm_set_variant(0)
+
 EPI_NONE, EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID = range(5)
-SHAPES = [(256, 256, 64), (512, 384, 192), (1024, 768, 768), (768, 2304, 128), (512, 128, 3072)]
+SHAPES = [(256, 256, 64), (512, 384, 192), (1024, 768, 768), (768, 2304, 128), (512, 128, 3072), (256, 256, 192),
+          (2048, 768, 3072), (512, 4096, 256)]
 
 
 def _ref(A, B):
@@ -74,3 +87,18 @@ def test_gemm_nt_rejects_bad_shapes(cuda):
     assert k.gemm_nt_supported(100, 128, 64) == 0
     with pytest.raises(RuntimeError):
         k.gemm_nt(A, B, EPI_NONE)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(8192, 2304, 768), (4096, 768, 3072), (4096, 4096, 768)])
+def test_gemm_nt_repeatable_large(cuda, M, N, K):
+    """Race screen: a full-chip grid run repeatedly must be bitwise identical (the kernel is
+    deterministic) and match the fp32 reference — an LDS RAW/WAR slip shows up as rare wrong tiles."""
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(11)
+    A = (torch.rand(M, K, device=cuda, generator=g) * 2 - 1).bfloat16()
+    B = (torch.rand(N, K, device=cuda, generator=g) * 2 - 1).bfloat16()
+    first = k.gemm_nt(A, B, EPI_NONE)
+    _close(first, _ref(A, B))
+    for _ in range(8):
+        assert torch.equal(k.gemm_nt(A, B, EPI_NONE), first)

@@ -44,14 +44,19 @@ def main():
             ref = A.float() @ B.float().t() + (bias if epi else 0)
             ours()
             err = ((C.float() - ref).abs().max() / ref.abs().max()).item()
-            a, b = [], []
+            a, b, c = [], [], []
             for _ in range(5):
                 a.append(timeit(ours))
                 b.append(timeit(theirs))
-            a.sort(), b.sort()
+                k.gemm_set_variant(1)
+                c.append(timeit(ours))
+                k.gemm_set_variant(0)
+            a.sort(), b.sort(), c.sort()
             fl = 2.0 * T * N * K
-            row = {"T": T, "gemm": name, "N": N, "K": K, "ours_us": round(a[2], 1), "hipblaslt_us": round(b[2], 1),
-                   "ours_tflops": round(fl / a[2] / 1e6, 1), "hipblaslt_tflops": round(fl / b[2] / 1e6, 1),
+            row = {"T": T, "gemm": name, "N": N, "K": K, "ours_us": round(a[2], 1), "v1_us": round(c[2], 1),
+                   "hipblaslt_us": round(b[2], 1),
+                   "ours_tflops": round(fl / a[2] / 1e6, 1), "v1_tflops": round(fl / c[2] / 1e6, 1),
+                   "hipblaslt_tflops": round(fl / b[2] / 1e6, 1),
                    "speedup": round(b[2] / a[2], 3), "rel_err": round(err, 5)}
             print(json.dumps(row), flush=True)
             out.append(row)
@@ -74,12 +79,16 @@ def main():
                     k.colsum_into(part, gb, False)
                     return d
                 theirs = lambda: k.gelu_bwd(torch.mm(A, Bt), pre, gb, False)
-            a, b = [], []
+            a, b, c = [], [], []
             for _ in range(5):
                 a.append(timeit(ours))
                 b.append(timeit(theirs))
-            a.sort(), b.sort()
-            row = {"T": T, "gemm": name, "N": N, "K": K, "ours_us": round(a[2], 1), "hipblaslt+ew_us": round(b[2], 1),
+                k.gemm_set_variant(1)
+                c.append(timeit(ours))
+                k.gemm_set_variant(0)
+            a.sort(), b.sort(), c.sort()
+            row = {"T": T, "gemm": name, "N": N, "K": K, "ours_us": round(a[2], 1), "v1_us": round(c[2], 1),
+                   "hipblaslt+ew_us": round(b[2], 1),
                    "speedup": round(b[2] / a[2], 3)}
             print(json.dumps(row), flush=True)
 

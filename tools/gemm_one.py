@@ -1,5 +1,6 @@
 #!/usr/bin/env python
-"""Run one NT GEMM shape repeatedly (for PMC collection): python tools/gemm_one.py T N K epi"""
+"""Run one NT GEMM shape repeatedly (for PMC collection): python tools/gemm_one.py T N K epi
+(HQ_GEMM_VARIANT=1 selects the v1 kernel)."""
 import os
 import sys
 
@@ -10,6 +11,7 @@ from ml_recipe_distributed_pytorch_amd import _native  # noqa: E402
 
 T, N, K, epi = (int(x) for x in sys.argv[1:5])
 k = _native.kernels()
+k.gemm_set_variant(int(os.environ.get("HQ_GEMM_VARIANT", "0")))
 dev = torch.device("cuda")
 A = (torch.rand(T, K, device=dev) * 2 - 1).bfloat16()
 B = (torch.rand(N, K, device=dev) * 2 - 1).bfloat16()
