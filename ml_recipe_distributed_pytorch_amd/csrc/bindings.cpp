@@ -169,6 +169,24 @@ Tensor gemm_nt(Tensor A, Tensor B, int64_t epi, c10::optional<Tensor> bias, c10:
   return C;
 }
 
+// Weight gradient: out [N,K] f32 (+)= dyᵀ·x with dy [T,N], x [T,K] bf16; split-K slabs from the caching allocator.
+int64_t gemm_tn_splits(int64_t T, int64_t N, int64_t K) { return hq_gemm_tn_splits((int)T, (int)N, (int)K); }
+
+void gemm_tn(Tensor dy, Tensor x, Tensor out, bool accumulate, int64_t splits) {
+  check(dy, BF16, "dy"); check(x, BF16, "x"); check(out, F32, "out");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "gemm_tn: dy [T,N], x [T,K]");
+  const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
+  TORCH_CHECK(out.numel() == N * K, "gemm_tn: out must hold N*K");
+  const int auto_s = hq_gemm_tn_splits((int)T, (int)N, (int)K);
+  TORCH_CHECK(auto_s > 0, "gemm_tn: unsupported shape T=", T, " N=", N, " K=", K, " (need T%64, N%256, K%256 == 0)");
+  const int S = splits > 0 ? (int)splits : auto_s;
+  TORCH_CHECK(T / 64 / S >= 2, "gemm_tn: too many splits");
+  c10::DeviceGuard g(dy.device());
+  Tensor part = at::empty({S, N, K}, out.options());
+  hq_gemm_tn(ptr<uint16_t>(dy), ptr<uint16_t>(x), ptr<float>(part), ptr<float>(out), (int)T, (int)N, (int)K, S, accumulate,
+             cur_stream());
+}
+
 void transpose_tiles(Tensor src, Tensor dst, Tensor tiles) {
   check(src, BF16, "src"); check(dst, BF16, "dst");
   TORCH_CHECK(tiles.device().is_cuda() && tiles.scalar_type() == at::kInt && tiles.is_contiguous() && tiles.dim() == 2 &&
@@ -369,6 +387,9 @@ PYBIND11_MODULE(_hq_kernels, m) {
         py::arg("out") = py::none());
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_set_variant", [](int64_t v) { hq_gemm_set_variant((int)v); });
+  m.def("gemm_tn", &gemm_tn, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("accumulate") = false,
+        py::arg("splits") = 0);
+  m.def("gemm_tn_splits", &gemm_tn_splits);
   m.def("transpose_tiles", &transpose_tiles);
   m.def("colsum_into", &colsum_into);
   m.def("fp8_quantize", &fp8_quantize);

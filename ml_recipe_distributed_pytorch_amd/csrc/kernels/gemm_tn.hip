@@ -1,0 +1,266 @@
+// Weight-gradient GEMM ("TN") for gfx950:  part[s] = Aᵀ·B over the s-th token range, i.e.
+//   dW[N, K] = Σ_t dy[t, n] · x[t, k]      A = dy [T, N], B = x [T, K], both token-major row-major,
+// split-K over the T tokens into S fp32 partial slabs, then hq_splitk_reduce adds the slabs into the
+// fp32 grad arena (optionally accumulating).  Replaces hipBLASLt's batched split-K wgrad.
+//
+// Same pipeline as gemm.hip's v2 NT kernel (256×256 output tile, 64-token K-tiles, 8 waves as
+// 2 (N) × 4 (K) ping-ponging wave groups, four phases per K-tile, one 16 KiB half-panel of LDS-DMA
+// per phase with three halves in flight under a counted vmcnt(6), buffer_load … lds with the K-tile
+// advance in the scalar offset).  What differs is the operand layout: a half-panel is a
+// [64 tokens][128 columns] slab (256-B rows) copied straight from the token-major tensor, and the
+// MFMA fragments — which need 8 consecutive TOKENS of one column per lane — come from pairs of
+// ds_read_b64_tr_b16 hardware-transposed reads (CDNA4 playbook T10).
+// LDS bank conflicts: a transposed read's 32-lane half touches 8 token rows × 32 B of one column
+// block; with 256-B rows those all hit the same banks, so each row's 32-B chunks are XOR-swizzled by
+//   f(t) = (t & 3) | ((t >> 3) & 1) << 2
+// (8 distinct values across the 8 rows → conflict-free).  The DMA image is lane-linear, so the
+// swizzle is applied on the per-lane SOURCE chunk and undone on the read (playbook rule 21).
+#include <algorithm>
+
+#include "hq_common.h"
+#include "hq_kernels.h"
+
+namespace {
+
+constexpr int BT = 64;          // tokens per K-tile
+constexpr int kThreads = 512;
+constexpr int HALF = BT * 256;  // [64 tokens][128 bf16] = 16 KiB
+constexpr int STAGE = 4 * HALF; // A0 A1 B0 B1
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) bf16x4_t lds_bf16x4;
+
+__device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ int tswz(int t) { return (t & 3) | (((t >> 3) & 1) << 2); }
+
+// Fragment of 8 consecutive tokens (ks·32 + 8g … +7) of column `cblk`·16 + (lane & 15) from a half
+// image at LDS byte address `img`.  `roff` = (8g + q)·256 + 8p and `sw` = f(8g + q) are per-lane
+// constants (q = (lane>>2)&3, p = lane&3, g = lane>>4): the transposed read's lane 4q+p addresses
+// row q, columns 4p..4p+3.  Inline asm, not the builtin: hipcc (ROCm 7.2) treats the builtin as
+// aliasing the in-flight LDS-DMA and drains vmcnt(0) before every fragment read, which would
+// serialise the pipeline; the consumer (mma) waits lgkmcnt(0) + sched_barrier itself.
+__device__ __forceinline__ bf16x8_t trfrag(uint32_t img, int roff, int sw, int cblk, int ks) {
+  const uint32_t a = img + roff + ((cblk ^ sw) << 5) + ks * (32 * 256);
+  typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+  u32x2 lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a) : "memory");
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:1024" : "=v"(hi) : "v"(a) : "memory");
+  typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+  const u32x4 u = {lo[0], lo[1], hi[0], hi[1]};
+  return __builtin_bit_cast(bf16x8_t, u);
+}
+
+template <int ABL>
+__global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                                                              float* __restrict__ part, int T, int N, int K, int S,
+                                                              int tiles_k) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+
+  // bijective XCD remap; consecutive ids on an XCD = the same token range (split) over neighbouring
+  // output tiles, so co-resident blocks share their dy / x slabs through that XCD's L2
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tiles = nwg / S;
+  const int split = id / tiles, tile = id % tiles;
+  const int n0 = (tile / tiles_k) * 256, k0 = (tile % tiles_k) * 256;
+  const int nkt = T / BT;
+  const int kt0 = (int)((long)split * nkt / S), kt1 = (int)((long)(split + 1) * nkt / S);
+  const int nt = kt1 - kt0;
+  HQ_DASSERT(n0 + 256 <= N && k0 + 256 <= K && nt >= 2);
+
+  const uint16_t* Ab = A + (size_t)kt0 * BT * N + n0;
+  const uint16_t* Bb = B + (size_t)kt0 * BT * K + k0;
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, nt * BT * N * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, nt * BT * K * 2, 0x00020000);
+
+  // staging: wave w moves rows (2w + i)·4 … +3 of a half (1 KiB per instruction, lane-linear:
+  // lane L → row +L/16, 16-B slot L%16), loading the source chunk that the swizzle places there
+  int voA[2], voB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 4 + (lane >> 4);
+    const int pos = lane & 15;
+    const int c16 = ((((pos >> 1) ^ tswz(row))) << 1) | (pos & 1);
+    voA[i] = (row * N + c16 * 8) * 2;
+    voB[i] = (row * K + c16 * 8) * 2;
+  }
+  auto stage = [&](const __amdgpu_buffer_rsrc_t& rs, const int (&vo)[2], int ld, int half, int t, char* img) {
+    if constexpr ((ABL & 1) != 0) return;
+    char* dst = img + wave_u * 2048;
+    const int so = half * 256 + t * BT * ld * 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + i * 1024), 16, vo[i], so, 0, 0);
+  };
+  auto stA = [&](int half, int t) { stage(rA, voA, N, half, t, smem + (t & 1) * STAGE + half * HALF); };
+  auto stB = [&](int half, int t) { stage(rB, voB, K, half, t, smem + (t & 1) * STAGE + (2 + half) * HALF); };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int roff = (8 * g + qq) * 256 + 8 * pp;
+  const int sw = tswz(8 * g + qq);
+  bf16x8_t af[2][4], bf0[2][2], bf1[2][2];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  auto readA = [&](int t, int mh) {
+    if constexpr ((ABL & 2) != 0) { if (t > 0) return; }
+    const uint32_t img = lds0 + (t & 1) * STAGE + mh * HALF;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[ks][i] = trfrag(img, roff, sw, wm * 4 + i, ks);
+  };
+  auto readB = [&](int t, int nh, bf16x8_t (&bf)[2][2]) {
+    if constexpr ((ABL & 2) != 0) { if (t > 0) return; }
+    const uint32_t img = lds0 + (t & 1) * STAGE + (2 + nh) * HALF;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[ks][j] = trfrag(img, roff, sw, wn * 2 + j, ks);
+  };
+  auto mma = [&](int mh, int nh, const bf16x8_t (&bf)[2][2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);   // keep the MFMAs below the wait (playbook rule 18)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mh * 4 + i][nh * 2 + j] = mfma16(bf[ks][j], af[ks][i], acc[mh * 4 + i][nh * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = []() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // prologue (always real loads): tile 0 A0 B0 B1 A1, tile 1 A0 B0; retire A0(0), B0(0)
+  {
+    auto pro = [&](const __amdgpu_buffer_rsrc_t& rs, const int (&vo)[2], int ld, int half, int t, char* img) {
+      char* dst = img + wave_u * 2048;
+      const int so = half * 256 + t * BT * ld * 2;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + i * 1024), 16, vo[i], so, 0, 0);
+    };
+    pro(rA, voA, N, 0, 0, smem + 0 * HALF);
+    pro(rB, voB, K, 0, 0, smem + 2 * HALF);
+    pro(rB, voB, K, 1, 0, smem + 3 * HALF);
+    pro(rA, voA, N, 1, 0, smem + 1 * HALF);
+    pro(rA, voA, N, 0, 1, smem + STAGE + 0 * HALF);
+    pro(rB, voB, K, 0, 1, smem + STAGE + 2 * HALF);
+  }
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  bar();
+
+  // schedule and hazard proof: gemm.hip, gemm_nt2_kernel (identical phase / stage / wait table)
+  auto ktile = [&](int t) {
+    const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
+    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    readB(t, 0, bf0);
+    readA(t, 0);
+    if (more1) stB(1, t + 1);
+    bar();
+    mma(0, 0, bf0);
+    bar();
+    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    readB(t, 1, bf1);
+    if (more1) stA(1, t + 1);
+    bar();
+    mma(0, 1, bf1);
+    bar();
+    readA(t, 1);
+    if (more2) stA(0, t + 2);
+    bar();
+    mma(1, 1, bf1);
+    bar();
+    if (more1) {
+      if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    if (more2) stB(0, t + 2);
+    bar();
+    mma(1, 0, bf0);
+    bar();
+  };
+  if (__builtin_amdgcn_readfirstlane(wm) == 0) {
+    for (int t = 0; t < nt; ++t) ktile(t);
+    bar();
+  } else {
+    bar();
+    for (int t = 0; t < nt; ++t) ktile(t);
+  }
+
+  // epilogue: fp32 slab, straight from the accumulators (lane: output row n, 4 consecutive k)
+  float* out = part + (size_t)split * N * K;
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int I = 0; I < 8; ++I) {
+    const int row = n0 + (I >> 2) * 128 + wm * 64 + (I & 3) * 16 + fr;
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+      const int col = k0 + (J >> 1) * 128 + wn * 32 + (J & 1) * 16 + fq * 4;
+      *reinterpret_cast<float4*>(out + (size_t)row * K + col) = make_float4(acc[I][J][0], acc[I][J][1], acc[I][J][2], acc[I][J][3]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(const float4* __restrict__ part, int S, size_t n4,
+                                                            float4* __restrict__ out, int accumulate) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    float4 a = accumulate ? out[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    int s = 0;
+    for (; s + 4 <= S; s += 4) {
+      const float4 p0 = part[(size_t)s * n4 + i], p1 = part[(size_t)(s + 1) * n4 + i];
+      const float4 p2 = part[(size_t)(s + 2) * n4 + i], p3 = part[(size_t)(s + 3) * n4 + i];
+      a.x += (p0.x + p1.x) + (p2.x + p3.x);
+      a.y += (p0.y + p1.y) + (p2.y + p3.y);
+      a.z += (p0.z + p1.z) + (p2.z + p3.z);
+      a.w += (p0.w + p1.w) + (p2.w + p3.w);
+    }
+    for (; s < S; ++s) {
+      const float4 p = part[(size_t)s * n4 + i];
+      a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
+    }
+    out[i] = a;
+  }
+}
+
+}  // namespace
+
+int hq_gemm_tn_splits(int T, int N, int K) {
+  if (T % BT || N % 256 || K % 256 || N < 256 || K < 256) return 0;
+  if ((size_t)T * N * 2 >= (1ull << 31) || (size_t)T * K * 2 >= (1ull << 31)) return 0;
+  const int tiles = (N / 256) * (K / 256);
+  int S = 256 / tiles;                     // one full round of the 256 CUs
+  if (S < 1) S = 1;
+  const int nkt = T / BT;
+  while (S > 1 && nkt / S < 8) --S;        // keep >= 8 K-tiles per block (prologue amortised)
+  if (nkt < 2) return 0;
+  return S;
+}
+
+void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, int T, int N, int K, int S, bool accumulate,
+                hipStream_t s) {
+  constexpr size_t lds = 2 * STAGE;
+  static bool init = [] {
+    (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    return true;
+  }();
+  (void)init;
+  const int tiles_k = K / 256, tiles = (N / 256) * tiles_k;
+  hipLaunchKernelGGL((gemm_tn_kernel<0>), dim3(tiles * S), dim3(kThreads), lds, s, A, B, part, T, N, K, S, tiles_k);
+  const size_t n4 = (size_t)N * K / 4;
+  const int grid = (int)std::min<size_t>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, (const float4*)part, S, n4, (float4*)out,
+                     accumulate ? 1 : 0);
+}

@@ -88,8 +88,8 @@ def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale
 #   HQ_GEMM=auto (default): the GEMMs whose epilogue fuses an elementwise pass — FFN1 + GELU,
 #     FFN2-dgrad + dGELU + FFN1 bias-grad (1.08x / 1.40x vs hipBLASLt + separate kernel at b256,
 #     profiles/) and the QKV dgrad + residual-gradient add (torch.addmm first copies the residual
-#     into the output: +56 µs at b256), plus the plain long-K (K >= 2048) dgrads where the v2 kernel
-#     is 1.04x hipBLASLt — when the 256-row tile grid fills the 256 CUs to >= 85 %.
+#     into the output: +56 µs at b256), plus the plain dgrads — when the 256-row tile grid fills the
+#     256 CUs to >= 85 %.  Weight gradients always take the split-K TN kernel (gemm_tn.hip).
 #     Plain forward projections stay on hipBLASLt with the shipped TunableOp picks (2-13 % faster);
 #   HQ_GEMM=mfma: every supported shape;  HQ_GEMM=blas: none.
 _EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID = range(5)
@@ -114,9 +114,9 @@ def _mfma(M: int, N: int, K: int, kind: str = "plain") -> bool:
         return True
     tiles = (M // 256) * (N // bn)
     fill = tiles / (-(-tiles // _CUS) * _CUS)
-    if kind == "dgrad":  # plain long-K dgrad: v2 kernel 1.03-1.04x hipBLASLt at b256 (profiles/)
-        return fill >= 0.85 and K >= 2048
-    return fill >= 0.85 and kind in ("dgelu", "gelu", "resid")
+    # plain dgrads (dy·W through the Wᵀ copy): v2 is 1.04x hipBLASLt's NT kernel on long K and beats the
+    # NN kernel torch.mm(dy, W) dispatches at K = 768 (123 vs 136 µs at b256, profiles/s2_*)
+    return fill >= 0.85 and kind in ("dgelu", "gelu", "resid", "dgrad")
 
 
 def linear_fwd(x, w, b, b32=None):
@@ -194,10 +194,18 @@ def _wgrad_splits(T: int, N: int, K: int) -> int:
 
 
 def linear_wgrad(dy, x, g_w, g_b, accumulate):
-    """g_w (fp32 arena view) (+)= dyᵀ·x with fp32 GEMM output; g_b (+)= column sums of dy."""
+    """g_w (fp32 arena view) (+)= dyᵀ·x with fp32 GEMM output; g_b (+)= column sums of dy.
+    GPU: the hand-written split-K TN MFMA kernel (gemm_tn.hip; 1.14-1.31x hipBLASLt's batched split-K
+    on the BERT shapes, profiles/) whenever the shape tiles (N, K multiples of 256, T of 64);
+    hipBLASLt otherwise (``HQ_GEMM=blas`` forces it)."""
     if dy.is_cuda:
         T, N = dy.shape
         K = x.shape[1]
+        if _GEMM_MODE != "blas" and g_w.is_contiguous() and _k().gemm_tn_splits(T, N, K) > 0:
+            _k().gemm_tn(dy, x, g_w, bool(accumulate))
+            if g_b is not None:
+                _k().bias_grad(dy, g_b, bool(accumulate))
+            return
         s = _wgrad_splits(T, N, K)
         if s > 1:
             part = torch.bmm(dy.view(s, T // s, N).transpose(1, 2), x.view(s, T // s, K), out_dtype=torch.float32)

@@ -102,3 +102,49 @@ def test_gemm_nt_repeatable_large(cuda, M, N, K):
     _close(first, _ref(A, B))
     for _ in range(8):
         assert torch.equal(k.gemm_nt(A, B, EPI_NONE), first)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,N,K", [(128, 256, 256), (1024, 768, 256), (4096, 2304, 768), (2048, 768, 3072),
+                                   (24576, 768, 768)])
+def test_gemm_tn_wgrad(cuda, T, N, K, variant):
+    """dW = dyᵀ·x (split-K TN kernel, fp32 out) vs fp32 torch, default and forced split counts,
+    plain and accumulating; bitwise repeatable."""
+    if variant:
+        pytest.skip("TN kernel has a single variant")
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(T + N + K)
+    dy = (torch.rand(T, N, device=cuda, generator=g) * 2 - 1).bfloat16()
+    x = (torch.rand(T, K, device=cuda, generator=g) * 2 - 1).bfloat16()
+    ref = dy.float().t() @ x.float()
+    out = torch.empty(N, K, device=cuda)
+    assert k.gemm_tn_splits(T, N, K) >= 1
+    k.gemm_tn(dy, x, out, False)
+    torch.testing.assert_close(out, ref, atol=1e-3 * T ** 0.5, rtol=1e-3)
+    first = out.clone()
+    for _ in range(3):
+        k.gemm_tn(dy, x, out, False)
+        assert torch.equal(out, first)
+    for s in (1, 3):
+        if T // 64 // s >= 2:
+            k.gemm_tn(dy, x, out, False, s)
+            torch.testing.assert_close(out, ref, atol=1e-3 * T ** 0.5, rtol=1e-3)
+    base = torch.randn(N, K, device=cuda, generator=g)
+    acc = base.clone()
+    k.gemm_tn(dy, x, acc, True)
+    torch.testing.assert_close(acc, base + ref, atol=1e-3 * T ** 0.5, rtol=1e-3)
+
+
+@pytest.mark.gpu
+def test_gemm_tn_asymmetric(cuda, variant):
+    """Integer data with an asymmetric pattern: catches transposed / misplaced output tiles exactly."""
+    if variant:
+        pytest.skip("TN kernel has a single variant")
+    k = _native.kernels()
+    T, N, K = 256, 512, 256
+    t = torch.arange(T, device=cuda)
+    dy = ((t[:, None] * 3 + torch.arange(N, device=cuda)[None, :] * 7) % 5 - 2).float().bfloat16()
+    x = ((t[:, None] * 5 + torch.arange(K, device=cuda)[None, :] * 11) % 7 - 3).float().bfloat16()
+    out = torch.empty(N, K, device=cuda)
+    k.gemm_tn(dy, x, out, False)
+    assert torch.equal(out, dy.float().t() @ x.float())
