@@ -172,7 +172,7 @@ Tensor gemm_nt(Tensor A, Tensor B, int64_t epi, c10::optional<Tensor> bias, c10:
 // Weight gradient: out [N,K] f32 (+)= dyᵀ·x with dy [T,N], x [T,K] bf16; split-K slabs from the caching allocator.
 int64_t gemm_tn_splits(int64_t T, int64_t N, int64_t K) { return hq_gemm_tn_splits((int)T, (int)N, (int)K); }
 
-void gemm_tn(Tensor dy, Tensor x, Tensor out, bool accumulate, int64_t splits) {
+void gemm_tn(Tensor dy, Tensor x, Tensor out, bool accumulate, int64_t splits, c10::optional<Tensor> bias_out) {
   check(dy, BF16, "dy"); check(x, BF16, "x"); check(out, F32, "out");
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "gemm_tn: dy [T,N], x [T,K]");
   const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
@@ -181,10 +181,16 @@ void gemm_tn(Tensor dy, Tensor x, Tensor out, bool accumulate, int64_t splits) {
   TORCH_CHECK(auto_s > 0, "gemm_tn: unsupported shape T=", T, " N=", N, " K=", K, " (need T%64, N%256, K%256 == 0)");
   const int S = splits > 0 ? (int)splits : auto_s;
   TORCH_CHECK(T / 64 / S >= 2, "gemm_tn: too many splits");
+  const bool has_bias = bias_out.has_value() && bias_out->defined();
+  if (has_bias) {
+    check(*bias_out, F32, "bias_out");
+    TORCH_CHECK(bias_out->numel() == N, "gemm_tn: bias_out must hold N");
+  }
   c10::DeviceGuard g(dy.device());
   Tensor part = at::empty({S, N, K}, out.options());
-  hq_gemm_tn(ptr<uint16_t>(dy), ptr<uint16_t>(x), ptr<float>(part), ptr<float>(out), (int)T, (int)N, (int)K, S, accumulate,
-             cur_stream());
+  Tensor bpart = has_bias ? at::empty({S, N}, out.options()) : Tensor();
+  hq_gemm_tn(ptr<uint16_t>(dy), ptr<uint16_t>(x), ptr<float>(part), ptr<float>(out), has_bias ? ptr<float>(bpart) : nullptr,
+             has_bias ? ptr<float>(*bias_out) : nullptr, (int)T, (int)N, (int)K, S, accumulate, cur_stream());
 }
 
 void transpose_tiles(Tensor src, Tensor dst, Tensor tiles) {
@@ -388,7 +394,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_set_variant", [](int64_t v) { hq_gemm_set_variant((int)v); });
   m.def("gemm_tn", &gemm_tn, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("accumulate") = false,
-        py::arg("splits") = 0);
+        py::arg("splits") = 0, py::arg("bias_out") = py::none());
   m.def("gemm_tn_splits", &gemm_tn_splits);
   m.def("transpose_tiles", &transpose_tiles);
   m.def("colsum_into", &colsum_into);

@@ -75,11 +75,12 @@ void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
                 float* part, int M, int N, int K, int lda, int ldb, int ldc, int epi, int bn, hipStream_t s);
 
 // Weight-gradient GEMM (gemm_tn.hip): out[N,K] (+)= Aᵀ·B, A = dy [T,N] bf16, B = x [T,K] bf16 (token-major),
-// split-K over T into S fp32 slabs part[S][N][K] (caller-provided) reduced into out.
+// split-K over T into S fp32 slabs part[S][N][K] (caller-provided) reduced into out; with bout != null
+// also the fused bias gradient bout[N] (+)= Σ_t A[t, n] through slabs bpart[S][N].
 // hq_gemm_tn_splits: the split count for this shape, 0 = unsupported (need T%64, N%256, K%256 == 0).
 int hq_gemm_tn_splits(int T, int N, int K);
-void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, int T, int N, int K, int S, bool accumulate,
-                hipStream_t s);
+void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, float* bpart, float* bout, int T, int N, int K,
+                int S, bool accumulate, hipStream_t s);
 
 // tiles: int32 [ntiles][6] = (src_off, dst_off, rows, cols, r0, c0); src [rows][cols] -> dst [cols][rows]
 void hq_transpose_tiles(const uint16_t* src, uint16_t* dst, const int* tiles, int ntiles, hipStream_t s);

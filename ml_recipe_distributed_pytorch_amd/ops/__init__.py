@@ -202,8 +202,8 @@ def linear_wgrad(dy, x, g_w, g_b, accumulate):
         T, N = dy.shape
         K = x.shape[1]
         if _GEMM_MODE != "blas" and g_w.is_contiguous() and _k().gemm_tn_splits(T, N, K) > 0:
-            _k().gemm_tn(dy, x, g_w, bool(accumulate))
-            if g_b is not None:
+            _k().gemm_tn(dy, x, g_w, bool(accumulate), 0, g_b if (g_b is not None and g_b.is_contiguous()) else None)
+            if g_b is not None and not g_b.is_contiguous():
                 _k().bias_grad(dy, g_b, bool(accumulate))
             return
         s = _wgrad_splits(T, N, K)

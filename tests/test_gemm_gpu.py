@@ -133,6 +133,16 @@ def test_gemm_tn_wgrad(cuda, T, N, K, variant):
     acc = base.clone()
     k.gemm_tn(dy, x, acc, True)
     torch.testing.assert_close(acc, base + ref, atol=1e-3 * T ** 0.5, rtol=1e-3)
+    # fused bias gradient (column sums of dy), plain and accumulating
+    db_ref = dy.float().sum(0)
+    db = torch.full((N,), 7.0, device=cuda)
+    k.gemm_tn(dy, x, out, False, 0, db)
+    torch.testing.assert_close(out, ref, atol=1e-3 * T ** 0.5, rtol=1e-3)
+    torch.testing.assert_close(db, db_ref, atol=1e-3 * T ** 0.5, rtol=1e-3)
+    b0 = torch.randn(N, device=cuda, generator=g)
+    db = b0.clone()
+    k.gemm_tn(dy, x, acc, True, 0, db)
+    torch.testing.assert_close(db, b0 + db_ref, atol=1e-3 * T ** 0.5, rtol=1e-3)
 
 
 @pytest.mark.gpu
