@@ -201,6 +201,7 @@ void transpose_tiles(Tensor src, Tensor dst, Tensor tiles) {
   hq_transpose_tiles(ptr<uint16_t>(src), ptr<uint16_t>(dst), ptr<int>(tiles), (int)tiles.size(0), cur_stream());
 }
 
+// out (+)= Σ_rows part.  `part` is scratch: the two-pass reduction overwrites some of its rows.
 void colsum_into(Tensor part, Tensor out, bool accumulate) {
   check(part, F32, "part"); check(out, F32, "out");
   TORCH_CHECK(part.dim() == 2 && part.size(1) == out.numel(), "colsum_into: part [P,N] / out [N]");

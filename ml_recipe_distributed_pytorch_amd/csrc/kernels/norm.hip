@@ -483,19 +483,26 @@ __global__ __launch_bounds__(256) void colpart_kernel(const uint16_t* __restrict
 }
 
 // out[q*H + c] (+)= Σ_p part[p][q][c]   for the columns named by (Q, H): part is [P][Q*H].
-// One 1024-thread block per 64 columns; 16 waves stride over P; LDS combine.  Deterministic.
-__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ part, int P, int N, HqOuts outs, int Hq, int accumulate) {
+// One 1024-thread block per 64 columns; 16 waves stride over the logical rows p < P, which live at
+// physical rows p·Pphys/P (Pphys == P: all rows; otherwise the chunk heads of colsum_chunk_kernel).
+// LDS combine.  Deterministic.
+__global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ part, int P, int N, HqOuts outs, int Hq,
+                                                      int accumulate, int Pphys) {
   __shared__ float red[16][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int col = blockIdx.x * 64 + lane;
   float s = 0.f;
   if (col < N) {
-    int p = wave;
-    for (; p + 48 < P; p += 64) {
-      s += part[(size_t)p * N + col] + part[(size_t)(p + 16) * N + col] + part[(size_t)(p + 32) * N + col] +
-           part[(size_t)(p + 48) * N + col];
+    if (Pphys == P) {
+      int p = wave;
+      for (; p + 48 < P; p += 64) {
+        s += part[(size_t)p * N + col] + part[(size_t)(p + 16) * N + col] + part[(size_t)(p + 32) * N + col] +
+             part[(size_t)(p + 48) * N + col];
+      }
+      for (; p < P; p += 16) s += part[(size_t)p * N + col];
+    } else {
+      for (int p = wave; p < P; p += 16) s += part[(size_t)((long)p * Pphys / P) * N + col];
     }
-    for (; p < P; p += 16) s += part[(size_t)p * N + col];
   }
   red[wave][lane] = s;
   __syncthreads();
@@ -508,6 +515,28 @@ __global__ __launch_bounds__(1024) void colsum_kernel(const float* __restrict__ 
       const int c = col % Hq;
       out[c] = accumulate ? out[c] + t : t;
     }
+  }
+}
+
+// First pass for tall partial matrices: block (x, c) sums rows [c·P/C, (c+1)·P/C) of its 64 columns
+// and writes the sum over the chunk's FIRST row (a row only this block reads), so the pass needs no
+// scratch and stays deterministic; colsum_kernel then folds the C chunk heads.  The single-pass
+// kernel ran only N/64 blocks (36 for a 2304-column LayerNorm partial of 3072 rows: ~20 µs).
+__global__ __launch_bounds__(1024) void colsum_chunk_kernel(float* __restrict__ part, int P, int N, int C) {
+  __shared__ float red[16][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int col = blockIdx.x * 64 + lane;
+  const int r0 = (int)((long)blockIdx.y * P / C), r1 = (int)((long)(blockIdx.y + 1) * P / C);
+  float s = 0.f;
+  if (col < N)
+    for (int p = r0 + wave; p < r1; p += 16) s += part[(size_t)p * N + col];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && col < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w][lane];
+    part[(size_t)r0 * N + col] = t;
   }
 }
 
@@ -527,7 +556,10 @@ void dispatch_nch(int H, F&& f) {
 }
 
 void colsum(const float* part, int P, int N, HqOuts outs, int Hq, bool accumulate, hipStream_t s) {
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, part, P, N, outs, Hq, accumulate ? 1 : 0);
+  const int C = P >= 128 ? std::min(32, P / 32) : P;
+  if (C < P)
+    hipLaunchKernelGGL(colsum_chunk_kernel, dim3((N + 63) / 64, C), dim3(1024), 0, s, const_cast<float*>(part), P, N, C);
+  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, part, C, N, outs, Hq, accumulate ? 1 : 0, P);
 }
 
 }  // namespace
