@@ -357,9 +357,25 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
       for (int j = 0; j < 8; ++j) dpart += x[j] * y[j];
     }
   }
+  // this wave's dropout keep-bit words for all key tiles, staged in LDS with the K/V prologue: loaded
+  // per tile they exposed a full HBM round trip (global load → vmcnt(0)) in every iteration
+  uint16_t* sM = reinterpret_cast<uint16_t*>(sB + Lp) + wave * n32 * 64;
+  constexpr int kMaxT = 16;
+  uint16_t mw[kMaxT];
+  const uint16_t* gbits = mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane;
+  if constexpr (DROP) {
+#pragma unroll
+    for (int t = 0; t < kMaxT; ++t)
+      if (t < n32 && qs < n32) mw[t] = gbits[(size_t)t * 64];
+  }
   load_head<NWB * 64>(sK, base + H, ld, L, Lp);
   load_head<NWB * 64>(sV, base + 2 * H, ld, L, Lp);
   for (int t = threadIdx.x; t < Lp; t += NWB * 64) sB[t] = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -INFINITY;
+  if constexpr (DROP) {
+#pragma unroll
+    for (int t = 0; t < kMaxT; ++t)
+      if (t < n32 && qs < n32) sM[t * 64 + lane] = mw[t];
+  }
   const float dlt = xor32_sum(dpart);  // δ = rowsum(dO·O) over all 64 dims
   const float lq = qok ? lse[(size_t)bh * L + qi] * LOG2E : INFINITY;
   if (qok && hh == 0) delta[(size_t)bh * L + qi] = dlt;
@@ -373,8 +389,6 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
   for (int d = 0; d < 2; ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
-  const uint16_t* my_bits = mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane;
-
   const f2_t dl2 = {dlt, dlt};
 #pragma unroll UNR
   for (int kt = 0; kt < n32; ++kt) {
@@ -395,7 +409,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
     uint32_t bits = 0xFFFFu;
     float ks = 1.f;
     if constexpr (DROP) {
-      bits = (uint32_t)my_bits[(size_t)kt * 64];
+      bits = (uint32_t)sM[kt * 64 + lane];
       ks = kscale;
     }
     float ds[16];
@@ -447,7 +461,8 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
   const int bh = blockIdx.x, b = bh / nh, h = bh % nh;
   HQ_DASSERT(L > 0 && L <= 512 && (NT == 0 || L == NT * 32));
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, hh = lane >> 5;
-  uint16_t* sW = reinterpret_cast<uint16_t*>(sD + Lp) + wave * 64;  // this wave's keep-bit words of one tile
+  // this wave's keep-bit words of every query tile, [tile][64], staged in LDS by the prologue
+  uint16_t* sW = reinterpret_cast<uint16_t*>(sD + Lp) + wave * n32 * 64;
   const int ks_idx = blockIdx.y * NWB + wave;  // 32-key subtile
   const int kj = ks_idx * 32 + (lane & 31);
   const bool kok = kj < L;
@@ -460,11 +475,23 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
     vf[s] = kok ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)kj * ld + 2 * H + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
   }
   const float kb = kok ? key_bias[(size_t)b * L + kj] * LOG2E : -INFINITY;
+  constexpr int kMaxT = 16;
+  uint16_t mw[kMaxT];
+  if constexpr (DROP) {
+#pragma unroll
+    for (int t = 0; t < kMaxT; ++t)
+      if (t < n32 && ks_idx < n32) mw[t] = mbits[(((size_t)bh * n32 + t) * n32 + ks_idx) * 64 + lane];
+  }
   load_head<NWB * 64, true>(sQ, base, ld, L, Lp, c_scale);  // Q·c, exactly as the forward's
   load_head<NWB * 64>(sO, dctx + (size_t)b * L * H + h * D, H, L, Lp);
   for (int t = threadIdx.x; t < Lp; t += NWB * 64) {
     sL[t] = t < L ? lse[(size_t)bh * L + t] * LOG2E : INFINITY;
     sD[t] = t < L ? delta[(size_t)bh * L + t] : 0.f;
+  }
+  if constexpr (DROP) {
+#pragma unroll
+    for (int t = 0; t < kMaxT; ++t)
+      if (t < n32 && ks_idx < n32) sW[t * 64 + lane] = mw[t];
   }
   __syncthreads();
   if (ks_idx * 32 >= L) return;
@@ -481,11 +508,9 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
   const int hh_f = (krel >> 2) & 1;
   const int r_f = (krel & 3) + 4 * (krel >> 3);
   const float ksc = DROP ? kscale : 1.f;
-  const uint16_t* wsrc = sW + 4 * hh + 32 * hh_f;
   auto tile_mask = [&](int qt, f2_t* mk) {  // mk[r/2] = {mask(r), mask(r+1)} ∈ {0, 1/(1-p)}
     if constexpr (DROP) {
-      sW[lane] = mbits[(((size_t)bh * n32 + qt) * n32 + ks_idx) * 64 + lane];
-      asm volatile("" ::: "memory");  // the u64 reads below alias these u16 stores (no TBAA reordering)
+      const uint16_t* wsrc = sW + qt * 64 + 4 * hh + 32 * hh_f;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const uint64_t w = *reinterpret_cast<const uint64_t*>(wsrc + 8 * g);
@@ -678,8 +703,9 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
   const uint16_t* bits = thr ? mbits : nullptr;
   const int Lp = (L + 31) & ~31, n32 = Lp / 32;
   const int nw = waves_for(L);
-  const size_t lds_dq = (size_t)Lp * D * 2 * 2 + Lp * sizeof(float);
-  const size_t lds_kv = (size_t)Lp * D * 2 * 2 + 2 * Lp * sizeof(float) + (size_t)nw * 64 * sizeof(uint16_t);
+  const size_t lds_bits = bits ? (size_t)nw * n32 * 64 * sizeof(uint16_t) : 0;  // staged keep-bit words
+  const size_t lds_dq = (size_t)Lp * D * 2 * 2 + Lp * sizeof(float) + lds_bits;
+  const size_t lds_kv = (size_t)Lp * D * 2 * 2 + 2 * Lp * sizeof(float) + lds_bits;
   auto run = [&](auto cw, auto cn) {
     constexpr int NW = decltype(cw)::value, NT = decltype(cn)::value;
     const dim3 grid(B * nh, (n32 + NW - 1) / NW);
