@@ -145,36 +145,39 @@ __device__ __forceinline__ float max16(const f32x16_t& a) {
   return fmaxf(m, a[15]);
 }
 
-// Cooperative copy of rows [0, Lp) of a [*, ld] bf16 matrix (64 columns starting at src) into a
-// [Lp][64] LDS image; rows >= L are zero.  Each thread issues all its 16-B loads before any store.
-template <int NT, bool SCALE = false>
-__device__ __forceinline__ void load_head(uint16_t* dst, const uint16_t* src, size_t ld, int L, int Lp,
-                                          float c = 1.f) {
-  constexpr int kMax = 8;  // up to 512 rows × 8 chunks / (NT threads)
-  uint4 buf[kMax];
+// Both head matrices of a kernel's prologue in ONE load phase: every thread issues all its 16-B loads
+// of A and of B before the first LDS store, so the workgroup pays a single exposed HBM latency instead
+// of one per matrix (with one workgroup per CU nothing else hides the prologue).
+template <int NT, bool SCALE_A = false>
+__device__ __forceinline__ void load_heads2(uint16_t* dstA, const uint16_t* srcA, size_t ldA, uint16_t* dstB,
+                                            const uint16_t* srcB, size_t ldB, int L, int Lp, float c = 1.f) {
+  constexpr int kMax = 8;
+  uint4 ba[kMax], bb[kMax];
   const int n = Lp * 8;
 #pragma unroll
   for (int i = 0; i < kMax; ++i) {
     const int t = threadIdx.x + i * NT;
-    buf[i] = make_uint4(0, 0, 0, 0);
-    if (t < n) {
-      const int row = t >> 3;
-      if (row < L) buf[i] = *reinterpret_cast<const uint4*>(src + (size_t)row * ld + (t & 7) * 8);
+    ba[i] = make_uint4(0, 0, 0, 0);
+    bb[i] = make_uint4(0, 0, 0, 0);
+    if (t < n && (t >> 3) < L) {
+      ba[i] = *reinterpret_cast<const uint4*>(srcA + (size_t)(t >> 3) * ldA + (t & 7) * 8);
+      bb[i] = *reinterpret_cast<const uint4*>(srcB + (size_t)(t >> 3) * ldB + (t & 7) * 8);
     }
   }
 #pragma unroll
   for (int i = 0; i < kMax; ++i) {
     const int t = threadIdx.x + i * NT;
     if (t < n) {
-      uint4 v = buf[i];
-      if constexpr (SCALE) {
+      uint4 v = ba[i];
+      if constexpr (SCALE_A) {
         float f[8];
         hq_unpack8(v, f);
 #pragma unroll
         for (int j = 0; j < 8; ++j) f[j] *= c;
         v = hq_pack8(f);
       }
-      *reinterpret_cast<uint4*>(dst + lds_off(t >> 3, (t & 7) * 8)) = v;
+      *reinterpret_cast<uint4*>(dstA + lds_off(t >> 3, (t & 7) * 8)) = v;
+      *reinterpret_cast<uint4*>(dstB + lds_off(t >> 3, (t & 7) * 8)) = bb[i];
     }
   }
 }
@@ -207,8 +210,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
   for (int s = 0; s < 4; ++s)
     qf[s] = (qi < L) ? prescale8(*reinterpret_cast<const bf16x8_t*>(base + (size_t)qi * ld + 16 * s + 8 * hh), c_scale)
                      : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-  load_head<NWB * 64>(sK, base + H, ld, L, Lp);
-  load_head<NWB * 64>(sV, base + 2 * H, ld, L, Lp);
+  load_heads2<NWB * 64>(sK, base + H, ld, sV, base + 2 * H, ld, L, Lp);
   for (int t = threadIdx.x; t < Lp; t += NWB * 64) sB[t] = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -INFINITY;
   __syncthreads();
   if (qs * 32 >= L) return;
@@ -225,16 +227,40 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
   const uint32_t row_idx = ((uint32_t)bh * L + (uint32_t)min(qi, L - 1)) * (uint32_t)L;
   uint16_t* my_bits = mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane;
 
+  // Software pipeline (unrolled NT > 0 path): the per-tile rescale branch splits the loop body into
+  // basic blocks the scheduler cannot cross, so the K-row fragments and bias of tile kt+1 and the
+  // V fragments of tile kt are read explicitly before the softmax of tile kt, hiding LDS latency.
+  bf16x8_t kn[4];
+  float4 bn[4];
+  auto fetch_k = [&](int kt) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) kn[s] = row8(sK, kt * 32, lo_, s);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bn[g] = *reinterpret_cast<const float4*>(sB + kt * 32 + 8 * g + 4 * hh);
+  };
+  if constexpr (NT > 0) fetch_k(0);
+
 #pragma unroll UNR
   for (int kt = 0; kt < n32; ++kt) {
     f32x16_t acc;
+    if constexpr (NT == 0) fetch_k(kt);
 #pragma unroll
     for (int g = 0; g < 4; ++g) {  // accumulator starts at the key-mask bias (log2 domain)
-      const float4 bb = *reinterpret_cast<const float4*>(sB + kt * 32 + 8 * g + 4 * hh);
-      acc[4 * g + 0] = bb.x; acc[4 * g + 1] = bb.y; acc[4 * g + 2] = bb.z; acc[4 * g + 3] = bb.w;
+      acc[4 * g + 0] = bn[g].x; acc[4 * g + 1] = bn[g].y; acc[4 * g + 2] = bn[g].z; acc[4 * g + 3] = bn[g].w;
     }
 #pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma32(row8(sK, kt * 32, lo_, s), qf[s], acc);
+    for (int s = 0; s < 4; ++s) acc = mfma32(kn[s], qf[s], acc);
+    bf16x8_t vt[2][2];
+    constexpr bool kVEarly = NT > 0 && !DROP;  // with dropout the early V fragments would spill (168 VGPRs)
+    if constexpr (NT > 0) {
+      if (kt + 1 < n32) fetch_k(kt + 1);
+    }
+    if constexpr (kVEarly) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) vt[s][d] = tr8(sV, kt * 32, lo_, s, d);
+    }
     const float mx = xor32_max(max16(acc));
     if (__any(mx > m_run)) {  // exact rescale skip: α = 1 for every lane whose max did not grow
       const float m_new = fmaxf(m_run, mx);
@@ -298,7 +324,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
     for (int s = 0; s < 2; ++s) {
       const bf16x8_t pb = pack_b(sc, s);
 #pragma unroll
-      for (int d = 0; d < 2; ++d) o[d] = mfma32(tr8(sV, kt * 32, lo_, s, d), pb, o[d]);
+      for (int d = 0; d < 2; ++d) o[d] = mfma32(kVEarly ? vt[s][d] : tr8(sV, kt * 32, lo_, s, d), pb, o[d]);
     }
   }
   const float l_tot = xor32_sum(l2.x + l2.y);
@@ -368,8 +394,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
     for (int t = 0; t < kMaxT; ++t)
       if (t < n32 && qs < n32) mw[t] = gbits[(size_t)t * 64];
   }
-  load_head<NWB * 64>(sK, base + H, ld, L, Lp);
-  load_head<NWB * 64>(sV, base + 2 * H, ld, L, Lp);
+  load_heads2<NWB * 64>(sK, base + H, ld, sV, base + 2 * H, ld, L, Lp);
   for (int t = threadIdx.x; t < Lp; t += NWB * 64) sB[t] = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -INFINITY;
   if constexpr (DROP) {
 #pragma unroll
@@ -482,8 +507,8 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
     for (int t = 0; t < kMaxT; ++t)
       if (t < n32 && ks_idx < n32) mw[t] = mbits[(((size_t)bh * n32 + t) * n32 + ks_idx) * 64 + lane];
   }
-  load_head<NWB * 64, true>(sQ, base, ld, L, Lp, c_scale);  // Q·c, exactly as the forward's
-  load_head<NWB * 64>(sO, dctx + (size_t)b * L * H + h * D, H, L, Lp);
+  // Q·c (exactly as the forward's) and dO
+  load_heads2<NWB * 64, true>(sQ, base, ld, sO, dctx + (size_t)b * L * H + h * D, H, L, Lp, c_scale);
   for (int t = threadIdx.x; t < Lp; t += NWB * 64) {
     sL[t] = t < L ? lse[(size_t)bh * L + t] * LOG2E : INFINITY;
     sD[t] = t < L ? delta[(size_t)bh * L + t] : 0.f;

@@ -67,7 +67,11 @@ class GradReducer:
         if native is None:
             native = on_gpu and backend == "nccl"
         if self.world > 1 and native:
-            self._native = self._make_native()
+            try:
+                self._native = self._make_native()
+            except Exception as e:  # e.g. RCCL refuses a second communicator: fall back to the PG's own
+                logger.warning(f"native RCCL reducer unavailable ({e}); using torch.distributed all_reduce")
+                self._native = None
         self._build_buckets()
         model.set_grad_listener(self._on_group_ready)
         if self.world > 1 and broadcast_params:
