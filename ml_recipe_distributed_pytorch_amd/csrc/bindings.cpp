@@ -138,17 +138,17 @@ Tensor gemm_nt(Tensor A, Tensor B, int64_t epi, c10::optional<Tensor> bias, c10:
   TORCH_CHECK(M < (1ll << 31) / 4 && N * K < (1ll << 31) && M * N < (1ll << 40), "gemm_nt: shape too large");
   const int bn = hq_gemm_nt_supported((int)M, (int)N, (int)K);
   TORCH_CHECK(bn > 0, "gemm_nt: unsupported shape M=", M, " N=", N, " K=", K, " (need M%256, N%128, K%64 == 0)");
-  TORCH_CHECK(epi >= HQ_EPI_NONE && epi <= HQ_EPI_RESID, "gemm_nt: bad epilogue");
+  TORCH_CHECK(epi >= HQ_EPI_NONE && epi <= HQ_EPI_DMUL, "gemm_nt: bad epilogue");
   c10::DeviceGuard g(A.device());
   Tensor C = (out.has_value() && out->defined()) ? *out : at::empty({M, N}, A.options());
   check(C, BF16, "out");
   TORCH_CHECK(C.size(0) == M && C.size(1) == N, "gemm_nt: out shape");
-  if (epi == HQ_EPI_BIAS || epi == HQ_EPI_GELU) {
+  if (epi == HQ_EPI_BIAS || epi == HQ_EPI_GELU || epi == HQ_EPI_GELUD) {
     TORCH_CHECK(bias.has_value() && bias->defined(), "gemm_nt: bias required");
     check(*bias, F32, "bias");
     TORCH_CHECK(bias->numel() == N, "gemm_nt: bias length");
   }
-  if (epi == HQ_EPI_GELU || epi == HQ_EPI_DGELU) {
+  if (epi == HQ_EPI_GELU || epi == HQ_EPI_DGELU || epi == HQ_EPI_GELUD || epi == HQ_EPI_DMUL) {
     TORCH_CHECK(pre.has_value() && pre->defined(), "gemm_nt: pre required");
     check(*pre, BF16, "pre");
     TORCH_CHECK(pre->size(0) == M && pre->size(1) == N, "gemm_nt: pre shape");
@@ -158,7 +158,7 @@ Tensor gemm_nt(Tensor A, Tensor B, int64_t epi, c10::optional<Tensor> bias, c10:
     check(*resid, BF16, "resid");
     TORCH_CHECK(resid->size(0) == M && resid->size(1) == N, "gemm_nt: resid shape");
   }
-  if (epi == HQ_EPI_DGELU) {
+  if (epi == HQ_EPI_DGELU || epi == HQ_EPI_DMUL) {
     TORCH_CHECK(part.has_value() && part->defined(), "gemm_nt: part required");
     check(*part, F32, "part");
     TORCH_CHECK(part->numel() == (M / 256) * N, "gemm_nt: part must hold [M/256, N]");

@@ -64,12 +64,13 @@ void hq_cast_f32_bf16(const float* src, uint16_t* dst, int64_t n, float scale, h
 void hq_cast_bf16_f32(const uint16_t* src, float* dst, int64_t n, float scale, hipStream_t s);
 
 // ------------------------------------------------------------------ MFMA GEMM (gemm.hip)
-enum { HQ_EPI_NONE = 0, HQ_EPI_BIAS = 1, HQ_EPI_GELU = 2, HQ_EPI_DGELU = 3, HQ_EPI_RESID = 4 };
+enum { HQ_EPI_NONE = 0, HQ_EPI_BIAS = 1, HQ_EPI_GELU = 2, HQ_EPI_DGELU = 3, HQ_EPI_RESID = 4, HQ_EPI_GELUD = 5, HQ_EPI_DMUL = 6 };
 // returns the block N-width the kernel will use for this shape (256 / 128), 0 = unsupported
 int hq_gemm_nt_supported(int M, int N, int K);
 // 0 = auto (v2 deep-pipeline kernel where supported), 1 = v1 kernel only (A/B and fallback)
 void hq_gemm_set_variant(int v);
-// C[M,N] = A[M,K]·B[N,K]^T (+epilogue); P = GELU pre-activation (out for EPI_GELU, in for EPI_DGELU);
+// C[M,N] = A[M,K]·B[N,K]^T (+epilogue); P = GELU pre-activation (out for EPI_GELU, in for EPI_DGELU)
+// or its derivative gelu'(pre) (out for EPI_GELUD, in for EPI_DMUL);
 // R = residual (EPI_RESID); part = [M/256][N] column partial sums (EPI_DGELU)
 void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,
                 float* part, int M, int N, int K, int lda, int ldb, int ldc, int epi, int bn, hipStream_t s);

@@ -9,6 +9,9 @@
 //   EPI_DGELU  C = acc · gelu'(P[m,n])  and per-block column sums of C (the bias gradient of the
 //              producing Linear) into part[M/BM][N]  — replaces the separate gelu_bwd pass
 //   EPI_RESID  C = acc + R[m,n]  (residual-gradient add of dgrad)
+//   EPI_GELUD  as EPI_GELU but P receives gelu'(pre) instead of pre: the forward already evaluates
+//              Φ and φ, so the derivative costs one FMA here and saves the backward ~15 VALU/element
+//   EPI_DMUL   C = acc · P[m,n] (P = stored gelu') + column partials — the backward of EPI_GELUD
 //
 // Structure (CDNA4 playbook §5):
 // * 256×BN block tile, BK = 64, 512 threads = 8 waves as 2 (M) × 4 (N); a wave owns 128 × BN/4.
@@ -187,7 +190,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   for (int j = 0; j < NJ; ++j) {
     const int nl = j * 16 + fq * 4;
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU) bv = *reinterpret_cast<const float4*>(bias + n0 + wn * WN + nl);
+    if constexpr (EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD) bv = *reinterpret_cast<const float4*>(bias + n0 + wn * WN + nl);
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       float v[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
@@ -200,7 +203,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   const int seg = lane % SEGS, rsub = lane / SEGS;
   const int mb = m0 + wm * 128, nb = n0 + wn * WN + seg * 8;
   float csum[8];
-  if constexpr (EPI == HQ_EPI_DGELU) {
+  if constexpr (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[e] = 0.f;
   }
@@ -216,6 +219,25 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
 #pragma unroll
       for (int e = 0; e < 8; ++e) x[e] = gelu_erf(x[e]);
       piece = hq_pack8(x);
+    } else if constexpr (EPI == HQ_EPI_GELUD) {
+      float x[8], g[8];
+      hq_unpack8(piece, x);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float c, d;
+        hq_normal_cdf_pdf(x[e], c, d);
+        g[e] = fmaf(x[e], d, c);   // gelu'(x)
+        x[e] *= c;                 // gelu(x)
+      }
+      *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
+      piece = hq_pack8(x);
+    } else if constexpr (EPI == HQ_EPI_DMUL) {
+      float d[8], gd[8];
+      hq_unpack8(piece, d);
+      hq_unpack8(*reinterpret_cast<const uint4*>(P + goff), gd);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { d[e] *= gd[e]; csum[e] += d[e]; }
+      piece = hq_pack8(d);
     } else if constexpr (EPI == HQ_EPI_DGELU) {
       float d[8], pr[8];
       hq_unpack8(piece, d);
@@ -233,7 +255,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
     }
     *reinterpret_cast<uint4*>(C + goff) = piece;
   }
-  if constexpr (EPI == HQ_EPI_DGELU) {
+  if constexpr (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL) {
     // column sums: lanes with equal `seg` hold the same 8 columns -> xor-reduce over rsub, then the
     // two M-waves through LDS (after everyone is done with its staging region)
 #pragma unroll
@@ -449,7 +471,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
     const int nh = J >> 1, j = J & 1;
     const int lc = nh * 32 + j * 16 + fq * 4;
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU)
+    if constexpr (EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD)
       bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
 #pragma unroll
     for (int I = 0; I < 8; ++I) {
@@ -462,7 +484,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
   const int seg = lane % SEGS, rsub = lane / SEGS;
   const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;   // 4 pieces per 32-col chunk
   float csum[8];
-  if constexpr (EPI == HQ_EPI_DGELU) {
+  if constexpr (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[e] = 0.f;
   }
@@ -479,6 +501,25 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
 #pragma unroll
       for (int e = 0; e < 8; ++e) x[e] = gelu_erf(x[e]);
       piece = hq_pack8(x);
+    } else if constexpr (EPI == HQ_EPI_GELUD) {
+      float x[8], g[8];
+      hq_unpack8(piece, x);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float c, d;
+        hq_normal_cdf_pdf(x[e], c, d);
+        g[e] = fmaf(x[e], d, c);   // gelu'(x)
+        x[e] *= c;                 // gelu(x)
+      }
+      *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
+      piece = hq_pack8(x);
+    } else if constexpr (EPI == HQ_EPI_DMUL) {
+      float d[8], gd[8];
+      hq_unpack8(piece, d);
+      hq_unpack8(*reinterpret_cast<const uint4*>(P + goff), gd);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { d[e] *= gd[e]; csum[e] += d[e]; }
+      piece = hq_pack8(d);
     } else if constexpr (EPI == HQ_EPI_DGELU) {
       float d[8], pr[8];
       hq_unpack8(piece, d);
@@ -496,7 +537,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
     }
     *reinterpret_cast<uint4*>(C + goff) = piece;
   }
-  if constexpr (EPI == HQ_EPI_DGELU) {
+  if constexpr (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL) {
 #pragma unroll
     for (int e = 0; e < 8; ++e)
       for (int o = SEGS; o < 64; o <<= 1) csum[e] += __shfl_xor(csum[e], o, 64);
@@ -581,5 +622,7 @@ void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
     case HQ_EPI_GELU: launch_epi<HQ_EPI_GELU>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
     case HQ_EPI_DGELU: launch_epi<HQ_EPI_DGELU>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
     case HQ_EPI_RESID: launch_epi<HQ_EPI_RESID>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
+    case HQ_EPI_GELUD: launch_epi<HQ_EPI_GELUD>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
+    case HQ_EPI_DMUL: launch_epi<HQ_EPI_DMUL>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
   }
 }

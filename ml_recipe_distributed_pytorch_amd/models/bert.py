@@ -183,9 +183,11 @@ class _LayerFn(torch.autograd.Function):
         if fp8:
             pre = proj(h1, "intermediate.dense")
             act = ops.gelu_fwd(pre)
-        else:
-            pre, act = ops.linear_gelu_fwd(h1, st.view(p + "intermediate.dense.weight"),
-                                           st.view(p + "intermediate.dense.bias"), Bm("intermediate.dense.bias"))
+            ctx.gelu_deriv = False
+        else:  # `pre` holds gelu'(pre) when the fused MFMA epilogue ran (ctx.gelu_deriv)
+            pre, act, ctx.gelu_deriv = ops.linear_gelu_fwd_d(h1, st.view(p + "intermediate.dense.weight"),
+                                                             st.view(p + "intermediate.dense.bias"),
+                                                             Bm("intermediate.dense.bias"))
         a2 = proj(act, "output.dense")
         h2, z2, m2, r2 = ops.ln_fwd(a2, h1, st.view(p + "output.LayerNorm.weight", "master"),
                                     st.view(p + "output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph,
@@ -232,8 +234,8 @@ class _LayerFn(torch.autograd.Function):
         dz2, da2 = ops.ln_bwd(dh2, None, z2, Wm("output.LayerNorm.weight"), m2, r2, ctx.ph, info.seed, op0 + 2,
                               G("output.LayerNorm.weight"), G("output.LayerNorm.bias"), G("output.dense.bias"), acc)
         wgrad(da2, act, G("output.dense.weight"), None)
-        dpre = ops.linear_dgrad_gelu(da2, W("output.dense.weight"), pre, G("intermediate.dense.bias"), acc,
-                                     wt=WT("output.dense.weight"))
+        dpre = ops.linear_dgrad_gelu_d(da2, W("output.dense.weight"), pre, ctx.gelu_deriv,
+                                       G("intermediate.dense.bias"), acc, wt=WT("output.dense.weight"))
         wgrad(dpre, h1, G("intermediate.dense.weight"), None)
         dh1_ffn = ops.linear_dgrad(dpre, W("intermediate.dense.weight"), wt=WT("intermediate.dense.weight"))
         # --- attention block ------------------------------------------------------------------

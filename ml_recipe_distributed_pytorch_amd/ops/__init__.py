@@ -92,8 +92,9 @@ def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale
 #     256 CUs to >= 85 %.  Weight gradients always take the split-K TN kernel (gemm_tn.hip).
 #     Plain forward projections stay on hipBLASLt with the shipped TunableOp picks (2-13 % faster);
 #   HQ_GEMM=mfma: every supported shape;  HQ_GEMM=blas: none.
-_EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID = range(5)
+_EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID, _EPI_GELUD, _EPI_DMUL = range(7)
 _GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
+GELU_DERIV = os.environ.get("HQ_GELU_DERIV", "1") == "1"   # FFN1 stores gelu'(pre) (linear_gelu_fwd_d)
 _CUS = 256
 
 
@@ -145,6 +146,31 @@ def linear_gelu_fwd(x, w, b, b32=None):
         return pre, act
     pre = linear_fwd(x, w, b, b32)
     return pre, gelu_fwd(pre)
+
+
+def linear_gelu_fwd_d(x, w, b, b32=None):
+    """(saved, act, is_deriv): like ``linear_gelu_fwd`` but, on the MFMA path, ``saved`` is gelu'(pre)
+    (bf16) instead of pre — the epilogue evaluates Φ and φ anyway, and the backward then needs one
+    multiply per element instead of a GELU-derivative evaluation (``linear_dgrad_gelu_d``)."""
+    if GELU_DERIV and x.is_cuda and b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1], "gelu"):
+        gd = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
+        act = _k().gemm_nt(x, w, _EPI_GELUD, bias=b32, pre=gd)
+        return gd, act, True
+    pre, act = linear_gelu_fwd(x, w, b, b32)
+    return pre, act, False
+
+
+def linear_dgrad_gelu_d(dy, w, saved, is_deriv, g_bias, accumulate, wt=None):
+    """Backward of ``linear_gelu_fwd_d``: dpre = (dy·W) ⊙ gelu'(pre) with the FFN1 bias gradient."""
+    if not is_deriv:
+        return linear_dgrad_gelu(dy, w, saved, g_bias, accumulate, wt)
+    M, N = dy.shape[0], w.shape[1]
+    assert wt is not None, "stored-derivative GELU backward needs the MFMA path (Wᵀ working copy)"
+    part = torch.empty(M // 256, N, dtype=torch.float32, device=dy.device)
+    dpre = _k().gemm_nt(dy, wt, _EPI_DMUL, pre=saved, part=part)
+    if g_bias is not None:
+        _k().colsum_into(part, g_bias, bool(accumulate))
+    return dpre
 
 
 def linear_dgrad(dy, w, wt=None):

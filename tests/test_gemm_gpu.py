@@ -158,3 +158,29 @@ def test_gemm_tn_asymmetric(cuda, variant):
     out = torch.empty(N, K, device=cuda)
     k.gemm_tn(dy, x, out, False)
     assert torch.equal(out, dy.float().t() @ x.float())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(512, 768, 256), (256, 3072, 768)])
+def test_gemm_nt_gelu_derivative_epilogues(cuda, M, N, K):
+    """EPI_GELUD stores gelu'(pre) next to gelu(pre); EPI_DMUL multiplies the dgrad by it (+ column
+    partials) — together the stored-derivative FFN1 forward/backward pair."""
+    EPI_GELUD, EPI_DMUL = 5, 6
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(9)
+    A = (torch.randn(M, K, device=cuda, generator=g) * 0.5).bfloat16()
+    B = (torch.randn(N, K, device=cuda, generator=g) * 0.1).bfloat16()
+    bias = torch.randn(N, device=cuda, generator=g) * 0.1
+    gd = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    act = k.gemm_nt(A, B, EPI_GELUD, bias=bias, pre=gd)
+    pre = (_ref(A, B) + bias).bfloat16().float()          # the kernel rounds pre to bf16 first
+    x = pre.clone().requires_grad_(True)
+    y = torch.nn.functional.gelu(x)
+    y.backward(torch.ones_like(y))
+    _close(act, y.detach())
+    _close(gd, x.grad, tol=1e-2)
+    part = torch.empty(M // 256, N, device=cuda)
+    d = k.gemm_nt(A, B, EPI_DMUL, pre=gd, part=part)
+    exp = _ref(A, B).bfloat16().float() * gd.float()
+    _close(d, exp)
+    torch.testing.assert_close(part.sum(0), exp.sum(0), atol=5e-2 * (1 + exp.abs().sum(0).max().item() / M), rtol=2e-2)

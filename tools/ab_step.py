@@ -1,0 +1,105 @@
+#!/usr/bin/env python
+"""In-process A/B of full training steps (BERT-base, the bench.py step) under runtime toggles, so small
+per-step differences are not swamped by box-to-box variance.  Rounds alternate A and B; prints the
+median ms/step of each.
+
+    python tools/ab_step.py --toggle gelu_deriv [--batch 256] [--rounds 4] [--steps 8]
+toggles: gelu_deriv (ops.GELU_DERIV), gemm_blas (ops GEMM mode auto vs blas), gemm_v1 (NT kernel v2 vs v1),
+         input_pipeline (on: bench.py's per-step host synthesis + pinned H2D; off: one resident batch)
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+from types import SimpleNamespace
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ml_recipe_distributed_pytorch_amd import _native, ops  # noqa: E402
+from ml_recipe_distributed_pytorch_amd.data.dummy import SpecialIds, synth_batch_native  # noqa: E402
+from ml_recipe_distributed_pytorch_amd.models.bert import BertForQuestionAnswering  # noqa: E402
+from ml_recipe_distributed_pytorch_amd.models.config import get_config  # noqa: E402
+from ml_recipe_distributed_pytorch_amd.models.losses import build_loss  # noqa: E402
+from ml_recipe_distributed_pytorch_amd.ops.tuning import enable_tuned_gemms  # noqa: E402
+from ml_recipe_distributed_pytorch_amd.train.engine import TrainEngine, to_device  # noqa: E402
+from ml_recipe_distributed_pytorch_amd.train.optim import FusedAdamW  # noqa: E402
+from ml_recipe_distributed_pytorch_amd.train.trainer import optimizer_groups  # noqa: E402
+
+
+def set_toggle(name, on):
+    if name == "gelu_deriv":
+        ops.GELU_DERIV = on
+    elif name == "gemm_blas":
+        ops.set_gemm_mode("blas" if on else "auto")
+    elif name == "gemm_v1":
+        _native.kernels().gemm_set_variant(1 if on else 0)
+    elif name == "input_pipeline":
+        pass
+    else:
+        raise SystemExit(f"unknown toggle {name}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--toggle", required=True)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--seq", type=int, default=384)
+    ap.add_argument("--model", default="bert-base-uncased")
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=8)
+    a = ap.parse_args()
+    enable_tuned_gemms()
+    dev = torch.device("cuda", 0)
+    cfg = get_config(a.model)
+    model = BertForQuestionAnswering(cfg, seed=0).to(dev).train()
+    lp = SimpleNamespace(loss="smooth", smooth_alpha=0.01, w_start=1, w_end=1, w_start_reg=1, w_end_reg=1, w_cls=1)
+    opt = FusedAdamW(optimizer_groups(model.named_parameters(), 1e-4), model.store, lr=1e-5, correct_bias=False,
+                     zero_grad_fn=model.zero_grad)
+    eng = TrainEngine(model, build_loss(lp), opt, max_grad_norm=1.0)
+    sp = SpecialIds()
+    batch = synth_batch_native(a.batch, a.seq, 64, sp, seed=0)
+    inputs, labels = to_device(batch[0], dev), to_device(batch[1], dev)
+    from ml_recipe_distributed_pytorch_amd.data.dummy import _refill
+    slots = [synth_batch_native(a.batch, a.seq, 64, sp, seed=i) for i in range(2)]
+    events = [torch.cuda.Event() for _ in slots]
+    for e in events:
+        e.record()
+    cnt = [0]
+
+    def piped():  # bench.py's next_batch
+        i = cnt[0]
+        s = i % 2
+        events[s].synchronize()
+        _refill(slots[s], sp, 64, seed=7919 * (i + 2))
+        di = {k: v.to(dev, non_blocking=True) for k, v in slots[s][0].items()}
+        dl = {k: v.to(dev, non_blocking=True) for k, v in slots[s][1].items()}
+        events[s].record()
+        cnt[0] += 1
+        return di, dl
+
+    def batch_for(on):
+        return piped() if (a.toggle == "input_pipeline" and on) else (inputs, labels)
+    res = {False: [], True: []}
+    for r in range(a.rounds + 1):
+        for on in (False, True):
+            set_toggle(a.toggle, on)
+            eng.step([batch_for(on)])
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.steps):
+                eng.step([batch_for(on)])
+            torch.cuda.synchronize()
+            if r > 0:  # round 0 = warm-up of both arms
+                res[on].append((time.perf_counter() - t0) / a.steps * 1e3)
+    out = {"toggle": a.toggle, "batch": a.batch, "off_ms": round(statistics.median(res[False]), 3),
+           "on_ms": round(statistics.median(res[True]), 3), "off_all": [round(x, 2) for x in res[False]],
+           "on_all": [round(x, 2) for x in res[True]]}
+    out["on_speedup"] = round(out["off_ms"] / out["on_ms"], 4)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
