@@ -193,6 +193,57 @@ void gemm_tn(Tensor dy, Tensor x, Tensor out, bool accumulate, int64_t splits, c
              has_bias ? ptr<float>(*bias_out) : nullptr, (int)T, (int)N, (int)K, S, accumulate, cur_stream());
 }
 
+// fp8 forward projection: C (bf16) = A8·B8ᵀ·sa·sb + bias (f32); GELUD: returns act, writes gelu' into `pre`
+// and, with out8/state given, act as e4m3 (delayed scaling, state f32[4], phase = step % 3).
+int64_t gemm_fp8_supported(int64_t M, int64_t N, int64_t K) { return hq_gemm_fp8_supported((int)M, (int)N, (int)K); }
+
+Tensor gemm_fp8(Tensor A8, Tensor B8, int64_t epi, Tensor bias, Tensor sa, Tensor sb, c10::optional<Tensor> pre,
+                c10::optional<Tensor> out8, c10::optional<Tensor> state, int64_t phase) {
+  TORCH_CHECK(A8.is_cuda() && A8.element_size() == 1 && A8.is_contiguous() && B8.is_cuda() && B8.element_size() == 1 &&
+              B8.is_contiguous(), "gemm_fp8: A8 / B8 must be contiguous 1-byte (e4m3) GPU tensors");
+  TORCH_CHECK(A8.dim() == 2 && B8.dim() == 2 && A8.size(1) == B8.size(1), "gemm_fp8: A8[M,K], B8[N,K]");
+  const int64_t M = A8.size(0), K = A8.size(1), N = B8.size(0);
+  TORCH_CHECK(hq_gemm_fp8_supported((int)M, (int)N, (int)K), "gemm_fp8: unsupported shape M=", M, " N=", N, " K=", K);
+  TORCH_CHECK(epi == HQ_EPI_BIAS || epi == HQ_EPI_GELUD, "gemm_fp8: epilogue must be BIAS or GELUD");
+  check(bias, F32, "bias"); check(sa, F32, "sa"); check(sb, F32, "sb");
+  TORCH_CHECK(bias.numel() == N && sa.numel() >= 1 && sb.numel() >= 1, "gemm_fp8: bias[N], sa, sb");
+  c10::DeviceGuard g(A8.device());
+  Tensor C = at::empty({M, N}, A8.options().dtype(BF16));
+  uint16_t* P = nullptr;
+  uint8_t* C8 = nullptr;
+  float* q8 = nullptr;
+  if (epi == HQ_EPI_GELUD) {
+    TORCH_CHECK(pre.has_value() && pre->defined(), "gemm_fp8: GELUD needs `pre` (gelu' output)");
+    check(*pre, BF16, "pre");
+    TORCH_CHECK(pre->size(0) == M && pre->size(1) == N, "gemm_fp8: pre shape");
+    P = ptr<uint16_t>(*pre);
+    if (out8.has_value() && out8->defined()) {
+      TORCH_CHECK(out8->is_cuda() && out8->element_size() == 1 && out8->is_contiguous() && out8->numel() == M * N,
+                  "gemm_fp8: out8 must be a contiguous 1-byte [M,N] tensor");
+      TORCH_CHECK(state.has_value() && state->defined(), "gemm_fp8: out8 needs the delayed-scaling state");
+      check(*state, F32, "state");
+      TORCH_CHECK(state->numel() == 4, "gemm_fp8: state must be f32[4]");
+      C8 = reinterpret_cast<uint8_t*>(out8->data_ptr());
+      q8 = ptr<float>(*state);
+    }
+  }
+  hq_gemm_fp8(reinterpret_cast<const uint8_t*>(A8.data_ptr()), reinterpret_cast<const uint8_t*>(B8.data_ptr()), ptr<uint16_t>(C),
+              ptr<float>(bias), P, ptr<float>(sa), ptr<float>(sb), C8, q8, (int)(phase % 3), (int)M, (int)N, (int)K,
+              (int)epi, cur_stream());
+  return C;
+}
+
+// x (bf16) -> e4m3 with the delayed scale of `state` (f32[4]); returns y (float8_e4m3fn); state[3] = scale
+Tensor fp8_quant_delayed(Tensor x, Tensor state, int64_t phase) {
+  check(x, BF16, "x"); check(state, F32, "state");
+  TORCH_CHECK(x.numel() % 8 == 0 && state.numel() == 4, "fp8_quant_delayed: numel % 8 / state f32[4]");
+  c10::DeviceGuard g(x.device());
+  auto y = at::empty(x.sizes(), x.options().dtype(at::kFloat8_e4m3fn));
+  hq_fp8_quant_delayed(ptr<uint16_t>(x), reinterpret_cast<uint8_t*>(y.data_ptr()), x.numel(), ptr<float>(state),
+                       (int)(phase % 3), cur_stream());
+  return y;
+}
+
 void transpose_tiles(Tensor src, Tensor dst, Tensor tiles) {
   check(src, BF16, "src"); check(dst, BF16, "dst");
   TORCH_CHECK(tiles.device().is_cuda() && tiles.scalar_type() == at::kInt && tiles.is_contiguous() && tiles.dim() == 2 &&
@@ -400,6 +451,10 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("transpose_tiles", &transpose_tiles);
   m.def("colsum_into", &colsum_into);
   m.def("fp8_quantize", &fp8_quantize);
+  m.def("fp8_quant_delayed", &fp8_quant_delayed);
+  m.def("gemm_fp8_supported", &gemm_fp8_supported);
+  m.def("gemm_fp8", &gemm_fp8, py::arg("A8"), py::arg("B8"), py::arg("epi"), py::arg("bias"), py::arg("sa"), py::arg("sb"),
+        py::arg("pre") = py::none(), py::arg("out8") = py::none(), py::arg("state") = py::none(), py::arg("phase") = 0);
   m.def("span_fwd", &span_fwd);
   m.def("span_bwd", &span_bwd);
   m.def("gelu_bwd", &gelu_bwd);

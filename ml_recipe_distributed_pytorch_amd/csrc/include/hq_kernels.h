@@ -83,6 +83,14 @@ int hq_gemm_tn_splits(int T, int N, int K);
 void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, float* bpart, float* bout, int T, int N, int K,
                 int S, bool accumulate, hipStream_t s);
 
+// fp8 (OCP e4m3) NT GEMM (gemm_fp8.hip): C = A8·B8ᵀ·sa·sb + bias, epi ∈ {HQ_EPI_BIAS, HQ_EPI_GELUD};
+// with C8 != null (GELUD) also act as e4m3 under delayed scaling driven by the 4-float state q8 / phase.
+int hq_gemm_fp8_supported(int M, int N, int K);
+void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, uint16_t* P, const float* sa,
+                 const float* sb, uint8_t* C8, float* q8, int phase, int M, int N, int K, int epi, hipStream_t s);
+// delayed-scaling e4m3 quantiser (one pass): y = x / s(prev amax), amax tracked in q8 (see gemm_fp8.hip)
+void hq_fp8_quant_delayed(const uint16_t* x, uint8_t* y, size_t n, float* q8, int phase, hipStream_t s);
+
 // tiles: int32 [ntiles][6] = (src_off, dst_off, rows, cols, r0, c0); src [rows][cols] -> dst [cols][rows]
 void hq_transpose_tiles(const uint16_t* src, uint16_t* dst, const int* tiles, int ntiles, hipStream_t s);
 // out[c] (+)= sum_p part[p][c], part f32 [P][N]

@@ -1,0 +1,336 @@
+// OCP fp8 (e4m3fn) "NT" GEMM for the --precision fp8 forward projections on gfx950:
+//   C[M,N] = (A8[M,K] · B8[N,K]ᵀ) · sa · sb (+ epilogue),  A8/B8 e4m3, sa/sb per-tensor dequant scales.
+//
+// The pipeline is gemm.hip's v2 (256×256 output tile, 8 ping-ponging waves, four phases per K-tile,
+// one 16 KiB half-panel of buffer_load…lds per phase under a counted vmcnt(6)) with the byte-identical
+// LDS image: a K-tile is 128 fp8 = 128 B per row, exactly the bf16 kernel's 64 × 2 B rows.  What
+// changes is the matrix core: v_mfma_scale_f32_16x16x128_f8f6f4 (block-scaled MX form, unit e8m0
+// scales) consumes a whole 128-deep K-tile per instruction at twice the bf16 FLOP rate, so per LDS
+// byte the MFMA time equals the bf16 kernel's while each K-tile carries twice the K — half the
+// K-tiles, half the load traffic.  Per-tensor scales are applied once in the epilogue.
+//
+// Fragment map (probed with exact integer data, tools/fp8_lab/mfma_probe.hip): lane l holds
+// A[row l&15][32·(l>>4) … +31] and B[col l&15][same k] — 32 contiguous bytes = two swizzled 16-B
+// LDS slots (2·fq, 2·fq+1); C/D is the standard 16×16 map.
+//
+// Epilogues: EPI_BIAS (QKV / out-proj / FFN2) and EPI_GELUD (FFN1: act = gelu(pre), P = gelu'(pre));
+// Q8 additionally writes act as e4m3 for the next fp8 GEMM under DELAYED scaling: the scale is derived
+// from the previous step's amax (slot (phase+2)%3 of the 4-float state), this step's amax accumulates
+// into slot `phase`, slot (phase+1)%3 is cleared for the step after, and the scale used is stored in
+// state[3] for the consumer GEMM's dequantisation.  No host synchronisation anywhere.
+#include <algorithm>
+
+#include "hq_common.h"
+#include "hq_kernels.h"
+
+namespace {
+
+constexpr int BM = 256, BN = 256, BK = 128;  // BK in fp8 elements (= bytes)
+constexpr int kThreads = 512;
+constexpr float kFp8Max = 448.f;
+constexpr float kMargin = 2.f;               // delayed-scaling headroom over last step's amax
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+__device__ __forceinline__ f32x4_t mfma_fp8(const i32x8& a, const i32x8& b, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
+// 32-byte fragment (k = 32·fq … +31) of LDS row `row`: slots 2fq and 2fq+1, source swizzle undone.
+// Inline asm: with plain loads hipcc (ROCm 7.2) drained vmcnt(0) before these reads in this kernel (it
+// could not rule out aliasing with the in-flight LDS-DMA); mma() waits lgkmcnt(0) + sched_barrier.
+__device__ __forceinline__ i32x8 frag32(uint32_t panel, int row, int fq) {
+  const int sw = (row >> 1) & 7;
+  const uint32_t a0 = panel + row * 128 + (((2 * fq) ^ sw) << 4);
+  const uint32_t a1 = panel + row * 128 + (((2 * fq + 1) ^ sw) << 4);
+  typedef __attribute__((ext_vector_type(4))) int i32x4;
+  i32x4 lo, hi;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(lo) : "v"(a0) : "memory");
+  asm volatile("ds_read_b128 %0, %1" : "=v"(hi) : "v"(a1) : "memory");
+  i32x8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return v;
+}
+
+__device__ __forceinline__ float delayed_scale(const float* st, int phase) {
+  const float prev = __uint_as_float(reinterpret_cast<const unsigned*>(st)[(phase + 2) % 3]);
+  return prev > 0.f ? prev * kMargin / kFp8Max : 1.f;   // first step: unit scale
+}
+
+template <int EPI, bool Q8>
+__global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                               uint16_t* __restrict__ C, const float* __restrict__ bias,
+                                                               uint16_t* __restrict__ P, const float* __restrict__ sa,
+                                                               const float* __restrict__ sb, uint8_t* __restrict__ C8,
+                                                               float* __restrict__ q8, int phase, int M, int N, int K,
+                                                               int lda, int ldb, int ldc) {
+  constexpr int PANEL = 256 * 128, STAGE = 2 * PANEL;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tiles_n = N / BN;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  HQ_DASSERT(m0 + BM <= M && n0 + BN <= N && K % BK == 0 && K >= 2 * BK);
+  const uint8_t* Ab = A + (size_t)m0 * lda;
+  const uint8_t* Bb = B + (size_t)n0 * ldb;
+  const int nt = K / BK;
+
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, BM * lda, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, BN * ldb, 0x00020000);
+  int voA[2], voB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * 16 + i * 8 + (lane >> 3);
+    const int src_slot = (lane & 7) ^ ((row >> 1) & 7);
+    voA[i] = row * lda + src_slot * 16;
+    voB[i] = row * ldb + src_slot * 16;
+  }
+  auto half = [&](const __amdgpu_buffer_rsrc_t& rs, const int (&vo)[2], int ld, int h, int t, char* panel) {
+    char* dst = panel + (h * 128 + wave_u * 16) * 128;
+    const int so = h * 128 * ld + t * BK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + i * 8 * 128), 16, vo[i], so, 0, 0);
+  };
+  auto stA = [&](int h, int t) { half(rA, voA, lda, h, t, smem + (t & 1) * STAGE); };
+  auto stB = [&](int h, int t) { half(rB, voB, ldb, h, t, smem + (t & 1) * STAGE + PANEL); };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  i32x8 af[4], bf0[2], bf1[2];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  auto readA = [&](int t, int mh) {
+    const uint32_t pa = lds0 + (t & 1) * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag32(pa, mh * 128 + wm * 64 + i * 16 + fr, fq);
+  };
+  auto readB = [&](int t, int nh, i32x8 (&bf)[2]) {
+    const uint32_t pb = lds0 + (t & 1) * STAGE + PANEL;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bf[j] = frag32(pb, nh * 128 + wn * 32 + j * 16 + fr, fq);
+  };
+  auto mma = [&](int mh, int nh, const i32x8 (&bf)[2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);   // keep the MFMAs below the wait (playbook rule 18)
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[mh * 4 + i][nh * 2 + j] = mfma_fp8(bf[j], af[i], acc[mh * 4 + i][nh * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = []() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  stA(0, 0); stB(0, 0); stB(1, 0); stA(1, 0); stA(0, 1); stB(0, 1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  bar();
+  // phase / stage / wait table and hazard proof: gemm.hip, gemm_nt2_kernel
+  auto ktile = [&](int t) {
+    const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
+    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    readB(t, 0, bf0);
+    readA(t, 0);
+    if (more1) stB(1, t + 1);
+    bar();
+    mma(0, 0, bf0);
+    bar();
+    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    readB(t, 1, bf1);
+    if (more1) stA(1, t + 1);
+    bar();
+    mma(0, 1, bf1);
+    bar();
+    readA(t, 1);
+    if (more2) stA(0, t + 2);
+    bar();
+    mma(1, 1, bf1);
+    bar();
+    if (more1) {
+      if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    if (more2) stB(0, t + 2);
+    bar();
+    mma(1, 0, bf0);
+    bar();
+  };
+  if (__builtin_amdgcn_readfirstlane(wm) == 0) {
+    for (int t = 0; t < nt; ++t) ktile(t);
+    bar();
+  } else {
+    bar();
+    for (int t = 0; t < nt; ++t) ktile(t);
+  }
+
+  // ---- epilogue: acc · (sa·sb) (+bias) -> bf16 staging (as gemm.hip v2), then row-coalesced pieces
+  const float dq = sa[0] * sb[0];
+  constexpr int WN = 64, RS = WN * 2 + 16;
+  char* wreg = smem + wave * (128 * RS);
+#pragma unroll
+  for (int J = 0; J < 4; ++J) {
+    const int nh = J >> 1, j = J & 1;
+    const int lc = nh * 32 + j * 16 + fq * 4;
+    const float4 bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
+#pragma unroll
+    for (int I = 0; I < 8; ++I) {
+      float v[4] = {fmaf(acc[I][J][0], dq, bv.x), fmaf(acc[I][J][1], dq, bv.y), fmaf(acc[I][J][2], dq, bv.z),
+                    fmaf(acc[I][J][3], dq, bv.w)};
+      *reinterpret_cast<uint2*>(wreg + (I * 16 + fr) * RS + lc * 2) = hq_pack4(v);
+    }
+  }
+  float s8 = 1.f, inv8 = 1.f, amax = 0.f;
+  if constexpr (Q8) {
+    s8 = delayed_scale(q8, phase);
+    inv8 = 1.f / s8;
+  }
+  constexpr int SEGS = WN / 8, ROWS_PER_IT = 64 / SEGS;
+  const int seg = lane % SEGS, rsub = lane / SEGS;
+  const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;
+#pragma unroll 4
+  for (int it = 0; it < 128 / ROWS_PER_IT; ++it) {
+    const int lr = it * ROWS_PER_IT + rsub;
+    const int grow = m0 + (lr >> 6) * 128 + wm * 64 + (lr & 63);
+    uint4 piece = *reinterpret_cast<const uint4*>(wreg + lr * RS + seg * 16);
+    const size_t goff = (size_t)grow * ldc + gcol;
+    if constexpr (EPI == HQ_EPI_GELUD) {
+      float x[8], g[8];
+      hq_unpack8(piece, x);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float c, d;
+        hq_normal_cdf_pdf(x[e], c, d);
+        g[e] = fmaf(x[e], d, c);
+        x[e] *= c;
+      }
+      *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
+      piece = hq_pack8(x);
+      if constexpr (Q8) {
+        float f[8];
+        hq_unpack8(piece, f);   // quantise the bf16-rounded act, exactly what the bf16 copy holds
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          amax = fmaxf(amax, fabsf(f[e]));
+          f[e] = fminf(fmaxf(f[e] * inv8, -kFp8Max), kFp8Max);
+        }
+        uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+        lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+        uint32_t hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+        hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+        *reinterpret_cast<uint2*>(C8 + goff) = make_uint2(lo, hi);
+      }
+    }
+    *reinterpret_cast<uint4*>(C + goff) = piece;
+  }
+  if constexpr (Q8) {
+    // one atomic per BLOCK: per-wave atomics on the single amax word serialised in L2 (~+300 µs/call)
+    amax = hq_wave_max(amax);
+    __syncthreads();                                  // every wave is done with its staging region
+    float* red = reinterpret_cast<float*>(smem);
+    if (lane == 0) red[wave] = amax;
+    __syncthreads();
+    unsigned* st = reinterpret_cast<unsigned*>(q8);
+    if (tid == 0) {
+      float m = red[0];
+#pragma unroll
+      for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w]);
+      atomicMax(st + phase, __float_as_uint(m));
+    }
+    if (blockIdx.x == 0 && tid == 0) {
+      st[(phase + 1) % 3] = 0u;   // cleared for the step after next's accumulation
+      q8[3] = s8;                 // dequant scale of this step's C8
+    }
+  }
+}
+
+constexpr size_t lds_bytes() {
+  const size_t stage = 2 * (size_t)(2 * 256 * 128);
+  const size_t epi = 8 * 128 * (size_t)(64 * 2 + 16);
+  return stage > epi ? stage : epi;
+}
+
+template <int EPI, bool Q8>
+void launch(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, uint16_t* P, const float* sa,
+            const float* sb, uint8_t* C8, float* q8, int phase, int M, int N, int K, hipStream_t s) {
+  constexpr size_t lds = lds_bytes();
+  static bool init = [] {
+    (void)hipFuncSetAttribute((const void*)gemm_fp8_kernel<EPI, Q8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    return true;
+  }();
+  (void)init;
+  hipLaunchKernelGGL((gemm_fp8_kernel<EPI, Q8>), dim3((M / BM) * (N / BN)), dim3(kThreads), lds, s, A, B, C, bias, P, sa, sb,
+                     C8, q8, phase, M, N, K, K, K, N);
+}
+
+// ------------------------------------------------------------------ delayed-scaling quantiser
+// y = e4m3(x / s), s = 2·amax_prev/448 from state slot (phase+2)%3 (unit when unset); this call's amax
+// into slot `phase`, slot (phase+1)%3 cleared, s stored in state[3].  One read of x instead of the
+// current-scaling path's two.
+__global__ __launch_bounds__(256) void quant_delayed_kernel(const uint16_t* __restrict__ x, uint2* __restrict__ y, size_t n8,
+                                                            float* __restrict__ q8, int phase) {
+  const float s = delayed_scale(q8, phase);
+  const float inv = 1.f / s;
+  float m = 0.f;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+    float f[8];
+    hq_unpack8(reinterpret_cast<const uint4*>(x)[i], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      m = fmaxf(m, fabsf(f[k]));
+      f[k] = fminf(fmaxf(f[k] * inv, -kFp8Max), kFp8Max);
+    }
+    uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+    uint32_t hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+    y[i] = make_uint2(lo, hi);
+  }
+  m = hq_wave_max(m);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  unsigned* st = reinterpret_cast<unsigned*>(q8);
+  if (threadIdx.x == 0) atomicMax(st + phase, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st[(phase + 1) % 3] = 0u;
+    q8[3] = s;
+  }
+}
+
+}  // namespace
+
+int hq_gemm_fp8_supported(int M, int N, int K) {
+  return (M % BM == 0 && N % BN == 0 && K % BK == 0 && K >= 2 * BK && (size_t)BM * K < (1ull << 31) &&
+          (size_t)BN * K < (1ull << 31)) ? 1 : 0;
+}
+
+void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, uint16_t* P, const float* sa,
+                 const float* sb, uint8_t* C8, float* q8, int phase, int M, int N, int K, int epi, hipStream_t s) {
+  if (epi == HQ_EPI_GELUD) {
+    if (C8) launch<HQ_EPI_GELUD, true>(A, B, C, bias, P, sa, sb, C8, q8, phase, M, N, K, s);
+    else launch<HQ_EPI_GELUD, false>(A, B, C, bias, P, sa, sb, C8, q8, phase, M, N, K, s);
+  } else {
+    launch<HQ_EPI_BIAS, false>(A, B, C, bias, P, sa, sb, C8, q8, phase, M, N, K, s);
+  }
+}
+
+void hq_fp8_quant_delayed(const uint16_t* x, uint8_t* y, size_t n, float* q8, int phase, hipStream_t s) {
+  const size_t n8 = n / 8;
+  const int grid = (int)std::min<size_t>((n8 + 255) / 256, 256 * 4);   // ≤ 1024 block-level atomics
+  hipLaunchKernelGGL(quant_delayed_kernel, dim3(grid ? grid : 1), dim3(256), 0, s, x, reinterpret_cast<uint2*>(y), n8, q8,
+                     phase);
+}

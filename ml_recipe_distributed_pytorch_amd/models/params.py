@@ -71,6 +71,7 @@ class ParamStore:
         self._t_tiles: Optional[torch.Tensor] = None
         self._t_dirty = True
         self._fp8: Dict[str, Tuple[torch.Tensor, torch.Tensor]] = {}
+        self._fp8_state: Dict[str, object] = {}
         self._fp8_dirty = True
 
     # ------------------------------------------------------------------ allocation
@@ -161,9 +162,13 @@ class ParamStore:
         if key not in self._t_off or not self._transposable():
             return None
         if self._fp8_dirty:
-            from .._native import kernels
-            k = kernels()
-            self._fp8 = {kk: tuple(k.fp8_quantize(self.view(kk))) for kk in self._t_keys}
+            # one delayed-scaling pass per weight (the amax of the previous update sets the scale; the
+            # first call seeds it by current scaling) instead of memset + amax + quantise launches
+            from .. import ops
+            if not self._fp8_state or next(iter(self._fp8_state.values())).buf.device != self.compute.device:
+                self._fp8_state = {kk: ops.Fp8DelayedState(self.compute.device) for kk in self._t_keys}
+            self._fp8 = {kk: (self._fp8_state[kk].quantize(self.view(kk)), self._fp8_state[kk].scale)
+                         for kk in self._t_keys}
             self._fp8_dirty = False
         return self._fp8[key]
 

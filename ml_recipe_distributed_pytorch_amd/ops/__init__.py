@@ -134,7 +134,67 @@ def linear_fwd_fp8(x, w8s, b):
     fp8 MFMA path (torch._scaled_mm), bf16 out.  ``w8s`` = (W fp8 [N,K], scale) from ParamStore.view_fp8."""
     x8, sx = _k().fp8_quantize(x)
     w8, sw = w8s
-    return torch._scaled_mm(x8, w8.t(), scale_a=sx, scale_b=sw, bias=b, out_dtype=torch.bfloat16)
+    return torch._scaled_mm(x8, w8.t(), scale_a=sx, scale_b=sw.reshape(()), bias=b, out_dtype=torch.bfloat16)
+
+
+class Fp8DelayedState:
+    """Per-site delayed-scaling state of an fp8 GEMM input: a device f32[4] (three rotating amax slots
+    + the scale in use, see gemm_fp8.hip) and a host step counter selecting the slots — so neither the
+    quantiser nor the GEMM ever synchronises with the host."""
+
+    def __init__(self, device):
+        self.buf = torch.zeros(4, dtype=torch.float32, device=device)
+        self.step = 0
+
+    def next_phase(self) -> int:
+        ph = self.step % 3
+        self.step += 1
+        return ph
+
+    @property
+    def scale(self):  # dequant scale of the most recent quantisation (1-element device view)
+        return self.buf[3:4]
+
+    def quantize(self, x):
+        """x (bf16) -> e4m3 in one pass under the delayed scale; the very first call seeds the
+        "previous amax" slot from x itself (current scaling) instead of falling back to a unit scale."""
+        ph = self.next_phase()
+        if self.step == 1:
+            _, s = _k().fp8_quantize(x)           # s = amax / 448 (device scalar)
+            self.buf[(ph + 2) % 3] = s * 448.0    # slots hold float bits; amax >= 0 orders as uint
+        return _k().fp8_quant_delayed(x, self.buf, ph)
+
+
+def linear_fwd_fp8_delayed(x, w8s, b, state: Fp8DelayedState):
+    """y = x·Wᵀ + b with x quantised in ONE pass under delayed scaling (scale from the previous
+    step's amax, this step's amax recorded on device) and hipBLASLt's fp8 MFMA GEMM."""
+    x8 = state.quantize(x)
+    w8, sw = w8s
+    return torch._scaled_mm(x8, w8.t(), scale_a=state.scale.reshape(()), scale_b=sw.reshape(()), bias=b,
+                            out_dtype=torch.bfloat16)
+
+
+def linear_fwd_fp8_prequant(x8, x_state: Fp8DelayedState, w8s, b):
+    """y = x8·Wᵀ·s + b for an input already in e4m3 (written by the producer under ``x_state``)."""
+    w8, sw = w8s
+    return torch._scaled_mm(x8, w8.t(), scale_a=x_state.scale.reshape(()), scale_b=sw.reshape(()), bias=b,
+                            out_dtype=torch.bfloat16)
+
+
+def linear_gelu_fwd_fp8(x, w8s, b32, in_state: Fp8DelayedState, out_state: Fp8DelayedState):
+    """FFN1 in fp8 on the own block-scaled MFMA kernel (gemm_fp8.hip): returns (gelu'(pre), act, act8)
+    — act in bf16 (saved for the FFN2 weight gradient) and in e4m3 under ``out_state``'s delayed scale
+    for the FFN2 fp8 GEMM; None when the shape does not tile (caller falls back)."""
+    M, K, N = x.shape[0], x.shape[1], w8s[0].shape[0]
+    if not _k().gemm_fp8_supported(M, N, K):
+        return None
+    x8 = in_state.quantize(x)
+    w8, sw = w8s
+    gd = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    act8 = torch.empty(M, N, dtype=torch.float8_e4m3fn, device=x.device)
+    act = _k().gemm_fp8(x8, w8, _EPI_GELUD, b32, in_state.scale, sw.reshape(1).float(), pre=gd, out8=act8,
+                        state=out_state.buf, phase=out_state.next_phase())
+    return gd, act, act8
 
 
 def linear_gelu_fwd(x, w, b, b32=None):
