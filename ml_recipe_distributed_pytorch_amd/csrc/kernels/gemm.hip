@@ -465,35 +465,51 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
   // local col lc = nh·32 + j·16 + ..; then row-coalesced 16-B pieces -> epilogue math -> global.
   constexpr int WN = 64;
   constexpr int RS = WN * 2 + 16;
+  constexpr int SEGS = WN / 8;                  // 8 pieces of 16 B per local row
+  constexpr int ROWS_PER_IT = 64 / SEGS;        // 8
+  constexpr int NIT = 128 / ROWS_PER_IT;        // 16 row-coalesced pieces per lane
+  constexpr bool kReadsAux = EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID;
+  const int seg = lane % SEGS, rsub = lane / SEGS;
+  const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;   // 4 pieces per 32-col chunk
+  auto grow_of = [&](int it) {
+    const int lr = it * ROWS_PER_IT + rsub;
+    return m0 + (lr >> 6) * 128 + wm * 64 + (lr & 63);
+  };
   char* wreg = smem + wave * (128 * RS);
+  constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD;
 #pragma unroll
   for (int J = 0; J < 4; ++J) {
     const int nh = J >> 1, j = J & 1;
     const int lc = nh * 32 + j * 16 + fq * 4;
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD)
-      bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
+    if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
 #pragma unroll
     for (int I = 0; I < 8; ++I) {
-      float v[4] = {acc[I][J][0] + bv.x, acc[I][J][1] + bv.y, acc[I][J][2] + bv.z, acc[I][J][3] + bv.w};
+      float v[4] = {acc[I][J][0], acc[I][J][1], acc[I][J][2], acc[I][J][3]};
+      if constexpr (kBias) { v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w; }  // no "+0" canonicalise adds
       *reinterpret_cast<uint2*>(wreg + (I * 16 + fr) * RS + lc * 2) = hq_pack4(v);
     }
   }
-  constexpr int SEGS = WN / 8;                  // 8 pieces of 16 B per local row
-  constexpr int ROWS_PER_IT = 64 / SEGS;        // 8
-  const int seg = lane % SEGS, rsub = lane / SEGS;
-  const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;   // 4 pieces per 32-col chunk
+  // The epilogue's second operand (P = stored pre / gelu', R = residual) comes from HBM: issue all 16
+  // pieces of this lane at once so ONE load latency is exposed instead of one per few pieces inside the
+  // store loop (64 VGPRs; the accumulators are dead now).  Issued after the staging writes: hipcc
+  // drains vmcnt(0) before the first LDS write (the main loop's LDS-DMA shares the counter).
+  uint4 aux[kReadsAux ? NIT : 1];
+  if constexpr (kReadsAux) {
+    const uint16_t* src = EPI == HQ_EPI_RESID ? R : P;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) aux[it] = *reinterpret_cast<const uint4*>(src + (size_t)grow_of(it) * ldc + gcol);
+  }
   float csum[8];
   if constexpr (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[e] = 0.f;
   }
-#pragma unroll 4
-  for (int it = 0; it < 128 / ROWS_PER_IT; ++it) {
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
     const int lr = it * ROWS_PER_IT + rsub;
-    const int grow = m0 + (lr >> 6) * 128 + wm * 64 + (lr & 63);
     uint4 piece = *reinterpret_cast<const uint4*>(wreg + lr * RS + seg * 16);
-    const size_t goff = (size_t)grow * ldc + gcol;
+    const size_t goff = (size_t)grow_of(it) * ldc + gcol;
     if constexpr (EPI == HQ_EPI_GELU) {
       *reinterpret_cast<uint4*>(P + goff) = piece;
       float x[8];
@@ -516,21 +532,21 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
     } else if constexpr (EPI == HQ_EPI_DMUL) {
       float d[8], gd[8];
       hq_unpack8(piece, d);
-      hq_unpack8(*reinterpret_cast<const uint4*>(P + goff), gd);
+      hq_unpack8(aux[it], gd);
 #pragma unroll
       for (int e = 0; e < 8; ++e) { d[e] *= gd[e]; csum[e] += d[e]; }
       piece = hq_pack8(d);
     } else if constexpr (EPI == HQ_EPI_DGELU) {
       float d[8], pr[8];
       hq_unpack8(piece, d);
-      hq_unpack8(*reinterpret_cast<const uint4*>(P + goff), pr);
+      hq_unpack8(aux[it], pr);
 #pragma unroll
       for (int e = 0; e < 8; ++e) { d[e] *= gelu_grad(pr[e]); csum[e] += d[e]; }
       piece = hq_pack8(d);
     } else if constexpr (EPI == HQ_EPI_RESID) {
       float d[8], rr[8];
       hq_unpack8(piece, d);
-      hq_unpack8(*reinterpret_cast<const uint4*>(R + goff), rr);
+      hq_unpack8(aux[it], rr);
 #pragma unroll
       for (int e = 0; e < 8; ++e) d[e] += rr[e];
       piece = hq_pack8(d);

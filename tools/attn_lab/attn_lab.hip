@@ -11,6 +11,16 @@ namespace {
 
 typedef float f2_t __attribute__((ext_vector_type(2)));
 
+// single-matrix prologue loader (the production kernels now use load_heads2 for K and V together)
+template <int NT>
+__device__ __forceinline__ void load_head(uint16_t* dst, const uint16_t* src, size_t ld, int L, int Lp) {
+  for (int t = threadIdx.x; t < Lp * 8; t += NT) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if ((t >> 3) < L) v = *reinterpret_cast<const uint4*>(src + (size_t)(t >> 3) * ld + (t & 7) * 8);
+    *reinterpret_cast<uint4*>(dst + lds_off(t >> 3, (t & 7) * 8)) = v;
+  }
+}
+
 // V1: prologue + epilogue only (what the loads cost with no compute).
 template <int NWB>
 __global__ __launch_bounds__(NWB * 64) void fwd_prologue_only(const uint16_t* __restrict__ qkv,
