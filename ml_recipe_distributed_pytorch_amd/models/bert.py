@@ -171,8 +171,10 @@ class _LayerFn(torch.autograd.Function):
         W8 = lambda k: st.view_fp8(p + k + ".weight")  # noqa: E731  (e4m3 weight + dequant scale)
         Bb = lambda k: st.view(p + k + ".bias")  # noqa: E731
 
+        kinds = {"qkv": "qkv", "attention.output.dense": "out", "output.dense": "ffn2"}
+
         def proj(inp, name):  # bf16 forward projection
-            return ops.linear_fwd(inp, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"))
+            return ops.linear_fwd(inp, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), kinds[name])
 
         # --precision fp8 (BASELINE config #5): QKV and FFN2 on hipBLASLt's fp8 GEMM with one-pass
         # delayed-scaling quantisation of their inputs, FFN1 on the own block-scaled MFMA kernel whose

@@ -94,6 +94,10 @@ def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale
 #   HQ_GEMM=mfma: every supported shape;  HQ_GEMM=blas: none.
 _EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID, _EPI_GELUD, _EPI_DMUL = range(7)
 _GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
+# Plain forward projections (bias epilogue) that take the MFMA kernel in auto mode, by name: qkv | out | ffn2.
+# In the full b256 step hipBLASLt's QKV pick runs 381 µs vs 316 µs standalone while the MFMA kernel holds
+# ~337 µs (profiles/s3_*), so QKV defaults to the MFMA kernel.
+FWD_MFMA = {k for k in os.environ.get("HQ_FWD_MFMA", "qkv").split(",") if k}
 GELU_DERIV = os.environ.get("HQ_GELU_DERIV", "1") == "1"   # FFN1 stores gelu'(pre) (linear_gelu_fwd_d)
 _CUS = 256
 
@@ -117,13 +121,14 @@ def _mfma(M: int, N: int, K: int, kind: str = "plain") -> bool:
     fill = tiles / (-(-tiles // _CUS) * _CUS)
     # plain dgrads (dy·W through the Wᵀ copy): v2 is 1.04x hipBLASLt's NT kernel on long K and beats the
     # NN kernel torch.mm(dy, W) dispatches at K = 768 (123 vs 136 µs at b256, profiles/s2_*)
-    return fill >= 0.85 and kind in ("dgelu", "gelu", "resid", "dgrad")
+    return fill >= 0.85 and (kind in ("dgelu", "gelu", "resid", "dgrad") or kind in FWD_MFMA)
 
 
-def linear_fwd(x, w, b, b32=None):
-    """y = x·Wᵀ + b.  GPU: hipBLASLt (bias epilogue) or the MFMA NT kernel (fp32 ``b32`` bias)."""
+def linear_fwd(x, w, b, b32=None, kind: str = "plain"):
+    """y = x·Wᵀ + b.  GPU: hipBLASLt (bias epilogue) or the MFMA NT kernel (fp32 ``b32`` bias); ``kind``
+    names the projection (qkv | out | ffn2) for the FWD_MFMA policy."""
     if x.is_cuda:
-        if b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1]):
+        if b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1], kind):
             return _k().gemm_nt(x, w, _EPI_BIAS, bias=b32)
         return torch.addmm(b, x, w.t()) if b is not None else torch.mm(x, w.t())
     return ref.linear_fwd(x, w, b)

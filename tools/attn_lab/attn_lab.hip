@@ -738,6 +738,20 @@ int main(int argc, char** argv) {
   };
 
 
+  {
+    auto k1 = fwd_prologue_only<12>;
+    HQ_CHECK(hipFuncSetAttribute((const void*)k1, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    report("prologue+epilogue only", time_it([&] {
+             hipLaunchKernelGGL(k1, dim3(B * nh, 1), dim3(768), lds, 0, qkv, kb, ctx1, lse1, L, nh, scale * LOG2E);
+           }));
+    auto k3 = fwd_v3_prologue<12, 12>;
+    HQ_CHECK(hipFuncSetAttribute((const void*)k3, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    report("v3 (DMA) prologue only", time_it([&] {
+             hipLaunchKernelGGL(k3, dim3(B * nh, 1), dim3(768), lds, 0, qkv, kb, ctx1, lse1, L, nh, scale * LOG2E);
+           }));
+  }
+  run_v4(fwd_v4<12, 12, 12>, "persistent");
+
   report("fwd prod p=0 (again)", time_it([&] { hq_attn_fwd(qkv, kb, ctx0, lse0, nullptr, B, L, nh, D, 0.f, 1, 1, scale, 0); }));
   report("fwd prod p=0.1", time_it([&] {
            static uint16_t* bits = nullptr;
