@@ -60,7 +60,7 @@ std::vector<Tensor> embed_fwd(Tensor ids, Tensor pids, Tensor tids, Tensor ww, T
 
 void embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tensor wp, Tensor wt, Tensor gamma, Tensor mean,
                Tensor rstd, double p, int64_t seed, int64_t opid, Tensor g_word, Tensor g_pos, Tensor g_type, Tensor g_gamma,
-               Tensor g_beta, bool accumulate, int64_t pad_word, int64_t pad_pos) {
+               Tensor g_beta, bool accumulate, int64_t pad_word, int64_t pad_pos, int64_t seq_len) {
   check(dy, BF16, "dy"); check(ids, I64, "ids"); check(pids, I64, "pos_ids"); check(tids, I64, "type_ids");
   check(ww, BF16, "w_word"); check(wp, BF16, "w_pos"); check(wt, BF16, "w_type"); check(gamma, F32, "gamma");
   check(mean, F32, "mean"); check(rstd, F32, "rstd");
@@ -77,7 +77,7 @@ void embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tenso
     hipMemsetAsync(g_pos.data_ptr(), 0, g_pos.numel() * 4, s);
     if (n_types > 2) hipMemsetAsync(g_type.data_ptr(), 0, g_type.numel() * 4, s);
   }
-  const int nb = hq_ln_bwd_partials((int)T);
+  const int nb = hq_embed_bwd_partials((int)T, (int)seq_len);
   auto part = at::empty({nb, 4 * H}, gamma.options());
   float* t0 = ptr<float>(g_type);
   HqOuts o = outs4(ptr<float>(g_gamma), ptr<float>(g_beta), n_types <= 2 ? t0 : nullptr,
@@ -85,7 +85,7 @@ void embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tenso
   hq_embed_bwd(ptr<uint16_t>(dy), ptr<int64_t>(ids), ptr<int64_t>(pids), ptr<int64_t>(tids), ptr<uint16_t>(ww),
                ptr<uint16_t>(wp), ptr<uint16_t>(wt), ptr<float>(gamma), ptr<float>(mean), ptr<float>(rstd),
                ptr<float>(g_word), ptr<float>(g_pos), t0, ptr<float>(part), o, (int)T, (int)H, n_types, (int)pad_word,
-               (int)pad_pos, (float)p, u32(seed), u32(opid), accumulate, (int)ww.size(0), (int)wp.size(0), s);
+               (int)pad_pos, (float)p, u32(seed), u32(opid), accumulate, (int)ww.size(0), (int)wp.size(0), (int)seq_len, s);
 }
 
 // ------------------------------------------------------------------ residual + dropout + LayerNorm
@@ -436,7 +436,10 @@ void cast_f32_bf16(Tensor src, Tensor dst, double scale) {
 PYBIND11_MODULE(_hq_kernels, m) {
   m.doc() = "gfx950 HIP kernels + RCCL reducer for ml_recipe_distributed_pytorch_amd";
   m.def("embed_fwd", &embed_fwd);
-  m.def("embed_bwd", &embed_bwd);
+  m.def("embed_bwd", &embed_bwd, py::arg("dy"), py::arg("ids"), py::arg("pids"), py::arg("tids"), py::arg("ww"),
+        py::arg("wp"), py::arg("wt"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"), py::arg("p"), py::arg("seed"),
+        py::arg("opid"), py::arg("g_word"), py::arg("g_pos"), py::arg("g_type"), py::arg("g_gamma"), py::arg("g_beta"),
+        py::arg("accumulate"), py::arg("pad_word"), py::arg("pad_pos"), py::arg("seq_len") = 0);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
   m.def("gelu_fwd", &gelu_fwd);

@@ -26,7 +26,9 @@ void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, c
                   const uint16_t* wp, const uint16_t* wt, const float* gamma, const float* mean, const float* rstd,
                   float* g_word, float* g_pos, float* g_type, float* part, HqOuts outs, int T, int H, int n_types,
                   int pad_word, int pad_pos, float p, uint32_t seed, uint32_t opid, bool accumulate, int V, int P,
-                  hipStream_t s);
+                  int L, hipStream_t s);
+// partial-sum rows embed_bwd needs for T tokens laid out as [T / L][L] (L <= 0: one sequence)
+int hq_embed_bwd_partials(int T, int L);
 void hq_gelu_fwd(const uint16_t* pre, uint16_t* out, size_t n, hipStream_t s);
 void hq_gelu_bwd(const uint16_t* dout, const uint16_t* pre, uint16_t* dpre, float* part, HqOuts outs, int T, int N,
                  bool accumulate, hipStream_t s);

@@ -3,8 +3,9 @@
 //   ln_fwd   : z = dropout(a) + resid (rounded to bf16, as HF under autocast) ; y = LN(z)
 //   ln_bwd   : dz = LN_bwd(dy [+ dy2]) ; da = dropout_bwd(dz) ; per-block partial Σ(g·x̂), Σg, Σda
 //   embed_fwd: y = dropout(LN(word[id] + pos[pid] + type[tid]))
-//   embed_bwd: recompute x̂, LN_bwd, f32 atomics into word/pos grads (256-B contiguous per wave
-//              instruction via an LDS transpose), type/γ/β grads through deterministic partials
+//   embed_bwd: recompute x̂, LN_bwd, f32 atomics into the word grads (256-B contiguous per wave
+//              instruction via an LDS transpose), position grads summed per wave over the batch
+//              (position-major walk) then one atomic flush, type/γ/β grads through deterministic partials
 //   gelu_fwd / gelu_bwd(+bias grad partials), bias_grad partials, colsum finalize
 //
 // Layout: one wave per row; lane owns 4 consecutive columns per 256-column chunk (8-byte bf16
@@ -91,7 +92,7 @@ __device__ __forceinline__ void block_partials(float (&acc)[NQ][NCH][4], float* 
     __syncthreads();
     for (int col = threadIdx.x; col < H; col += 256) {
       float s = lds[col] + lds[H + col] + lds[2 * H + col] + lds[3 * H + col];
-      part[((size_t)blockIdx.x * NQ + q) * H + col] = s;
+      part[(((size_t)blockIdx.y * gridDim.x + blockIdx.x) * NQ + q) * H + col] = s;  // linear block id (2-D grids)
     }
     __syncthreads();
   }
@@ -336,6 +337,43 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
 }
 
 // part layout per block: [gamma | beta | type0 | type1] × H
+//
+// Position-major traversal: wave w of block (x, y) owns sequence position l = x·4 + w and walks the
+// kEmbNB batch rows b = y·kEmbNB … (row = b·L + l).  With the default position ids (pid = l for every
+// b) the wave sums the position gradient in registers and flushes it with ONE set of atomics per wave
+// (a flush also runs whenever the pid changes, so arbitrary position ids stay exact) — the old
+// row-major walk issued 768 position atomics per token, all 256 tokens of a position contending on
+// the same 3 KB.  The next row's dy / embedding rows / statistics are loaded while the current row
+// is reduced (one dependent HBM round trip per row otherwise).
+constexpr int kEmbNB = 16;
+
+template <int NCH>
+struct EmbRow {
+  int64_t id, pid, tid;
+  float mu, rs;
+  uint2 w[NCH], p[NCH], t[NCH], d[NCH];
+};
+
+template <int NCH>
+__device__ __forceinline__ void emb_load(EmbRow<NCH>& r, size_t row, const uint16_t* __restrict__ dy,
+                                         const int64_t* __restrict__ ids, const int64_t* __restrict__ pids,
+                                         const int64_t* __restrict__ tids, const uint16_t* __restrict__ ww,
+                                         const uint16_t* __restrict__ wp, const uint16_t* __restrict__ wt,
+                                         const float* __restrict__ mean, const float* __restrict__ rstd, int H, int lane) {
+  r.id = ids[row]; r.pid = pids[row]; r.tid = tids[row];
+  r.mu = mean[row]; r.rs = rstd[row];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    if (col < H) {
+      r.w[c] = *reinterpret_cast<const uint2*>(ww + (size_t)r.id * H + col);
+      r.p[c] = *reinterpret_cast<const uint2*>(wp + (size_t)r.pid * H + col);
+      r.t[c] = *reinterpret_cast<const uint2*>(wt + (size_t)r.tid * H + col);
+      r.d[c] = *reinterpret_cast<const uint2*>(dy + row * H + col);
+    }
+  }
+}
+
 template <int NCH>
 __global__ __launch_bounds__(256) void embed_bwd_kernel(
     const uint16_t* __restrict__ dy, const int64_t* __restrict__ ids, const int64_t* __restrict__ pids,
@@ -343,9 +381,9 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
     const uint16_t* __restrict__ wt, const float* __restrict__ gamma, const float* __restrict__ mean,
     const float* __restrict__ rstd, float* __restrict__ g_word, float* __restrict__ g_pos, float* __restrict__ g_type,
     float* __restrict__ part, int T, int H, int n_types, int pad_word, int pad_pos, uint32_t key, uint32_t thr,
-    float kscale, int V, int P) {
+    float kscale, int V, int P, int B, int L) {
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][H] reduction scratch, reused as dx rows
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   float acc[4][NCH][4];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
@@ -353,22 +391,44 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[q][c][i] = 0.f;
-  float gam[NCH][4];
+  float gam[NCH][4], pacc[NCH][4];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = c * 256 + lane * 4;
     float4 g = col < H ? *reinterpret_cast<const float4*>(gamma + col) : make_float4(0.f, 0.f, 0.f, 0.f);
     gam[c][0] = g.x; gam[c][1] = g.y; gam[c][2] = g.z; gam[c][3] = g.w;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pacc[c][i] = 0.f;
   }
+  int pcur = -1;
+  auto flush_pos = [&]() {
+    if (pcur >= 0 && pcur != pad_pos) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int col = c * 256 + lane * 4;
+        if (col < H)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) atomicAdd(g_pos + (size_t)pcur * H + col + i, pacc[c][i]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pacc[c][i] = 0.f;
+  };
   float* myrow = lds + wave * H;
-  const int row0 = blockIdx.x * kWaves * kRowsPerWave;
-  for (int r = 0; r < kRowsPerWave; ++r) {
-    const int row = row0 + r * kWaves + wave;
-    if (row >= T) break;
-    const int64_t id = ids[row], pid = pids[row], tid = tids[row];
+  const int l = blockIdx.x * kWaves + wave;
+  const int b0 = blockIdx.y * kEmbNB, b1 = min(B, b0 + kEmbNB);
+  EmbRow<NCH> cur, nxt;
+  if (l < L && b0 < b1) emb_load<NCH>(nxt, (size_t)b0 * L + l, dy, ids, pids, tids, ww, wp, wt, mean, rstd, H, lane);
+  for (int b = b0; l < L && b < b1; ++b) {
+    const size_t row = (size_t)b * L + l;
+    cur = nxt;
+    if (b + 1 < b1) emb_load<NCH>(nxt, row + L, dy, ids, pids, tids, ww, wp, wt, mean, rstd, H, lane);
+    const int64_t id = cur.id, pid = cur.pid, tid = cur.tid;
     HQ_DASSERT(id >= 0 && id < V && pid >= 0 && pid < P && tid >= 0 && tid < n_types);
-    const size_t base = (size_t)row * H;
-    const float mu = mean[row], rs = rstd[row];
+    const size_t base = row * H;
+    const float mu = cur.mu, rs = cur.rs;
     float g[NCH][4], xh[NCH][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -376,10 +436,10 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
       const int col = c * 256 + lane * 4;
       if (col < H) {
         float f1[4], f2[4], f3[4], m[4] = {1.f, 1.f, 1.f, 1.f};
-        hq_unpack4(*reinterpret_cast<const uint2*>(ww + (size_t)id * H + col), f1);
-        hq_unpack4(*reinterpret_cast<const uint2*>(wp + (size_t)pid * H + col), f2);
-        hq_unpack4(*reinterpret_cast<const uint2*>(wt + (size_t)tid * H + col), f3);
-        hq_unpack4(*reinterpret_cast<const uint2*>(dy + base + col), g[c]);
+        hq_unpack4(cur.w[c], f1);
+        hq_unpack4(cur.p[c], f2);
+        hq_unpack4(cur.t[c], f3);
+        hq_unpack4(cur.d[c], g[c]);
         if (thr) hq_keep4((uint32_t)(base + col), key, thr, kscale, m);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -398,30 +458,41 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
     }
     s1 = hq_wave_sum(s1) / H;
     s2 = hq_wave_sum(s2) / H;
+    if ((int)pid != pcur) {  // wave-uniform: the running position sum belongs to another position
+      flush_pos();
+      pcur = (int)pid;
+    }
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = c * 256 + lane * 4;
       if (col < H) {
         float dx[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) dx[i] = rs * (g[c][i] * gam[c][i] - s1 - xh[c][i] * s2);
-        if (n_types <= 2) {
+        for (int i = 0; i < 4; ++i) {
+          dx[i] = rs * (g[c][i] * gam[c][i] - s1 - xh[c][i] * s2);
+          pacc[c][i] += dx[i];
+        }
+        if (n_types <= 2) {  // static indices only: acc[2 + (tid & 1)] put the whole array in scratch memory
+          const bool t1 = (tid & 1) != 0;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc[2 + (tid & 1)][c][i] += dx[i];
+          for (int i = 0; i < 4; ++i) {
+            acc[2][c][i] += t1 ? 0.f : dx[i];
+            acc[3][c][i] += t1 ? dx[i] : 0.f;
+          }
         }
         *reinterpret_cast<float4*>(myrow + col) = make_float4(dx[0], dx[1], dx[2], dx[3]);
       }
     }
     // wave-private LDS row, re-read lane-contiguous so each atomic wave-instruction is 256 B contiguous
     // (LDS ops of one wave complete in issue order; the aliasing stores keep the compiler order)
-    const bool do_word = (int)id != pad_word, do_pos = (int)pid != pad_pos;
+    const bool do_word = (int)id != pad_word;
     for (int col = lane; col < H; col += 64) {
       const float d = myrow[col];
       if (do_word) atomicAdd(g_word + (size_t)id * H + col, d);
-      if (do_pos) atomicAdd(g_pos + (size_t)pid * H + col, d);
       if (n_types > 2) atomicAdd(g_type + (size_t)tid * H + col, d);
     }
   }
+  flush_pos();
   __syncthreads();
   block_partials<NCH, 4>(acc, lds, part, H);
 }
@@ -577,6 +648,10 @@ void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, con
 }
 
 int hq_ln_bwd_partials(int T) { return (T + kWaves * kRowsPerWave - 1) / (kWaves * kRowsPerWave); }
+int hq_embed_bwd_partials(int T, int L) {
+  if (L <= 0 || T % L) L = T;
+  return ((L + kWaves - 1) / kWaves) * ((T / L + kEmbNB - 1) / kEmbNB);
+}
 
 void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const float* gamma, const float* mean,
                const float* rstd, uint16_t* dz, uint16_t* da, float* part, HqOuts outs, int T, int H, float p,
@@ -608,15 +683,18 @@ void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, c
                   const uint16_t* wp, const uint16_t* wt, const float* gamma, const float* mean, const float* rstd,
                   float* g_word, float* g_pos, float* g_type, float* part, HqOuts outs, int T, int H,
                   int n_types, int pad_word, int pad_pos, float p, uint32_t seed, uint32_t opid, bool accumulate,
-                  int V, int P, hipStream_t s) {
+                  int V, int P, int L, hipStream_t s) {
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const uint32_t key = hq_op_key(seed, opid);
   const float ks = hq_keep_scale(thr);
-  const int nb = hq_ln_bwd_partials(T);
+  if (L <= 0 || T % L) L = T;  // rows are b·L + l; any other layout is one "sequence" of T positions
+  const int B = T / L;
+  const dim3 grid((L + kWaves - 1) / kWaves, (B + kEmbNB - 1) / kEmbNB);
+  const int nb = hq_embed_bwd_partials(T, L);
   dispatch_nch(H, [&](auto nch) {
-    hipLaunchKernelGGL(embed_bwd_kernel<decltype(nch)::value>, dim3(nb), dim3(256), 4 * H * sizeof(float), s, dy, ids,
+    hipLaunchKernelGGL(embed_bwd_kernel<decltype(nch)::value>, grid, dim3(256), 4 * H * sizeof(float), s, dy, ids,
                        pids, tids, ww, wp, wt, gamma, mean, rstd, g_word, g_pos, g_type, part, T, H, n_types, pad_word,
-                       pad_pos, key, thr, ks, V, P);
+                       pad_pos, key, thr, ks, V, P, B, L);
   });
   // outs: gamma, beta, type0, type1 (type rows only when n_types <= 2)
   colsum(part, nb, 4 * H, outs, H, accumulate, s);

@@ -149,7 +149,7 @@ class _EmbeddingFn(torch.autograd.Function):
                           st.view(e + "word_embeddings.weight", "grad"), st.view(e + "position_embeddings.weight", "grad"),
                           st.view(e + "token_type_embeddings.weight", "grad"), st.view(e + "LayerNorm.weight", "grad"),
                           st.view(e + "LayerNorm.bias", "grad"), acc, m.config.pad_token_id,
-                          m.config.pad_token_id if m.config.family == "roberta" else -1)
+                          m.config.pad_token_id if m.config.family == "roberta" else -1, info.L)
             m._group_ready("embeddings")
         return None, None, None, None, None
 

@@ -29,11 +29,13 @@ def embed_fwd(ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, beta, eps, p
 
 
 def embed_bwd(dy, ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, mean, rstd, p, seed, opid,
-              g_word, g_pos, g_type, g_gamma, g_beta, accumulate, pad_word=-1, pad_pos=-1):
+              g_word, g_pos, g_type, g_gamma, g_beta, accumulate, pad_word=-1, pad_pos=-1, seq_len=0):
+    """``seq_len`` = L of the [B, L] token layout (0: unknown) — lets the kernel walk one position across
+    the batch and sum the position-embedding gradient in registers."""
     if dy.is_cuda:
         return _k().embed_bwd(dy, ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, mean, rstd, float(p),
                               int(seed), int(opid), g_word, g_pos, g_type, g_gamma, g_beta, bool(accumulate),
-                              int(pad_word), int(pad_pos))
+                              int(pad_word), int(pad_pos), int(seq_len))
     return ref.embed_bwd(dy, ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, mean, rstd, p, seed, opid,
                          g_word, g_pos, g_type, g_gamma, g_beta, accumulate, pad_word, pad_pos)
 

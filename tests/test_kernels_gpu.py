@@ -54,7 +54,11 @@ def test_ln_fwd_bwd(cuda, H, p):
 
 @pytest.mark.parametrize("H,ntypes", [(768, 2), (128, 1)])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_embedding(cuda, H, ntypes, p):
+@pytest.mark.parametrize("layout", ["flat", "seq", "seq_randpos"])
+def test_embedding(cuda, H, ntypes, p, layout):
+    """embed fwd/bwd vs the fp32 oracle.  ``seq`` passes L so the backward walks positions across the
+    batch (register-summed position grads); ``seq_randpos`` gives every token a random position id so
+    the per-pid flush path is exercised; ``flat`` = unknown layout (seq_len 0)."""
     k = _native.kernels()
     torch.manual_seed(1)
     V, P, B, L = 1000, 64, 4, 50
@@ -63,7 +67,7 @@ def test_embedding(cuda, H, ntypes, p):
     gamma, beta = torch.randn(H) * 0.3 + 1, torch.randn(H) * 0.1
     ids = torch.randint(0, V, (T,))
     ids[::7] = 0
-    pids = torch.arange(L).repeat(B)
+    pids = torch.randint(0, P, (T,)) if layout == "seq_randpos" else torch.arange(L).repeat(B)
     tids = torch.randint(0, ntypes, (T,))
     dev = lambda t: t.to(cuda)  # noqa: E731
     y, m, rs = k.embed_fwd(dev(ids), dev(pids), dev(tids), dev(ww), dev(wp), dev(wt), dev(gamma), dev(beta), 1e-12, p, 99, 0)
@@ -75,7 +79,7 @@ def test_embedding(cuda, H, ntypes, p):
     gg, gb = torch.zeros(H), torch.zeros(H)
     out = [dev(t) for t in (gw, gp, gt, gg, gb)]
     k.embed_bwd(dev(dy), dev(ids), dev(pids), dev(tids), dev(ww), dev(wp), dev(wt), dev(gamma), m, rs, p, 99, 0, *out,
-                False, 0, -1)
+                False, 0, -1, 0 if layout == "flat" else L)
     ref.embed_bwd(dy, ids, pids, tids, ww, wp, wt, gamma, m.cpu(), rs.cpu(), p, 99, 0, gw, gp, gt, gg, gb, False, 0, -1)
     for a, b, n in zip(out, (gw, gp, gt, gg, gb), ["word", "pos", "type", "gamma", "beta"]):
         _close(a, b, 5e-2, 2e-2, n)

@@ -38,9 +38,10 @@ def main():
     gw, gp, gt = torch.zeros(V, H, device=dev), torch.zeros(P, H, device=dev), torch.zeros(2, H, device=dev)
     gg, gb = torch.zeros(H, device=dev), torch.zeros(H, device=dev)
     for name, i, p, pw, pp in (("full", ids, pids, 0, -1), ("no_pos_atomics", ids, torch.full_like(pids, 511), 0, 511),
-                              ("no_word_atomics", torch.zeros_like(ids), pids, 0, -1)):
+                              ("no_word_atomics", torch.zeros_like(ids), pids, 0, -1),
+                              ("no_atomics", torch.zeros_like(ids), torch.full_like(pids, 511), 0, 511)):
         us = timeit(lambda: k.embed_bwd(dy, i, p, tids, ww, wp, wt, g, mean, rstd, 0.1, 1, 0, gw, gp, gt, gg, gb,
-                                        False, pw, pp))
+                                        False, pw, pp, L))
         print(f"embed_bwd {name:16s} {us:8.1f} us")
     print(f"embed_fwd {timeit(lambda: k.embed_fwd(ids, pids, tids, ww, wp, wt, g, b, 1e-12, 0.1, 1, 0)):8.1f} us")
 
