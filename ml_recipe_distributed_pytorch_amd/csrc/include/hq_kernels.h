@@ -69,7 +69,8 @@ void hq_cast_bf16_f32(const uint16_t* src, float* dst, int64_t n, float scale, h
 enum { HQ_EPI_NONE = 0, HQ_EPI_BIAS = 1, HQ_EPI_GELU = 2, HQ_EPI_DGELU = 3, HQ_EPI_RESID = 4, HQ_EPI_GELUD = 5, HQ_EPI_DMUL = 6 };
 // returns the block N-width the kernel will use for this shape (256 / 128), 0 = unsupported
 int hq_gemm_nt_supported(int M, int N, int K);
-// 0 = auto (v2 deep-pipeline kernel where supported), 1 = v1 kernel only (A/B and fallback)
+// 0 = auto (v3 persistent kernel for K <= 2304, v2 deep-pipeline kernel otherwise), 1 = v1 only,
+// 2 = v2 only, 3 = v3 wherever supported (A/B and fallback)
 void hq_gemm_set_variant(int v);
 // C[M,N] = A[M,K]·B[N,K]^T (+epilogue); P = GELU pre-activation (out for EPI_GELU, in for EPI_DGELU)
 // or its derivative gelu'(pre) (out for EPI_GELUD, in for EPI_DMUL);

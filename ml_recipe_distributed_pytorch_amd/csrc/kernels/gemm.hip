@@ -568,7 +568,318 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
   }
 }
 
-int g_gemm_variant = 0;   // 0 = auto (v2 where supported), 1 = force v1
+// ================================================================================ v3: persistent
+// v2's per-tile fixed cost (WG launch, the prologue's first HBM round trip, the epilogue's drain) is
+// ~11k cycles per 256² tile — a third of a K = 768 tile (profiles/s3_prof: the same 464 GFLOP run
+// 1.03 PF/s as 4608 K=768 tiles, 1.20 PF/s as 1152 K=3072 tiles).  v3 keeps ONE workgroup per CU
+// walking tiles (tile = id, id + grid, …) and runs the LDS-DMA pipeline straight across the tile seam:
+// K-tile 0 of the next tile is staged during the last two K-tiles of this one (exactly the loads the
+// steady state would issue for t+1 / t+2), so its data lands under the last MFMA phases and the
+// epilogue.  Only the next tile's K-tile-1 first halves (A0, B0), which v2 would stage into the buffer
+// the epilogue now borrows, are held back until the epilogue is done.
+//
+// Epilogue LDS: the buffer of this tile's last K-tile (free once every wave passed its last MFMA
+// phase) holds seven waves' 64-row staging regions, wave 7's lies past both buffers; the 128 local
+// rows of each wave are staged in two 64-row rounds.  The epilogue's global loads/stores (E per lane,
+// EPI-dependent, all issued between the next tile's K-tile-0 halves and its K-tile-1 halves) are
+// counted into the first K-tile's vmcnt waits.  Raw barriers only (a __syncthreads fence would drain
+// the in-flight DMA).
+template <int EPI>
+struct NT3Epi {
+  static constexpr int kStores = 16 * (1 + (EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD ? 1 : 0));
+  static constexpr int kLoads = (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID) ? 16 : 0;
+  static constexpr int E = kStores + kLoads;   // vm ops per lane (the part store of waves 0-3 is not counted: a
+};                                             // smaller count only waits longer)
+
+template <int EPI>
+__global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                                                               uint16_t* __restrict__ C, const float* __restrict__ bias,
+                                                               uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
+                                                               float* __restrict__ part, int M, int N, int K, int lda,
+                                                               int ldb, int ldc) {
+  constexpr int BN = 256;
+  constexpr int PANEL = 256 * 128;
+  constexpr int STAGE = 2 * PANEL;
+  constexpr int WN = 64;
+  constexpr int RS = WN * 2 + 16;
+  constexpr int REGION = 64 * RS;            // one wave's 64-row staging round (9216 B)
+  constexpr int SPARE = 2 * STAGE;           // past both stage buffers: wave 7's region, then csum scratch
+  constexpr int E = NT3Epi<EPI>::E;
+  static_assert(7 * REGION <= STAGE && SPARE + REGION + 2 * BN * 4 <= 160 * 1024, "LDS plan");
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tiles_n = N / BN, ntiles = (M / BM) * tiles_n;
+  const int nt = K / BK;
+  HQ_DASSERT(K % BK == 0 && nt >= 2 && N % BN == 0 && M % BM == 0);
+
+  int voA[2], voB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * 16 + i * 8 + (lane >> 3);
+    const int src_slot = (lane & 7) ^ ((row >> 1) & 7);
+    voA[i] = (row * lda + src_slot * 8) * 2;
+    voB[i] = (row * ldb + src_slot * 8) * 2;
+  }
+  // buffer descriptors over a tile's A row panel / B column panel
+  auto rsrc_a = [&](int tile) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)(tile / tiles_n) * BM * lda), (short)0, BM * lda * 2,
+                                             0x00020000);
+  };
+  auto rsrc_b = [&](int tile) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(B + (size_t)(tile % tiles_n) * BN * ldb), (short)0, BN * ldb * 2,
+                                             0x00020000);
+  };
+  // one 16 KiB half (128 rows × 64 bf16) of K-tile `kt` into LDS buffer `buf`
+  auto stA = [&](__amdgpu_buffer_rsrc_t rs, int half, int kt, int buf) {
+    char* dst = smem + buf * STAGE + (half * 128 + wave_u * 16) * 128;
+    const int so = half * 128 * lda * 2 + kt * BK * 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + i * 8 * 128), 16, voA[i], so, 0, 0);
+  };
+  auto stB = [&](__amdgpu_buffer_rsrc_t rs, int half, int kt, int buf) {
+    char* dst = smem + buf * STAGE + PANEL + (half * 128 + wave_u * 16) * 128;
+    const int so = half * 128 * ldb * 2 + kt * BK * 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + i * 8 * 128), 16, voB[i], so, 0, 0);
+  };
+
+  f32x4_t acc[8][4];
+  const int fr = lane & 15, fq = lane >> 4;
+  bf16x8_t af[2][4];
+  bf16x8_t bf0[2][2], bf1[2][2];
+  auto readA = [&](int buf, int mh) {
+    const char* pa = smem + buf * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[ks][i] = frag(pa, mh * 128 + wm * 64 + i * 16 + fr, ks * 4 + fq);
+  };
+  auto readB = [&](int buf, int nh, bf16x8_t (&bf)[2][2]) {
+    const char* pb = smem + buf * STAGE + PANEL;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[ks][j] = frag(pb, nh * 128 + wn * 32 + j * 16 + fr, ks * 4 + fq);
+  };
+  auto mma = [&](int mh, int nh, const bf16x8_t (&bf)[2][2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mh * 4 + i][nh * 2 + j] = mfma16(bf[ks][j], af[ks][i], acc[mh * 4 + i][nh * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = []() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  int tile = id;
+  if (tile >= ntiles) return;   // whole workgroup
+  __amdgpu_buffer_rsrc_t ca = rsrc_a(tile), cb = rsrc_b(tile);
+  int p0 = 0;                   // LDS buffer of this tile's K-tile 0
+  // prologue of the first tile (as v2): K-tile 0 (A0 B0 B1 A1) and the first two halves of K-tile 1
+  stA(ca, 0, 0, 0); stB(cb, 0, 0, 0); stB(cb, 1, 0, 0); stA(ca, 1, 0, 0);
+  stA(ca, 0, 1, 1); stB(cb, 0, 1, 1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  bar();
+  bool first = true;
+
+  for (;;) {
+    const int next = tile + nwg;
+    const bool last = next >= ntiles;
+    const __amdgpu_buffer_rsrc_t na = rsrc_a(last ? tile : next), nb = rsrc_b(last ? tile : next);
+    const int tm = tile / tiles_n, tn = tile % tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+    // One K-tile = 4 phases (v2's table); "t+1" / "t+2" halves past this tile's end come from the next
+    // tile's K-tile 0 (t+1 == nt, t+2 == nt); the next tile's K-tile 1 (t+2 == nt+1) is held back.
+    auto ktile = [&](int t) {
+      const bool more1 = t + 1 < nt || !last;
+      const bool more2 = t + 2 < nt || (t + 2 == nt && !last);
+      const int b0 = (p0 + t) & 1, b1 = b0 ^ 1;
+      const bool x1 = t + 1 >= nt, x2 = t + 2 >= nt;        // the "ahead" halves belong to the next tile
+      const __amdgpu_buffer_rsrc_t a1 = x1 ? na : ca, b1r = x1 ? nb : cb;
+      const __amdgpu_buffer_rsrc_t a2 = x2 ? na : ca, b2r = x2 ? nb : cb;
+      const int k1 = x1 ? t + 1 - nt : t + 1, k2 = x2 ? t + 2 - nt : t + 2;
+      // P0 (0,0)
+      if (t == 0 && !first) {
+        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E) : "memory");
+      } else if (more1) {
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      readB(b0, 0, bf0);
+      readA(b0, 0);
+      if (more1) stB(b1r, 1, k1, b1);
+      bar();
+      mma(0, 0, bf0);
+      bar();
+      // P1 (0,1)
+      if (t == 0 && !first) {
+        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E) : "memory");
+      } else if (more1) {
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      readB(b0, 1, bf1);
+      if (more1) stA(a1, 1, k1, b1);
+      bar();
+      mma(0, 1, bf1);
+      bar();
+      // P2 (1,1)
+      readA(b0, 1);
+      if (more2) stA(a2, 0, k2, b0);
+      bar();
+      mma(1, 1, bf1);
+      bar();
+      // P3 (1,0)
+      if (more1) {
+        if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      }
+      if (more2) stB(b2r, 0, k2, b0);
+      bar();
+      mma(1, 0, bf0);
+      bar();
+    };
+    if (__builtin_amdgcn_readfirstlane(wm) == 0) {
+      for (int t = 0; t < nt; ++t) ktile(t);
+      bar();
+    } else {
+      bar();
+      for (int t = 0; t < nt; ++t) ktile(t);
+    }
+    // every wave has passed its last MFMA phase: the buffer of the last K-tile is free
+    const int bl = (p0 + nt - 1) & 1;
+    char* wreg = wave < 7 ? smem + bl * STAGE + wave * REGION : smem + SPARE;
+
+    // ---- epilogue (v2's math), 64 local rows per round
+    constexpr int SEGS = WN / 8, ROWS_PER_IT = 64 / SEGS;
+    constexpr bool kReadsAux = EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID;
+    constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD;
+    const int seg = lane % SEGS, rsub = lane / SEGS;
+    const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;
+    float csum[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+#pragma unroll
+    for (int rnd = 0; rnd < 2; ++rnd) {
+#pragma unroll
+      for (int J = 0; J < 4; ++J) {
+        const int nh = J >> 1, j = J & 1;
+        const int lc = nh * 32 + j * 16 + fq * 4;
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
+#pragma unroll
+        for (int I = 0; I < 4; ++I) {
+          const f32x4_t& a = acc[rnd * 4 + I][J];
+          float v[4] = {a[0], a[1], a[2], a[3]};
+          if constexpr (kBias) { v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w; }
+          *reinterpret_cast<uint2*>(wreg + (I * 16 + fr) * RS + lc * 2) = hq_pack4(v);
+        }
+      }
+      uint4 aux[kReadsAux ? 8 : 1];
+      auto goff_of = [&](int it) {   // it: 0..7 within this round
+        const int lr = it * ROWS_PER_IT + rsub;  // 0..63
+        return (size_t)(m0 + rnd * 128 + wm * 64 + lr) * ldc + gcol;
+      };
+      if constexpr (kReadsAux) {
+        const uint16_t* src = EPI == HQ_EPI_RESID ? R : P;
+#pragma unroll
+        for (int it = 0; it < 8; ++it) aux[it] = *reinterpret_cast<const uint4*>(src + goff_of(it));
+      }
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int lr = it * ROWS_PER_IT + rsub;
+        uint4 piece = *reinterpret_cast<const uint4*>(wreg + lr * RS + seg * 16);
+        const size_t goff = goff_of(it);
+        if constexpr (EPI == HQ_EPI_GELU) {
+          *reinterpret_cast<uint4*>(P + goff) = piece;
+          float x[8];
+          hq_unpack8(piece, x);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = gelu_erf(x[e]);
+          piece = hq_pack8(x);
+        } else if constexpr (EPI == HQ_EPI_GELUD) {
+          float x[8], g[8];
+          hq_unpack8(piece, x);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            float c, d;
+            hq_normal_cdf_pdf(x[e], c, d);
+            g[e] = fmaf(x[e], d, c);
+            x[e] *= c;
+          }
+          *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
+          piece = hq_pack8(x);
+        } else if constexpr (EPI == HQ_EPI_DMUL) {
+          float d[8], gd[8];
+          hq_unpack8(piece, d);
+          hq_unpack8(aux[it], gd);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { d[e] *= gd[e]; csum[e] += d[e]; }
+          piece = hq_pack8(d);
+        } else if constexpr (EPI == HQ_EPI_DGELU) {
+          float d[8], pr[8];
+          hq_unpack8(piece, d);
+          hq_unpack8(aux[it], pr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { d[e] *= gelu_grad(pr[e]); csum[e] += d[e]; }
+          piece = hq_pack8(d);
+        } else if constexpr (EPI == HQ_EPI_RESID) {
+          float d[8], rr[8];
+          hq_unpack8(piece, d);
+          hq_unpack8(aux[it], rr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) d[e] += rr[e];
+          piece = hq_pack8(d);
+        }
+        *reinterpret_cast<uint4*>(C + goff) = piece;
+      }
+    }
+    if constexpr (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        for (int o = SEGS; o < 64; o <<= 1) csum[e] += __shfl_xor(csum[e], o, 64);
+      float* red = reinterpret_cast<float*>(smem + SPARE + REGION);  // [2][BN], by tile column
+      if (rsub == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[wm * BN + (gcol - n0) + e] = csum[e];
+      }
+      bar();
+      for (int c = tid; c < BN; c += kThreads) part[(size_t)tm * N + n0 + c] = red[c] + red[BN + c];
+    }
+    if (last) break;
+    // every wave has read its staging rounds out of buffer bl: stage the next tile's K-tile-1 halves there
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    stA(na, 0, 1, bl); stB(nb, 0, 1, bl);
+    tile = next;
+    ca = na;
+    cb = nb;
+    p0 = (p0 + nt) & 1;
+    first = false;
+  }
+}
+
+int g_gemm_variant = 0;   // 0 = auto (v3 for K <= 2304, else v2), 1 = force v1, 2 = force v2, 3 = force v3
 
 constexpr size_t epi_lds(int bn) {
   const size_t stage = 2 * (size_t)(BM * 128 + bn * 128);
@@ -580,8 +891,22 @@ template <int EPI>
 void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,
                 float* part, int M, int N, int K, int lda, int ldb, int ldc, int bn, hipStream_t s) {
   const int grid = (M / BM) * (N / bn);
-  if (bn == 256 && g_gemm_variant == 0 && K >= 2 * BK && (size_t)BM * lda * 2 < (1ull << 31) &&
-      (size_t)256 * ldb * 2 < (1ull << 31)) {
+  const bool srd_ok = (size_t)BM * lda * 2 < (1ull << 31) && (size_t)256 * ldb * 2 < (1ull << 31);
+  // v3 (persistent, pipelined across tiles) where the per-tile fixed cost matters: K <= 2304 (+2-6 % at
+  // K = 768 / 2304 on the b256 shapes, -1-3 % at K = 3072: tools/gemm_nt3_check.py, profiles/s3_gemm_v3)
+  const bool v3_auto = g_gemm_variant == 0 && K <= 2304;
+  if (bn == 256 && (g_gemm_variant == 3 || v3_auto) && K >= 2 * BK && srd_ok) {
+    constexpr size_t lds = 2 * 2 * 256 * 128 + 64 * 144 + 2 * 256 * 4;
+    static int ncu = [] {
+      int dev = 0, n = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipFuncSetAttribute((const void*)gemm_nt3_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      return n > 0 ? n : 256;
+    }();
+    hipLaunchKernelGGL((gemm_nt3_kernel<EPI>), dim3(std::min(grid, ncu)), dim3(kThreads), lds, s, A, B, C, bias, P, R, part,
+                       M, N, K, lda, ldb, ldc);
+  } else if (bn == 256 && (g_gemm_variant == 0 || g_gemm_variant == 2 || g_gemm_variant == 3) && K >= 2 * BK && srd_ok) {
     // production v2: buffer_load…lds staging (+8-12 % over global_load_lds on the BERT shapes,
     // tools/gemm_lab); grouped 8-row-panel tile order only for wide N (+15 % at 8192², neutral at
     // N <= 3072 where an XCD's co-resident tiles already share few panels).

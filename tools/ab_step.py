@@ -36,6 +36,8 @@ def set_toggle(name, on):
         ops.set_gemm_mode("blas" if on else "auto")
     elif name == "gemm_v1":
         _native.kernels().gemm_set_variant(1 if on else 0)
+    elif name == "gemm_v2":   # on: per-tile v2 everywhere; off: auto (persistent v3 for K <= 2304)
+        _native.kernels().gemm_set_variant(2 if on else 0)
     elif name.startswith("fwd_mfma="):  # e.g. fwd_mfma=qkv,out,ffn2 : B runs those forward projections on MFMA
         ops.FWD_MFMA = set(name.split("=", 1)[1].split(",")) if on else set()
     elif name == "input_pipeline":

@@ -1,0 +1,106 @@
+#!/usr/bin/env python
+"""Persistent NT GEMM (variant 3) vs the per-tile v2 kernel (variant 0): bitwise comparison over shapes
+and epilogues (same MFMA order → identical bits), a repeat-run race screen, then timings at the b256
+projection shapes.
+
+    python tools/gemm_nt3_check.py [--T 98304] [--repeats 5]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from ml_recipe_distributed_pytorch_amd import _native  # noqa: E402
+
+EPI = {"none": 0, "bias": 1, "gelu": 2, "dgelu": 3, "resid": 4, "gelud": 5, "dmul": 6}
+
+
+def run(k, A, B, e, bias, P, R, part, variant):
+    k.gemm_set_variant(variant)
+    kw = {}
+    if e in (1, 2, 5):
+        kw["bias"] = bias
+    if e in (2, 3, 5, 6):
+        kw["pre"] = P
+    if e in (3, 6):
+        kw["part"] = part
+    if e == 4:
+        kw["resid"] = R
+    out = k.gemm_nt(A, B, e, **kw)
+    k.gemm_set_variant(0)
+    return out
+
+
+def timeit(fn, iters=20):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    fn()
+    ev[0].record()
+    for _ in range(iters):
+        fn()
+    ev[1].record()
+    ev[1].synchronize()
+    return ev[0].elapsed_time(ev[1]) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--T", type=int, default=98304)
+    ap.add_argument("--repeats", type=int, default=5)
+    a = ap.parse_args()
+    k = _native.kernels()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    bad = 0
+    # correctness: small and odd tile counts (fewer tiles than CUs, not a multiple of the grid), every epilogue
+    for (M, N, K) in ((256, 256, 128), (512, 768, 192), (2560, 768, 768), (256 * 300, 512, 256), (4096, 3072, 768),
+                      (24576, 768, 2304)):
+        A = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
+        B = (torch.rand(N, K, device=dev) * 0.2 - 0.1).bfloat16()
+        bias = torch.rand(N, device=dev)
+        R = torch.randn(M, N, device=dev).bfloat16()
+        for name, e in EPI.items():
+            P0 = torch.randn(M, N, device=dev).bfloat16()
+            P3 = P0.clone()
+            part0 = torch.zeros(M // 256, N, device=dev)
+            part3 = torch.zeros(M // 256, N, device=dev)
+            c0 = run(k, A, B, e, bias, P0, R, part0, 0)
+            outs = []
+            for _ in range(a.repeats):
+                P3.copy_(P0 if e not in (2, 5) else P3)
+                c3 = run(k, A, B, e, bias, P3, R, part3, 3)
+                outs.append(c3.clone())
+            same = all(torch.equal(o, c0) for o in outs)
+            same_p = torch.equal(P3, P0) if e in (2, 5) else True
+            same_part = torch.equal(part3, part0) if e in (3, 6) else True
+            ok = same and same_p and same_part
+            bad += not ok
+            print(json.dumps({"M": M, "N": N, "K": K, "epi": name, "bitwise_equal": ok}), flush=True)
+    T = a.T
+    for N, K, epis in ((3072, 768, ("none", "bias", "gelud", "dmul")), (768, 768, ("none", "bias", "resid")),
+                       (2304, 768, ("bias",)), (768, 3072, ("none", "bias")), (768, 2304, ("resid",))):
+        A = (torch.rand(T, K, device=dev) * 2 - 1).bfloat16()
+        B = (torch.rand(N, K, device=dev) * 0.2 - 0.1).bfloat16()
+        bias = torch.rand(N, device=dev)
+        P = torch.randn(T, N, device=dev).bfloat16()
+        R = torch.randn(T, N, device=dev).bfloat16()
+        part = torch.empty(T // 256, N, device=dev)
+        fl = 2.0 * T * N * K
+        for name in epis:
+            e = EPI[name]
+            res = {}
+            for v in (0, 3, 0, 3):
+                us = sorted(timeit(lambda: run(k, A, B, e, bias, P, R, part, v)) for _ in range(3))[1]
+                res.setdefault(v, []).append(us)
+            u0, u3 = min(res[0]), min(res[3])
+            print(json.dumps({"T": T, "N": N, "K": K, "epi": name, "v2_us": round(u0, 1), "v3_us": round(u3, 1),
+                              "v3_tflops": round(fl / u3 / 1e6, 1), "speedup": round(u0 / u3, 3)}), flush=True)
+        del A, B, P, R, part
+    print("MISMATCHES", bad)
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()
