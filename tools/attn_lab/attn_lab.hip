@@ -751,6 +751,24 @@ int main(int argc, char** argv) {
            }));
   }
   run_v4(fwd_v4<12, 12, 12>, "persistent");
+  {
+    auto k = fwd_v3<12, 12>;
+    HQ_CHECK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    for (int rep = 0; rep < 2; ++rep) {
+      report("v3 DMA prologue p=0", time_it([&] {
+               hipLaunchKernelGGL(k, dim3(B * nh, 1), dim3(768), lds, 0, qkv, kb, ctx1, lse1, L, nh, scale * LOG2E);
+             }));
+      report("fwd prod p=0 (interleaved)",
+             time_it([&] { hq_attn_fwd(qkv, kb, ctx0, lse0, nullptr, B, L, nh, D, 0.f, 1, 1, scale, 0); }));
+    }
+    HQ_CHECK(hipDeviceSynchronize());
+    std::vector<uint16_t> a(T * H), b(T * H);
+    HQ_CHECK(hipMemcpy(a.data(), ctx0, T * H * 2, hipMemcpyDeviceToHost));
+    HQ_CHECK(hipMemcpy(b.data(), ctx1, T * H * 2, hipMemcpyDeviceToHost));
+    double md = 0;
+    for (size_t i = 0; i < a.size(); ++i) md = std::max(md, (double)fabsf(bf2f(a[i]) - bf2f(b[i])));
+    printf("  v3 vs prod max|diff| = %.3g\n", md);
+  }
 
   report("fwd prod p=0 (again)", time_it([&] { hq_attn_fwd(qkv, kb, ctx0, lse0, nullptr, B, L, nh, D, 0.f, 1, 1, scale, 0); }));
   report("fwd prod p=0.1", time_it([&] {

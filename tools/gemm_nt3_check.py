@@ -55,8 +55,9 @@ def main():
     torch.manual_seed(0)
     bad = 0
     # correctness: small and odd tile counts (fewer tiles than CUs, not a multiple of the grid), every epilogue
+    # (2560, 768): 30 tiles; (98304, 768): 1152 tiles = 4.5 rounds -> the half-tile items; (256*300, 512): 600
     for (M, N, K) in ((256, 256, 128), (512, 768, 192), (2560, 768, 768), (256 * 300, 512, 256), (4096, 3072, 768),
-                      (24576, 768, 2304)):
+                      (24576, 768, 2304), (98304, 768, 768), (98304 - 256 * 7, 768, 256)):
         A = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
         B = (torch.rand(N, K, device=dev) * 0.2 - 0.1).bfloat16()
         bias = torch.rand(N, device=dev)
@@ -66,7 +67,7 @@ def main():
             P3 = P0.clone()
             part0 = torch.zeros(M // 256, N, device=dev)
             part3 = torch.zeros(M // 256, N, device=dev)
-            c0 = run(k, A, B, e, bias, P0, R, part0, 0)
+            c0 = run(k, A, B, e, bias, P0, R, part0, 2)
             outs = []
             for _ in range(a.repeats):
                 P3.copy_(P0 if e not in (2, 5) else P3)
@@ -91,10 +92,10 @@ def main():
         for name in epis:
             e = EPI[name]
             res = {}
-            for v in (0, 3, 0, 3):
+            for v in (2, 3, 2, 3):
                 us = sorted(timeit(lambda: run(k, A, B, e, bias, P, R, part, v)) for _ in range(3))[1]
                 res.setdefault(v, []).append(us)
-            u0, u3 = min(res[0]), min(res[3])
+            u0, u3 = min(res[2]), min(res[3])
             print(json.dumps({"T": T, "N": N, "K": K, "epi": name, "v2_us": round(u0, 1), "v3_us": round(u3, 1),
                               "v3_tflops": round(fl / u3 / 1e6, 1), "speedup": round(u0 / u3, 3)}), flush=True)
         del A, B, P, R, part
