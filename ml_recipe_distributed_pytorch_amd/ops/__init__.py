@@ -99,7 +99,8 @@ _GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
 # Plain forward projections (bias epilogue) that take the MFMA kernel in auto mode, by name: qkv | out | ffn2.
 # In the full b256 step hipBLASLt's QKV pick runs 381 µs vs 316 µs standalone while the MFMA kernel holds
 # ~337 µs (+0.4 % step); the out-projection / FFN2 forwards are step-neutral either way (profiles/s3_ab), so
-# all three default to the own kernel and the bf16 training step runs no vendor GEMM.
+# all three default to the own kernel and the bf16 encoder runs no vendor GEMM (the tiny pooler/head
+# GEMMs stay in torch).
 FWD_MFMA = {k for k in os.environ.get("HQ_FWD_MFMA", "qkv,out,ffn2").split(",") if k}
 GELU_DERIV = os.environ.get("HQ_GELU_DERIV", "1") == "1"   # FFN1 stores gelu'(pre) (linear_gelu_fwd_d)
 _CUS = 256
