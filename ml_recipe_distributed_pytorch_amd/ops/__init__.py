@@ -92,7 +92,7 @@ def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale
 #     profiles/) and the QKV dgrad + residual-gradient add (torch.addmm first copies the residual
 #     into the output: +56 µs at b256), plus the plain dgrads — when the 256-row tile grid fills the
 #     256 CUs to >= 85 %.  Weight gradients always take the split-K TN kernel (gemm_tn.hip).
-#     Plain forward projections stay on hipBLASLt with the shipped TunableOp picks (2-13 % faster);
+#     Plain forward projections follow FWD_MFMA below (all three on the MFMA kernel by default);
 #   HQ_GEMM=mfma: every supported shape;  HQ_GEMM=blas: none.
 _EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID, _EPI_GELUD, _EPI_DMUL = range(7)
 _GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
