@@ -144,6 +144,7 @@ def main():
                       "parallelism": f"dp{world}", "allreduce_dtype": args.allreduce_dtype,
                       "bucket_cap_mb": args.bucket_cap_mb},
            "mfu_bf16_dense": round(value * flops_per_sample / (world * 2.5e15), 4),
+           "max_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2),
            "final_loss": round(final_loss, 4)}
     if args.profile:
         out["phase_ms"] = {k: round(v / args.steps, 3) for k, v in phase.items()}

@@ -169,6 +169,9 @@ def get_trainer_parser() -> ArgumentParser:
     parser.add_argument("--no_sync_accum", type=cast2(int), default=1,
                         help="1: all-reduce only at the accumulation boundary (fix of D1); 0: every micro-batch.")
     parser.add_argument("--dist_timeout", type=float, default=1800.0, help="Process-group timeout in seconds.")
+    parser.add_argument("--auto_batch_split", action="store_true",
+                        help="GPU: raise --batch_split only as far as the HBM memory model (train/memory.py) needs "
+                             "for train_batch_size // batch_split to fit (288 GB MI355X: usually 1).")
     parser.add_argument("--profile", action="store_true", help="Per-phase step timers + perf/* TB scalars.")
     parser.add_argument("--torch_profile_dir", type=cast2(str), default=None,
                         help="Export a torch.profiler Chrome trace of optimizer steps --torch_profile_steps here.")

@@ -96,3 +96,29 @@ def test_bert_base_fp8_forward_close_to_bf16(cuda):
     m.zero_grad()
     loss.backward()
     assert torch.isfinite(m.store.grad).all()
+
+
+def test_memory_model_matches_measured_slope(cuda):
+    """train/memory.py's per-sample bytes vs the measured growth of the fwd+bwd peak between two batch
+    sizes (BERT-base, L = 256) — the model --auto_batch_split sizes micro-batches with."""
+    from ml_recipe_distributed_pytorch_amd.train.memory import estimate
+    cfg = get_config("bert-base-uncased")
+    L = 256
+    m = BertForQuestionAnswering(cfg, seed=0).to(cuda).train()
+    peaks = {}
+    for B in (8, 40):
+        ids, mask, tt = _inputs(B, L, cfg.vocab_size)
+        ids, mask, tt = ids.to(cuda), mask.to(cuda), tt.to(cuda)
+        m.zero_grad()
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats(cuda)
+        base = torch.cuda.memory_allocated(cuda)
+        loss = sum(v.float().mean() for v in m(ids, mask, tt).values())
+        loss.backward()
+        torch.cuda.synchronize()
+        peaks[B] = torch.cuda.max_memory_allocated(cuda) - base
+        del loss
+    measured = (peaks[40] - peaks[8]) / 32
+    est = estimate(cfg, L)
+    modelled = est.act_bytes_per_sample + est.transient_bytes_per_sample
+    assert measured == pytest.approx(modelled, rel=0.2), (measured, modelled)
