@@ -76,7 +76,8 @@ def kernels():
             raise RuntimeError("HQ_KERNELS_DEBUG=1 but the debug kernel library is not built. Run "
                                "`python -m ml_recipe_distributed_pytorch_amd.csrc.build --kernels --debug`.")
         return _SyncedKernels(mod)
-    mod = _load("_hq_kernels")
+    # HQ_KERNELS_DIR: load an alternative release build (A/B of two kernel variants in one GPU call)
+    mod = _load("_hq_kernels", os.environ.get("HQ_KERNELS_DIR", _PKG_DIR))
     if mod is None:
         raise RuntimeError(
             "HIP kernel library _hq_kernels.so is not built. Run `python -m ml_recipe_distributed_pytorch_amd.csrc.build` "

@@ -125,6 +125,42 @@ __device__ __forceinline__ bf16x8_t prescale8(const bf16x8_t& q, float c) {
 
 __device__ __forceinline__ int acc_row(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
 
+// One 64-column output row per lane pair from two transposed 32x32 accumulators (the O / dQ / dK / dV
+// layout: lane q and q+32 hold the two 4-column halves of each 8-column group) as 16-B stores (playbook
+// T21): one permlane32 swap per pair of groups hands lane q the 8 columns of the even group and lane q+32
+// those of the odd one — 4 dwordx4 stores per lane instead of 8 dwordx2 (the store tail is issue-bound).
+__device__ __forceinline__ void store_row64(uint16_t* out, const f32x16_t (&a)[2], float mul, int hh) {
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; g += 2) {
+      const float va[4] = {a[d][4 * g] * mul, a[d][4 * g + 1] * mul, a[d][4 * g + 2] * mul, a[d][4 * g + 3] * mul};
+      const float vb[4] = {a[d][4 * g + 4] * mul, a[d][4 * g + 5] * mul, a[d][4 * g + 6] * mul, a[d][4 * g + 7] * mul};
+      const uint2 A = hq_pack4(va), B = hq_pack4(vb);
+      // swap(vdst = A, src = B): lanes 32-63 of A trade with lanes 0-31 of B, so lane q now holds
+      // [own A | partner's A] = group g and lane q+32 [partner's B | own B] = group g+1
+      const auto r0 = __builtin_amdgcn_permlane32_swap(A.x, B.x, false, false);
+      const auto r1 = __builtin_amdgcn_permlane32_swap(A.y, B.y, false, false);
+      *reinterpret_cast<uint4*>(out + d * 32 + 8 * g + 8 * hh) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+    }
+}
+
+// Static issue priority of a workgroup's waves for the whole main loop (MI355X_MICROARCH "Two waves per
+// SIMD", item 4): VALU issue on a SIMD goes to the higher-priority, then the older wave.  g_attn_prio
+// (host: HQ_ATTN_PRIO) 0 = off, 1 = second half of the waves at prio 1, 2 = three levels (3 waves/SIMD).
+__device__ int g_attn_prio = 0;
+// forward online softmax: tolerated growth (log2 units) of a row max before a rescale (host: HQ_ATTN_DEFER)
+__device__ float g_attn_defer = 8.f;
+__device__ __forceinline__ void wave_prio(int wave, int nw) {
+  const int mode = g_attn_prio;
+  if (mode == 1) {
+    if (wave >= nw / 2) __builtin_amdgcn_s_setprio(1);
+  } else if (mode == 2) {
+    if (wave >= (2 * nw) / 3) __builtin_amdgcn_s_setprio(2);
+    else if (wave >= nw / 3) __builtin_amdgcn_s_setprio(1);
+  }
+}
+
 // Packed-f32 pair (v_pk_add/mul/fma_f32 on gfx950: two lanes' worth of f32 work per VALU issue).
 typedef float f2_t __attribute__((ext_vector_type(2)));
 
@@ -216,6 +252,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
   if (qs * 32 >= L) return;
   LdsOffsets lo_;
   lo_.init(lane);
+  wave_prio(wave, NWB);
 
   f32x16_t o[2];
 #pragma unroll
@@ -223,6 +260,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
   float m_run = -INFINITY;
+  const float defer = g_attn_defer;
   f2_t l2 = {0.f, 0.f};  // running row sum, two partial sums (packed adds)
   const uint32_t row_idx = ((uint32_t)bh * L + (uint32_t)min(qi, L - 1)) * (uint32_t)L;
   uint16_t* my_bits = mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane;
@@ -262,7 +300,11 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
         for (int d = 0; d < 2; ++d) vt[s][d] = tr8(sV, kt * 32, lo_, s, d);
     }
     const float mx = xor32_max(max16(acc));
-    if (__any(mx > m_run)) {  // exact rescale skip: α = 1 for every lane whose max did not grow
+    // deferred max (playbook T13): rescale only when some lane's tile max exceeds its running max by more
+    // than `defer`, so after the first tiles the branch (and its O-wide multiply) is rarely taken.  P
+    // then stays <= 2^defer: exact in the fp32 row sum and O accumulators, and bf16 P keeps its
+    // relative precision; LSE = m_run + log2(l) remains exact for the backward.
+    if (__any(mx > m_run + defer)) {
       const float m_new = fmaxf(m_run, mx);
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
       m_run = m_new;
@@ -329,15 +371,8 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
   }
   const float l_tot = xor32_sum(l2.x + l2.y);
   const float inv = (DROP ? kscale : 1.f) / l_tot;
-  if (qi < L) {
-    uint16_t* out = ctx + ((size_t)b * L + qi) * H + h * D;
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float v4[4] = {o[d][4 * g] * inv, o[d][4 * g + 1] * inv, o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv};
-        *reinterpret_cast<uint2*>(out + d * 32 + 8 * g + 4 * hh) = hq_pack4(v4);
-      }
+  if (qi < L) {  // lanes q and q+32 share qi: the permlane partners are active together
+    store_row64(ctx + ((size_t)b * L + qi) * H + h * D, o, inv, hh);
     if (hh == 0) lse[(size_t)bh * L + qi] = (m_run + __builtin_amdgcn_logf(l_tot)) * LN2;  // v_log_f32 = log2
   }
 }
@@ -408,6 +443,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
   if (qs * 32 >= L) return;
   LdsOffsets lo_;
   lo_.init(lane);
+  wave_prio(wave, NWB);
 
   f32x16_t dq[2];
 #pragma unroll
@@ -453,16 +489,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
       for (int d = 0; d < 2; ++d) dq[d] = mfma32(tr8(sK, kt * 32, lo_, s, d), sb, dq[d]);
     }
   }
-  if (qok) {
-    uint16_t* out = dqkv + ((size_t)b * L + qi) * ld + h * D;
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float v4[4] = {dq[d][4 * g] * scale, dq[d][4 * g + 1] * scale, dq[d][4 * g + 2] * scale, dq[d][4 * g + 3] * scale};
-        *reinterpret_cast<uint2*>(out + d * 32 + 8 * g + 4 * hh) = hq_pack4(v4);
-      }
-  }
+  if (qok) store_row64(dqkv + ((size_t)b * L + qi) * ld + h * D, dq, scale, hh);
 }
 
 // ============================================================================ backward: dK, dV
@@ -522,6 +549,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
   if (ks_idx * 32 >= L) return;
   LdsOffsets lo_;
   lo_.init(lane);
+  wave_prio(wave, NWB);
 
   // Two passes over the queries (dV, then dK with S recomputed): +25 % MFMA, but the live set of a
   // single pass (K/V fragments + dV/dK accumulators + S/dP tiles ≈ 200 VGPRs) spills at the 168-VGPR
@@ -589,15 +617,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
         for (int d = 0; d < 2; ++d) dv[d] = mfma32(tr8(sO, qt * 32, lo_, s, d), pb, dv[d]);
       }
     }
-    if (kok) {
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          float v4[4] = {dv[d][4 * g], dv[d][4 * g + 1], dv[d][4 * g + 2], dv[d][4 * g + 3]};
-          *reinterpret_cast<uint2*>(out + 2 * H + d * 32 + 8 * g + 4 * hh) = hq_pack4(v4);
-        }
-    }
+    if (kok) store_row64(out + 2 * H, dv, 1.f, hh);
   }
   // ------------------------------------------------------------------ pass 2: dKᵀ += Qᵀ·dS
   {
@@ -641,16 +661,8 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
         for (int d = 0; d < 2; ++d) dk[d] = mfma32(tr8(sQ, qt * 32, lo_, s, d), sb, dk[d]);
       }
     }
-    if (kok) {
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          // sQ holds Q·c (c = scale·log2e): dK = scale·Σ dS·q = Σ dS·(q·c) / log2e
-          float k4[4] = {dk[d][4 * g] * LN2, dk[d][4 * g + 1] * LN2, dk[d][4 * g + 2] * LN2, dk[d][4 * g + 3] * LN2};
-          *reinterpret_cast<uint2*>(out + H + d * 32 + 8 * g + 4 * hh) = hq_pack4(k4);
-        }
-    }
+    // sQ holds Q·c (c = scale·log2e): dK = scale·Σ dS·q = Σ dS·(q·c) / log2e
+    if (kok) store_row64(out + H, dk, LN2, hh);
   }
 }
 
@@ -689,8 +701,24 @@ size_t hq_attn_mask_bytes(int B, int L, int nh) {
   return (size_t)B * nh * n32 * n32 * 64 * sizeof(uint16_t);
 }
 
+static void set_attn_prio() {
+  static const bool once = [] {
+    const char* e = getenv("HQ_ATTN_PRIO");
+    const int v = e ? atoi(e) : 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_prio), &v, sizeof(int));
+    const char* d = getenv("HQ_ATTN_DEFER");
+    if (d) {
+      const float f = (float)atof(d);
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_defer), &f, sizeof(float));
+    }
+    return true;
+  }();
+  (void)once;
+}
+
 void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, float* lse, uint16_t* mbits, int B, int L,
                  int nh, int dh, float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s) {
+  set_attn_prio();
   if (dh != D || L > 512) { fprintf(stderr, "hq_attn_fwd: head_dim %d / L %d unsupported\n", dh, L); abort(); }
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const uint32_t key = hq_op_key(seed, opid);
@@ -722,6 +750,7 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
 void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx, const float* lse, const float* key_bias,
                  const uint16_t* mbits, uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p,
                  float scale, hipStream_t s) {
+  set_attn_prio();
   if (dh != D || L > 512) { fprintf(stderr, "hq_attn_bwd: head_dim %d / L %d unsupported\n", dh, L); abort(); }
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const float ks = hq_keep_scale(thr);

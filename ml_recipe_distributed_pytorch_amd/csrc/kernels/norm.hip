@@ -139,25 +139,32 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
     gam[c][0] = g.x; gam[c][1] = g.y; gam[c][2] = g.z; gam[c][3] = g.w;
   }
   const int row0 = blockIdx.x * kWaves * kRowsPerWave + wave;
-  uint2 cdy[NCH], cdy2[NCH], cz[NCH];
-  float cmu = 0.f, crs = 0.f;
+  // loads run TWO rows ahead (c = this row, n = next, f = the one after): with one row in flight per
+  // wave the kernel left ~15 % of the HBM bandwidth unused at its 4 waves/SIMD occupancy
+  uint2 cdy[NCH], cdy2[NCH], cz[NCH], ndy[NCH], ndy2[NCH], nz[NCH];
+  float cmu = 0.f, crs = 0.f, nmu = 0.f, nrs = 0.f;
   if (row0 < T) {
     ln_bwd_load<NCH>(dy, dy2, z, (size_t)row0 * H, lane, H, cdy, cdy2, cz);
     cmu = mean[row0];
     crs = rstd[row0];
+  }
+  if (kRowsPerWave > 1 && row0 + kWaves < T) {
+    ln_bwd_load<NCH>(dy, dy2, z, (size_t)(row0 + kWaves) * H, lane, H, ndy, ndy2, nz);
+    nmu = mean[row0 + kWaves];
+    nrs = rstd[row0 + kWaves];
   }
 #pragma unroll
   for (int r = 0; r < kRowsPerWave; ++r) {
     const int row = row0 + r * kWaves;
     if (row < T) {
       const size_t base = (size_t)row * H;
-      uint2 ndy[NCH], ndy2[NCH], nz[NCH];
-      float nmu = 0.f, nrs = 0.f;
-      const int nrow = row + kWaves;
-      if (r + 1 < kRowsPerWave && nrow < T) {
-        ln_bwd_load<NCH>(dy, dy2, z, (size_t)nrow * H, lane, H, ndy, ndy2, nz);
-        nmu = mean[nrow];
-        nrs = rstd[nrow];
+      uint2 fdy[NCH], fdy2[NCH], fz[NCH];
+      float fmu = 0.f, frs = 0.f;
+      const int frow = row + 2 * kWaves;
+      if (r + 2 < kRowsPerWave && frow < T) {
+        ln_bwd_load<NCH>(dy, dy2, z, (size_t)frow * H, lane, H, fdy, fdy2, fz);
+        fmu = mean[frow];
+        frs = rstd[frow];
       }
       float g[NCH][4], xh[NCH][4];
       float s1 = 0.f, s2 = 0.f;
@@ -202,9 +209,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
         }
       }
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) { cdy[c] = ndy[c]; cdy2[c] = ndy2[c]; cz[c] = nz[c]; }
-      cmu = nmu;
-      crs = nrs;
+      for (int c = 0; c < NCH; ++c) {
+        cdy[c] = ndy[c]; cdy2[c] = ndy2[c]; cz[c] = nz[c];
+        ndy[c] = fdy[c]; ndy2[c] = fdy2[c]; nz[c] = fz[c];
+      }
+      cmu = nmu; crs = nrs;
+      nmu = fmu; nrs = frs;
     }
   }
   block_partials<NCH, 3>(acc, lds, part, H);

@@ -45,7 +45,7 @@ def main():
             ("ln_bwd (dy)", lambda: k.ln_bwd(dy, None, z, g, mean, rstd, 0.1, 1, 0, gg, gb, gbias, False), 4 * mb),
             ("ln_bwd (dy + dy2)", lambda: k.ln_bwd(dy, r, z, g, mean, rstd, 0.1, 1, 0, gg, gb, gbias, False), 5 * mb)):
         us = sorted(timeit(fn) for _ in range(5))[2]
-        print(f"{name:20s} {us:8.1f} us  {nbytes / us / 1e3:6.2f} TB/s (row tensors only)")
+        print(f"{name:20s} {us:8.1f} us  {nbytes / us:6.2f} TB/s (row tensors only)")
 
 
 if __name__ == "__main__":
