@@ -138,7 +138,7 @@ def test_attention_bert_base_shape(cuda):
 @pytest.mark.parametrize("ramp", [0.05, 0.3, -0.05])
 def test_attention_deferred_rescale(cuda, ramp):
     """Row maxima that keep growing across key tiles (a key-bias ramp: +2.3 / +14 log2 units per tile, or
-    falling) and large-magnitude scores: exercises the forward's deferred rescale (HQ_ATTN_DEFER, P <= 2^8
+    falling): exercises the forward's deferred rescale (HQ_ATTN_DEFER, P <= 2^8
     between rescales) against the fp32 reference, forward and backward.  (Scaling the scores up 2x instead
     fails the bf16-vs-fp32 tolerances with the rescale deferred or not — HQ_ATTN_DEFER=0 measured worse,
     6.3e-2 vs 4.7e-2 ctx max err — so that is the bf16 P / pre-scaled Q precision, not the deferral.)"""
