@@ -62,7 +62,12 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
-        info = hqdist.init_distributed("nccl")
+        # HQ_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with every rank on cuda:0 (one-GPU box; gloo
+        # all-reduces the CUDA buckets through host memory) — never for a measurement
+        backend = os.environ.get("HQ_BENCH_BACKEND", "nccl")
+        if backend != "nccl":
+            os.environ["LOCAL_RANK"] = "0"
+        info = hqdist.init_distributed(backend)
         rank, device = info.rank, info.device
     else:
         rank, device = 0, torch.device("cuda", 0)
