@@ -35,14 +35,18 @@ def build_trainer(params, model_params, device, *, rank: int, local_idx: int, us
     model, tokenizer = factories.init_model(model_params, device=device, bpe_dropout=params.bpe_dropout,
                                             seed=params.seed, precision=params.precision)
     optimizer = factories.init_optimizer(params, model)
-    if getattr(params, "auto_batch_split", False) and device.type == "cuda":
+    auto = getattr(params, "auto_batch_split", None)
+    if device.type == "cuda" and auto is not False:  # default on for GPUs (None), off on CPU
         from ..train.memory import device_hbm_bytes, estimate, plan_batch_split
         hbm = device_hbm_bytes(device)
         split = plan_batch_split(model.config, params.max_seq_len, params.train_batch_size, hbm, params.batch_split)
         micro = params.train_batch_size // split
-        logging.getLogger(__name__).info(
-            f"auto_batch_split: batch_split {params.batch_split} -> {split} (micro-batch {micro}, modelled "
-            f"{estimate(model.config, params.max_seq_len).total(micro) / 1e9:.1f} GB of {hbm / 1e9:.0f} GB HBM)")
+        if split != params.batch_split:
+            logging.getLogger(__name__).info(
+                f"auto_batch_split: batch_split {params.batch_split} -> {split} (micro-batch "
+                f"{params.train_batch_size // params.batch_split} -> {micro}, modelled "
+                f"{estimate(model.config, params.max_seq_len).total(micro) / 1e9:.1f} GB of {hbm / 1e9:.0f} GB HBM; "
+                f"--auto_batch_split False keeps the configured split)")
         params.batch_split = split
     dist_rank = rank if hqdist.info().distributed else -1
     if dist_rank in (-1, 0):  # prepare (and cache) the dataset in the main process first

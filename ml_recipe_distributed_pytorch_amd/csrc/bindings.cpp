@@ -465,6 +465,14 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("grad_norm", &grad_norm);
+  m.def("sq_norm_partials", [](Tensor x, int64_t nparts) {
+    check(x, F32, "x");
+    TORCH_CHECK(x.is_contiguous(), "x must be contiguous");
+    c10::DeviceGuard g(x.device());
+    auto part = at::empty({nparts}, x.options());
+    hq_sq_norm_partials(ptr<float>(x), x.numel(), ptr<float>(part), (int)nparts, cur_stream());
+    return part;
+  });
   m.def("adamw", &adamw);
   m.def("adamod", &adamod);
   m.def("cast_f32_bf16", &cast_f32_bf16);
@@ -477,6 +485,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
       .def("allreduce_bf16", &HqReducer::allreduce_bf16, py::call_guard<py::gil_scoped_release>())
       .def("broadcast", &HqReducer::broadcast, py::call_guard<py::gil_scoped_release>())
       .def("wait", &HqReducer::wait)
+      .def("probe_f32", &HqReducer::probe_f32)
       .def("fence_from", &HqReducer::fence_from)
       .def("synchronize", &HqReducer::synchronize, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("comm_stream", &HqReducer::comm_stream)

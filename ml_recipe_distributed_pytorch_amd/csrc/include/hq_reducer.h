@@ -18,6 +18,9 @@ class HqReducer {
   void allreduce_bf16(int64_t ptr_f32, int64_t scratch_bf16, int64_t count, int64_t compute_stream);
   void broadcast(int64_t ptr, int64_t count, int dtype, int root, int64_t compute_stream);
   void wait(int64_t compute_stream);
+  // ordering probe (tests, HQ_REDUCER_VERIFY): after the same fence an all-reduce would take, the comm
+  // stream writes deterministic per-block sum-of-squares partials of [ptr, ptr+count) to `partials`
+  void probe_f32(int64_t ptr, int64_t count, int64_t partials, int nparts, int64_t compute_stream);
   // comm stream waits for all work issued so far on `stream` (e.g. a side stream computing grads)
   void fence_from(int64_t stream);
   void synchronize();

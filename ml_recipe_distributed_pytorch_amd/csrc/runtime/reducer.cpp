@@ -99,6 +99,11 @@ void HqReducer::broadcast(int64_t ptr, int64_t count, int dtype, int root, int64
   NCCL_CHECK(ncclBroadcast((const void*)ptr, (void*)ptr, (size_t)count, dt, root, (ncclComm_t)comm_, (hipStream_t)stream_));
 }
 
+void HqReducer::probe_f32(int64_t ptr, int64_t count, int64_t partials, int nparts, int64_t compute_stream) {
+  fence_from(compute_stream);
+  hq_sq_norm_partials((const float*)ptr, count, (float*)partials, nparts, (hipStream_t)stream_);
+}
+
 void HqReducer::wait(int64_t compute_stream) {
   hipEvent_t e = (hipEvent_t)next_event();
   HIP_CHECK_THROW(hipEventRecord(e, (hipStream_t)stream_));

@@ -107,3 +107,22 @@ def all_reduce_mean_floats(values, device=None):
     t = torch.tensor(list(values), dtype=torch.float64, device=dev)
     dist.all_reduce(t)
     return (t / dist.get_world_size()).tolist()
+
+
+def all_gather_object(obj):
+    """Every rank's ``obj`` in rank order (``[obj]`` without a process group)."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def all_reduce_sum_floats(values, device=None):
+    """Element-wise sum of a list of python floats over ranks (float64)."""
+    if not (dist.is_initialized() and dist.get_world_size() > 1):
+        return list(values)
+    dev = device or _INFO.device
+    t = torch.tensor(list(values), dtype=torch.float64, device=dev)
+    dist.all_reduce(t)
+    return t.tolist()

@@ -11,6 +11,17 @@ the remaining backward.  ``finalize()`` makes the compute stream wait for the la
 * CPU / gloo (and GPU when ``native=False``): ``torch.distributed.all_reduce(async_op=True)``.
 * ``prepare(sync=False)`` = DDP ``no_sync``: no communication during accumulation micro-batches
   (fixes reference D1, which all-reduced every micro-batch).
+* ``kind`` says which path runs ("native-rccl" | "torch-nccl" | "torch-gloo" | "none") and bench.py
+  reports it.  A failing native RCCL init is FATAL on an nccl process group (an 8-GPU number must never
+  silently measure the fallback); ``HQ_REDUCER_FALLBACK=1`` opts into the torch.distributed path.
+* ``force=True`` keeps the reducer active at world size 1 (a 1-rank RCCL communicator): every bucket of
+  a real backward goes through fence → ncclAllReduce → wait, which is how one GPU rehearses the 8-GPU
+  path (bench.py ``--force_reducer``; tests/test_kernels_gpu.py checks bitwise-equal weights).
+* ``verify=True`` (or ``HQ_REDUCER_VERIFY=1``): the comm stream also records a deterministic checksum of
+  every bucket at the exact point its all-reduce reads it; ``check_order()`` compares them with the final
+  gradients — a bucket read before its (side-stream) weight-gradient GEMMs finished shows up as a mismatch.
+* ``timing=True``: HIP events on the compute and comm streams give the comm span and the EXPOSED wait
+  (comm still running after the backward's last kernel) per synchronised step (``pop_timings()``).
 
 Sizing for xGMI: MI355X peers are point-to-point links (7 × ~153 GB/s per GPU); RCCL splits a
 bucket over its channels/rings, so 32 MiB buckets give each channel multi-MiB chunks while the first
@@ -20,6 +31,7 @@ from __future__ import annotations
 
 import itertools
 import logging
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -47,7 +59,8 @@ class Bucket:
 
 class GradReducer:
     def __init__(self, model, *, bucket_cap_mb: float = 32.0, allreduce_dtype: str = "fp32",
-                 native: Optional[bool] = None, broadcast_params: bool = True, group=None):
+                 native: Optional[bool] = None, broadcast_params: bool = True, group=None, force: bool = False,
+                 verify: Optional[bool] = None, timing: bool = False):
         self.model = model
         self.store = model.store
         self.group = group
@@ -55,6 +68,7 @@ class GradReducer:
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.bucket_cap = int(bucket_cap_mb * 1024 * 1024)
         self.allreduce_dtype = allreduce_dtype
+        self.force = bool(force)
         self.active = False
         self.buckets: List[Bucket] = []
         self.group_to_bucket: Dict[str, Bucket] = {}
@@ -65,13 +79,27 @@ class GradReducer:
         on_gpu = self.store.device.type == "cuda"
         backend = dist.get_backend(group) if dist.is_initialized() else None
         if native is None:
-            native = on_gpu and backend == "nccl"
-        if self.world > 1 and native:
+            native = on_gpu and (backend == "nccl" or (self.force and self.world == 1))
+        self.kind = "none"
+        if (self.world > 1 or self.force) and native:
             try:
                 self._native = self._make_native()
-            except Exception as e:  # e.g. RCCL refuses a second communicator: fall back to the PG's own
-                logger.warning(f"native RCCL reducer unavailable ({e}); using torch.distributed all_reduce")
+                self.kind = "native-rccl"
+            except Exception as e:
+                if os.environ.get("HQ_REDUCER_FALLBACK", "0") != "1" or self.world == 1:
+                    raise RuntimeError(f"native RCCL reducer failed to initialise: {e} "
+                                       "(HQ_REDUCER_FALLBACK=1 allows the torch.distributed path)") from e
+                logger.warning(f"native RCCL reducer unavailable ({e}); HQ_REDUCER_FALLBACK=1 → torch.distributed")
                 self._native = None
+        if self._native is None and self.world > 1:
+            self.kind = f"torch-{backend}"
+        if verify is None:
+            verify = os.environ.get("HQ_REDUCER_VERIFY", "0") == "1"
+        self.verify = bool(verify) and self._native is not None
+        self._probes: Dict[int, torch.Tensor] = {}
+        self.timing = bool(timing) and self._native is not None
+        self._tev: List[tuple] = []
+        self._first_ev = None
         self._build_buckets()
         model.set_grad_listener(self._on_group_ready)
         if self.world > 1 and broadcast_params:
@@ -79,13 +107,16 @@ class GradReducer:
 
     # ------------------------------------------------------------------ setup
     def _make_native(self):
-        key = f"hq_rccl_uid_{next(_uid_counter)}"
-        store = dist.distributed_c10d._get_default_store()
-        if self.rank == 0:
+        if self.world == 1:  # forced single-rank communicator: no rendezvous needed
             uid = kernels().rccl_unique_id()
-            store.set(key, uid)
         else:
-            uid = store.get(key)
+            key = f"hq_rccl_uid_{next(_uid_counter)}"
+            store = dist.distributed_c10d._get_default_store()
+            if self.rank == 0:
+                uid = kernels().rccl_unique_id()
+                store.set(key, uid)
+            else:
+                uid = store.get(key)
         dev = self.store.device.index if self.store.device.index is not None else torch.cuda.current_device()
         red = kernels().Reducer(self.rank, self.world, bytes(uid), dev)
         logger.info(f"native RCCL reducer up (rank {self.rank}/{self.world}, device {dev})")
@@ -127,8 +158,12 @@ class GradReducer:
         self.store.sync_compute()
 
     # ------------------------------------------------------------------ per step
+    @property
+    def n_buckets(self) -> int:
+        return len(self.buckets)
+
     def prepare(self, sync: bool = True):
-        self.active = sync and self.world > 1
+        self.active = sync and (self.world > 1 or self.force)
         for b in self.buckets:
             b.pending = len(b.groups)
             b.launched = False
@@ -157,6 +192,16 @@ class GradReducer:
             stream = torch.cuda.current_stream().cuda_stream
             if side is not None:  # weight grads computed on the side stream
                 self._native.fence_from(side.cuda_stream)
+            if self.timing and self._first_ev is None:
+                self._native.fence_from(stream)
+                self._first_ev = torch.cuda.Event(enable_timing=True)
+                self._first_ev.record(self._comm_stream())
+            if self.verify:
+                part = self._probes.get(b.index)
+                if part is None:
+                    part = self._probes[b.index] = torch.empty(self._PROBE_PARTS, dtype=torch.float32,
+                                                               device=self.store.device)
+                self._native.probe_f32(view.data_ptr(), b.numel, part.data_ptr(), self._PROBE_PARTS, stream)
             if self.allreduce_dtype == "bf16":
                 self._native.allreduce_bf16(view.data_ptr(), self._scratch[b.start:b.end].data_ptr(), b.numel, stream)
             else:
@@ -177,6 +222,14 @@ class GradReducer:
             if not b.launched:
                 self._launch(b)
         if self._native is not None:
+            if self.timing:
+                cur = torch.cuda.current_stream()
+                done_bwd = torch.cuda.Event(enable_timing=True)
+                done_bwd.record(cur)
+                done_comm = torch.cuda.Event(enable_timing=True)
+                done_comm.record(self._comm_stream())
+                self._tev.append((self._first_ev, done_bwd, done_comm))
+                self._first_ev = None
             self._native.wait(torch.cuda.current_stream().cuda_stream)
         else:
             scale = None if dist.get_backend(self.group) == "nccl" else 1.0 / self.world
@@ -186,6 +239,40 @@ class GradReducer:
                     if scale is not None:
                         self.store.grad[b.start:b.end].mul_(scale)
         self.active = False
+
+    _PROBE_PARTS = 256
+
+    def _comm_stream(self):
+        st = getattr(self, "_ext_stream", None)
+        if st is None:
+            st = self._ext_stream = torch.cuda.ExternalStream(self._native.comm_stream, device=self.store.device)
+        return st
+
+    def pop_timings(self) -> Dict[str, float]:
+        """Mean comm span and exposed comm wait (ms) over the steps since the last call (synchronises)."""
+        if not self._tev:
+            return {}
+        torch.cuda.synchronize(self.store.device)
+        span = [f.elapsed_time(c) for f, _, c in self._tev if f is not None]
+        exposed = [max(0.0, b.elapsed_time(c)) for _, b, c in self._tev]
+        self._tev.clear()
+        out = {"comm_wait_ms": sum(exposed) / len(exposed)}
+        if span:
+            out["comm_span_ms"] = sum(span) / len(span)
+        return out
+
+    def check_order(self) -> Dict[int, float]:
+        """After a synchronised step with ``verify``: {bucket: max |probe − final| / max|final|} — all zeros
+        when the comm stream read each bucket only after every kernel writing it had finished (only valid
+        while the all-reduce leaves the data unchanged, i.e. a forced world-1 fp32 reducer)."""
+        out = {}
+        for i, part in self._probes.items():
+            b = self.buckets[i]
+            ref = kernels().sq_norm_partials(self.store.grad[b.start:b.end], self._PROBE_PARTS)
+            torch.cuda.synchronize(self.store.device)
+            den = float(ref.abs().max()) or 1.0
+            out[i] = float((part - ref).abs().max()) / den
+        return out
 
     def verify_sequence(self):
         """Collective-sequence checker: every rank must have issued the same bucket all-reduces in the

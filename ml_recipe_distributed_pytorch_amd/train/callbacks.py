@@ -32,6 +32,10 @@ class TestCallback:
     def _reset(self):
         pass
 
+    def merge_across_ranks(self):
+        """Sharded evaluation: make this rank's state cover every rank's shard (collective; every rank
+        calls it before ``at_epoch_end``).  Stateless callbacks have nothing to merge."""
+
 
 def _acc(true, pred):
     return float((true == pred).float().mean().item())
@@ -74,6 +78,10 @@ class MAPCallback(TestCallback):
 
     def _reset(self):
         self.map_meter = MAPMeter()
+
+    def merge_across_ranks(self):
+        from ..parallel import dist as hqdist
+        self.map_meter.merge_states(hqdist.all_gather_object(self.map_meter.state()))
 
 
 class SaveBestCallback(TestCallback):

@@ -62,11 +62,14 @@ def max_micro_batch(cfg, seq_len: int, hbm_bytes: float, headroom: float = 0.9) 
 
 
 def plan_batch_split(cfg, seq_len: int, train_batch_size: int, hbm_bytes: float, requested: int = 1,
-                     headroom: float = 0.9) -> int:
-    """Smallest accumulation split >= ``requested`` that divides ``train_batch_size`` and whose micro-batch
-    fits the memory model (the reference's ``--batch_split`` semantics: micro = train_batch_size // split)."""
+                     headroom: float = 0.9, merge: bool = True) -> int:
+    """Smallest accumulation split that divides ``train_batch_size`` and whose micro-batch fits the memory
+    model (the reference's ``--batch_split`` semantics: micro = train_batch_size // split).  ``merge=True``
+    may go BELOW ``requested`` (the reference config's 128 micro-batches of 2, sized for a 12 GB K80,
+    become one micro-batch of 256 on a 288 GB MI355X); ``merge=False`` only ever raises it."""
     cap = max_micro_batch(cfg, seq_len, hbm_bytes, headroom)
-    for split in range(max(1, requested), train_batch_size + 1):
+    lo = 1 if merge else max(1, requested)
+    for split in range(lo, train_batch_size + 1):
         if train_batch_size % split == 0 and train_batch_size // split <= max(cap, 1):
             return split
     return train_batch_size

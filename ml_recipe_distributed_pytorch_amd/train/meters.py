@@ -20,6 +20,22 @@ class AverageMeter:
         self._counter += 1
         self._avg_value += (float(value) - self._avg_value) / self._counter
 
+    @property
+    def count(self) -> int:
+        return self._counter
+
+    @property
+    def sum(self) -> float:
+        return self._avg_value * self._counter
+
+    @classmethod
+    def from_sum_count(cls, total: float, count: int) -> "AverageMeter":
+        """A meter whose mean is ``total / count`` (merging per-rank meters of a sharded evaluation)."""
+        m = cls()
+        m._counter = int(count)
+        m._avg_value = float(total) / count if count else 0.0
+        return m
+
 
 class APMeter:
     """Average precision of one binary target (sklearn ``average_precision_score``)."""
@@ -42,6 +58,10 @@ class APMeter:
         self.pred_probas = []
         self.true_labels = []
 
+    def extend(self, other: "APMeter"):
+        self.pred_probas.extend(other.pred_probas)
+        self.true_labels.extend(other.true_labels)
+
 
 class MAPMeter:
     """Per-class AP dict plus their mean under ``'map'``."""
@@ -62,3 +82,15 @@ class MAPMeter:
 
     def reset(self):
         self.aps_dict = defaultdict(APMeter)
+
+    def state(self):
+        """Plain lists (picklable) of every class' predictions and targets."""
+        return {k: (list(v.pred_probas), list(v.true_labels)) for k, v in self.aps_dict.items()}
+
+    def merge_states(self, states):
+        """Rebuild from the ``state()`` of every shard, in rank order (the union of the shards)."""
+        self.reset()
+        for st in states:
+            for k, (p, t) in st.items():
+                self.aps_dict[k].pred_probas.extend(p)
+                self.aps_dict[k].true_labels.extend(t)

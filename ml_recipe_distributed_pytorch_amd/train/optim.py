@@ -226,13 +226,10 @@ def linear_schedule_with_warmup(num_warmup_steps: int, num_training_steps: int):
     return fn
 
 
-class _LinearWarmup:
-    def __init__(self, w, t):
-        self.w, self.t = w, t
-
-    def __call__(self, step):
-        return linear_schedule_with_warmup(self.w, self.t)(step)
-
-
 def get_linear_schedule_with_warmup(optimizer, num_warmup_steps: int, num_training_steps: int, last_epoch: int = -1):
-    return torch.optim.lr_scheduler.LambdaLR(optimizer, _LinearWarmup(num_warmup_steps, num_training_steps), last_epoch)
+    """The multiplier is a plain closure on purpose: ``LambdaLR.state_dict`` serialises the ``__dict__`` of
+    callable *objects* and ``load_state_dict`` writes it back, so a resumed run with more epochs would
+    inherit the old (warmup, total) and train at LR 0.  Functions are not serialised, so a resume keeps
+    the current run's schedule (as with transformers' lambda in the reference)."""
+    return torch.optim.lr_scheduler.LambdaLR(optimizer, linear_schedule_with_warmup(num_warmup_steps, num_training_steps),
+                                             last_epoch)

@@ -10,7 +10,9 @@ differences:
   ranks with ``eval_shard``;
 * ``DistributedSampler.set_epoch`` is called every epoch (D6);
 * checkpoints save under ``'apex'`` never, load tolerates ``'apex'``/``'amp'`` (D7) and also
-  store/restore ``epoch`` (resume continues at the next epoch);
+  store/restore ``epoch`` + ``epoch_complete``: resuming an end-of-epoch checkpoint continues at the
+  next epoch; resuming ``interrupt.ch`` (written mid-epoch) re-enters the interrupted epoch and skips
+  the micro-batches that epoch had already consumed (same sampler permutation under a fixed seed);
 * apex levels map to native bf16 mixed precision (O0 → fp32 compute);
 * per-step losses stay on device; one device→host sync per ``log_every`` optimizer steps (D14);
 * ``perf/samples_per_sec`` and ``perf/step_ms`` TensorBoard scalars.
@@ -73,6 +75,20 @@ def _fault_hook(rank: int, step: int):
         raise RuntimeError(f"injected fault at step {step}")
 
 
+class EvalShardSampler(torch.utils.data.Sampler):
+    """Rank ``r`` of ``w`` evaluates indices ``r, r + w, …`` — no padding duplicates (unlike
+    ``DistributedSampler``), so the union of the shards is exactly the test set."""
+
+    def __init__(self, n: int, rank: int, world: int):
+        self.idx = list(range(rank, n, world))
+
+    def __iter__(self):
+        return iter(self.idx)
+
+    def __len__(self):
+        return len(self.idx)
+
+
 @dataclass
 class Trainer:
     model: Any
@@ -128,7 +144,7 @@ class Trainer:
                                                       sampler=self.train_sampler, drop_last=True)
         test_sampler = None
         if self.test_dataset is not None and self.eval_shard and self.world > 1:
-            test_sampler = DistributedSampler(self.test_dataset, shuffle=False)
+            test_sampler = EvalShardSampler(len(self.test_dataset), self.rank, self.world)
         self.test_dataloader = self._init_dataloader(self.test_dataset, "Test", batch_size=self.test_batch_size,
                                                      sampler=test_sampler, drop_last=False)
         self.scheduler = None
@@ -151,6 +167,8 @@ class Trainer:
                                       profile=self.profile)
         self.global_step = 0
         self.start_epoch = 1
+        self.epoch_complete = True
+        self._resume_skip = 0  # micro-batches of the resumed (interrupted) epoch already consumed
         self.writer = self._init_writer(self.local_rank, self.writer_dir) if self.rank == 0 else None
         if self.debug:
             self.n_epochs = 2  # after the scheduler was built, as the reference (D8)
@@ -223,7 +241,9 @@ class Trainer:
         after_epoch_funcs = after_epoch_funcs or []
         for epoch_i in range(self.start_epoch, self.n_epochs + 1):
             self.epoch = epoch_i
+            self.epoch_complete = False
             self._train(epoch_i)
+            self.epoch_complete = True
             if self.reducer is not None:
                 self.reducer.verify_sequence()
             for func in after_epoch_funcs:
@@ -240,7 +260,18 @@ class Trainer:
         avg = {}
         last_t, last_step = time.perf_counter(), self.global_step
         samples_per_step = self.train_batch_size * self.world
-        data = tqdm(self.train_dataloader, desc=f"Train (epoch #{epoch_i} / {self.n_epochs})",
+        loader, skip = self.train_dataloader, self._resume_skip
+        self._resume_skip = 0
+        if skip:
+            # re-enter an interrupted epoch: drop the samples it had consumed (whole optimizer steps)
+            micro_bs = int(self.train_batch_size // self.batch_split)
+            rest = list(iter(self.train_sampler))[skip * micro_bs:]
+            logger.info(f"Resuming epoch {epoch_i} after {skip} consumed micro-batches ({len(rest)} samples left).")
+            loader = DataLoader(self.train_dataset, batch_size=micro_bs, num_workers=self.n_jobs, sampler=rest,
+                                drop_last=True, shuffle=False, collate_fn=self.collate_fun,
+                                pin_memory=self.device.type == "cuda")
+        self._epoch_start_step = self.global_step - skip // max(1, self.batch_split)
+        data = tqdm(loader, desc=f"Train (epoch #{epoch_i} / {self.n_epochs})",
                     disable=self.rank != 0 or not logger.isEnabledFor(logging.INFO))
         for i, (inputs, labels) in enumerate(data):
             inputs, labels = self._to_device((inputs, labels))
@@ -337,12 +368,7 @@ class Trainer:
                 logger.info("Test was interrupted because of debug mode.")
                 break
         if self.eval_shard and self.world > 1:
-            keys = sorted(avg_meters)
-            vals = hqdist.all_reduce_mean_floats([avg_meters[k]() for k in keys])
-            for k, v in zip(keys, vals):
-                m = AverageMeter()
-                m.update(v)
-                avg_meters[k] = m
+            self._merge_eval_shards(avg_meters, callbacks or [])
         for cb in callbacks or []:
             cb.at_epoch_end(avg_meters, self)
         self._update_writer(avg_meters, prefix="test")
@@ -350,6 +376,20 @@ class Trainer:
         logger.info(f"Test metrics after epoch {epoch_i} - {self._console_str(metrics)}")
         self.last_metrics = metrics
         self.set_train()
+
+    @staticmethod
+    def _merge_eval_shards(avg_meters, callbacks):
+        """Collective: every rank ends with the meters of the whole test set.  Keys are the union over
+        ranks (a shard may lack e.g. ``s_acc`` when none of its spans is valid), reduced as fixed-order
+        (sum, count) pairs; callbacks merge their own state (MAP: gathered predictions)."""
+        keys = sorted(set().union(*hqdist.all_gather_object(sorted(avg_meters))))
+        local = [avg_meters[k] if k in avg_meters else AverageMeter() for k in keys]
+        red = hqdist.all_reduce_sum_floats([m.sum for m in local] + [float(m.count) for m in local])
+        n = len(keys)
+        for i, k in enumerate(keys):
+            avg_meters[k] = AverageMeter.from_sum_count(red[i], int(red[n + i]))
+        for cb in callbacks:
+            cb.merge_across_ranks()
 
     # ------------------------------------------------------------------ checkpoints
     def _unwrapped(self):
@@ -361,6 +401,8 @@ class Trainer:
                 "scheduler": self.scheduler.state_dict() if self.scheduler is not None else None,
                 "global_step": self.global_step,
                 "epoch": getattr(self, "epoch", 0),
+                "epoch_complete": bool(self.epoch_complete),
+                "epoch_start_step": int(getattr(self, "_epoch_start_step", self.global_step)),
                 **self.extra_state}
 
     def save_state_dict(self, path_):
@@ -382,13 +424,24 @@ class Trainer:
         self._unwrapped().load_state_dict(state["model"])
         self.global_step = int(state.get("global_step", 0))
         if "epoch" in state and state["epoch"]:
-            self.start_epoch = int(state["epoch"]) + 1
+            if state.get("epoch_complete", True):
+                self.start_epoch = int(state["epoch"]) + 1
+            else:  # interrupt.ch: finish the interrupted epoch instead of skipping its remainder
+                self.start_epoch = int(state["epoch"])
+                done = self.global_step - int(state.get("epoch_start_step", self.global_step))
+                self._resume_skip = max(0, done) * self.batch_split
         logger.info(f"Model weights were loaded from {path_} checkpoint.")
         if not self.drop_optimizer:
             if self.optimizer is not None and state.get("optimizer") is not None:
                 self.optimizer.load_state_dict(state["optimizer"])
             if self.scheduler is not None and state.get("scheduler") is not None:
                 self.scheduler.load_state_dict(state["scheduler"])
+                # the restored optimizer carries the OLD run's last LR: re-evaluate this run's schedule at
+                # the restored step so the first resumed step already follows it
+                sch = self.scheduler
+                for g, base, fn in zip(self.optimizer.param_groups, sch.base_lrs, sch.lr_lambdas):
+                    g["lr"] = base * fn(sch.last_epoch)
+                sch._last_lr = [g["lr"] for g in self.optimizer.param_groups]
             if "apex" in state or "amp" in state:
                 logger.info("Checkpoint carries apex AMP state; native bf16 mixed precision needs none (ignored).")
             logger.info(f"Optimizer and scheduler also were restored from {path_} checkpoint.")

@@ -169,9 +169,12 @@ def get_trainer_parser() -> ArgumentParser:
     parser.add_argument("--no_sync_accum", type=cast2(int), default=1,
                         help="1: all-reduce only at the accumulation boundary (fix of D1); 0: every micro-batch.")
     parser.add_argument("--dist_timeout", type=float, default=1800.0, help="Process-group timeout in seconds.")
-    parser.add_argument("--auto_batch_split", action="store_true",
-                        help="GPU: raise --batch_split only as far as the HBM memory model (train/memory.py) needs "
-                             "for train_batch_size // batch_split to fit (288 GB MI355X: usually 1).")
+    parser.add_argument("--auto_batch_split", type=_opt_bool, default=None, nargs="?", const=True,
+                        help="GPU only (default on; False disables): pick the smallest --batch_split whose micro-batch "
+                             "train_batch_size // batch_split fits the HBM memory model (train/memory.py) — merges the "
+                             "reference's 128 micro-batches of 2 into one of 256 on a 288 GB MI355X, or raises the "
+                             "split when a micro-batch would not fit.  The per-step gradient is the same mean over "
+                             "train_batch_size samples (up to the per-micro-batch CE normalisation over valid spans).")
     parser.add_argument("--profile", action="store_true", help="Per-phase step timers + perf/* TB scalars.")
     parser.add_argument("--torch_profile_dir", type=cast2(str), default=None,
                         help="Export a torch.profiler Chrome trace of optimizer steps --torch_profile_steps here.")
@@ -185,6 +188,20 @@ def get_trainer_parser() -> ArgumentParser:
     parser.add_argument("--nproc_per_node", type=cast2(int), default=None,
                         help="Processes per node (default: #visible GPUs, or 1 on CPU). On CPU >1 spawns gloo ranks.")
     return parser
+
+
+def _opt_bool(v):
+    """Tri-state flag value: None (unset → per-device default), True or False (cfg ``key = True``)."""
+    if v is None or isinstance(v, bool):
+        return v
+    t = str(v).strip().lower()
+    if t in ("none", ""):
+        return None
+    if t in ("1", "true", "yes", "on"):
+        return True
+    if t in ("0", "false", "no", "off"):
+        return False
+    raise ValueError(f"expected True/False/None, got {v!r}")
 
 
 def get_predictor_parser() -> ArgumentParser:

@@ -16,6 +16,7 @@ TINY = VTINY + ["--test_batch_size", "8"]
 
 
 def _cfg(tmp_path, **over):
+    over.setdefault("batch_split", "1")  # the shipped cfg keeps the reference's 128 (micro-batch 2 of 256)
     text = open(BASE).read()
     lines = []
     for line in text.splitlines():
@@ -65,13 +66,23 @@ def test_train_resume_and_interrupt(tmp_path, monkeypatch):
     _train(["-c", cfg2, "--dump_dir", str(tmp_path), "--last", str(exp / "last.ch")] + TINY)
     st2 = torch.load(exp / "last.ch", weights_only=True)
     assert st2["global_step"] == 8 and st2["epoch"] == 2 and (exp / "epoch_2.ch").exists()
+    # the resumed epoch follows the NEW run's schedule (8 steps, warmup 4): the LR never collapses to 0
+    from ml_recipe_distributed_pytorch_amd.utils.tb import read_events
+    ev = list((tmp_path / "board" / "exp").glob("events.out.tfevents.*"))
+    lrs = {step: v for step, t, v in read_events(str(ev[0])) if t == "train/lr"}
+    assert sorted(lrs) == [5, 6, 7, 8] and all(v > 0 for s_, v in lrs.items() if s_ < 8), lrs
     # fault injection: KeyboardInterrupt at step 3 → interrupt.ch holds step 3
     monkeypatch.setenv("HQ_FAULT", "0:3:interrupt")
     cfg3 = _cfg(tmp_path, debug="False", n_epochs="1", train_batch_size="8", batch_split="1",
                 dummy_dataset_len="32", experiment_name="exp3")
     _train(["-c", cfg3, "--dump_dir", str(tmp_path)] + TINY)
     st3 = torch.load(tmp_path / "exp3" / "interrupt.ch", weights_only=True)
-    assert st3["global_step"] == 3
+    assert st3["global_step"] == 3 and st3["epoch"] == 1 and st3["epoch_complete"] is False
+    # resuming interrupt.ch finishes the interrupted epoch (1 step left) instead of skipping it
+    monkeypatch.delenv("HQ_FAULT")
+    _train(["-c", cfg3, "--dump_dir", str(tmp_path), "--last", str(tmp_path / "exp3" / "interrupt.ch")] + TINY)
+    st4 = torch.load(tmp_path / "exp3" / "last.ch", weights_only=True)
+    assert st4["global_step"] == 4 and st4["epoch"] == 1 and st4["epoch_complete"] is True
 
 
 def test_profiling_outputs(tmp_path):
@@ -152,3 +163,21 @@ def test_launch_plan_arithmetic(monkeypatch):
     plan = make_plan(p)
     assert plan.env and not plan.spawn and plan.world_size == 4 and plan.global_rank(0) == 3  # D4
     assert clamp_jobs(16, 64) == 1  # D20: never 0 workers
+
+
+def test_reference_config_verbatim_runs(tmp_path):
+    """Drop-in contract: the UNMODIFIED reference test_bert.cfg (tests/fixtures, verbatim) runs through the
+    reference launch shim ``modules/train.py --local_rank 0`` with batch_split = 128 semantics (micro-batches
+    of 2; on CPU auto_batch_split stays off) — only the model size / sequence length are overridden."""
+    cfg = os.path.join(ROOT, "tests", "fixtures", "reference_test_bert.cfg")
+    cmd = [sys.executable, os.path.join(ROOT, "modules", "train.py"), "-c", cfg, "--dump_dir", str(tmp_path),
+           "--local_rank", "0"] + VTINY
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    log = open(next((tmp_path / "test").glob("*.log"))).read()
+    # 2 epochs x 10000 samples / micro-batch 2 // batch_split 128 = 78 optimizer steps
+    assert "#Training steps: 78." in log and "auto_batch_split: batch_split" not in log
+    from ml_recipe_distributed_pytorch_amd.utils.tb import read_events
+    ev = list((tmp_path / "board" / "test").glob("events.out.tfevents.*"))
+    steps = sorted({s for s, t, _ in read_events(str(ev[0])) if t == "train/loss"})
+    assert steps == [1, 2]  # debug: one optimizer step per epoch, two epochs

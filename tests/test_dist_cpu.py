@@ -130,3 +130,51 @@ def test_collective_sequence_checker_detects_divergence(tmp_path):
     for r in range(2):
         first, second = torch.load(tmp_path / f"seq{r}.pt", weights_only=True).tolist()
         assert first and not second
+
+
+def _eval_items(n=9, L=32):
+    """Per-sample (inputs, labels) with mixed classes and some ignored (-1) span targets."""
+    inputs, labels = _batch(B=n, L=L, seed=7)
+    labels["start_class"][::3] = -1
+    labels["end_class"] = torch.randint(0, L, (n,), generator=torch.Generator().manual_seed(5))
+    labels["end_class"][1::4] = -1
+    return [({k: v[i] for k, v in inputs.items()}, {k: v[i] for k, v in labels.items()}) for i in range(n)]
+
+
+def _stack(items):
+    return ({k: torch.stack([it[0][k] for it in items]) for k in items[0][0]},
+            {k: torch.stack([it[1][k] for it in items]) for k in items[0][1]})
+
+
+def _eval_metrics(eval_shard):
+    from ml_recipe_distributed_pytorch_amd.data.items import LABELS
+    from ml_recipe_distributed_pytorch_amd.train.callbacks import AccuracyCallback, MAPCallback
+    from ml_recipe_distributed_pytorch_amd.train.trainer import Trainer
+    model, loss, _ = _build(seed=3)
+    tr = Trainer(model=model, loss=loss, collate_fun=_stack, test_dataset=_eval_items(), test_batch_size=1,
+                 n_jobs=0, eval_shard=eval_shard)
+    tr.test(1, callbacks=[MAPCallback(LABELS), AccuracyCallback()])
+    return tr.last_metrics
+
+
+def _eval_worker(rank, world, port, out_dir):
+    _setup(rank, world, port)
+    from ml_recipe_distributed_pytorch_amd.parallel import dist as hqdist
+    m = _eval_metrics(eval_shard=True)
+    torch.save(m, os.path.join(out_dir, f"eval{rank}.pt"))
+    hqdist.destroy()
+
+
+def test_sharded_eval_matches_unsharded(tmp_path):
+    """eval_shard over 2 gloo ranks (uneven 5/4 split, a shard without some keys) gives every rank the
+    metrics of the single-process evaluation: merged (sum, count) meters and MAP over gathered predictions."""
+    mp.spawn(_eval_worker, args=(2, free_port(), str(tmp_path)), nprocs=2, join=True)
+    ref = _eval_metrics(eval_shard=False)
+    for r in range(2):
+        got = torch.load(tmp_path / f"eval{r}.pt", weights_only=True)
+        assert set(got) == set(ref)
+        for k, v in ref.items():
+            if v != v:
+                assert got[k] != got[k], k
+            else:
+                assert abs(got[k] - v) < 1e-9 * max(1.0, abs(v)), (k, got[k], v)

@@ -32,7 +32,8 @@ def test_plan_batch_split():
     split = plan_batch_split(cfg, 384, 256, 12 * 2**30)
     assert split > 1 and 256 % split == 0
     assert estimate(cfg, 384).total(256 // split) <= 0.9 * 12 * 2**30
-    assert plan_batch_split(cfg, 384, 256, 288 * 2**30, requested=4) == 4   # never below the requested split
+    assert plan_batch_split(cfg, 384, 256, 288 * 2**30, requested=4, merge=False) == 4  # raise-only mode
+    assert plan_batch_split(cfg, 512, 256, 288 * 2**30, requested=128) == 1  # reference cfg: 128 × 2 → 1 × 256
 
 
 def test_auto_batch_split_flag_parses():

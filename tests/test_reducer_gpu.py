@@ -1,0 +1,85 @@
+"""The native RCCL gradient reducer inside a real BERT-base training step, on one GPU.
+
+With ``force=True`` the reducer keeps a 1-rank RCCL communicator active, so every bucket of the backward
+goes through the multi-GPU path (arena slice → fence → ncclAllReduce(avg) on the high-priority comm stream
+→ compute-stream wait) — the 8-GPU code path minus the peers.  Averaging over one rank is the identity,
+so the weights after each step must be BITWISE equal to a run without a reducer; and with the
+weight-gradient GEMMs on a side stream (``HQ_WGRAD_STREAM=1``) the comm-stream checksums taken where the
+all-reduce reads each bucket must equal the final gradients (stream-ordering test)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(dev, reducer_kw=None, seed=11):
+    from types import SimpleNamespace
+    from ml_recipe_distributed_pytorch_amd.models.bert import BertForQuestionAnswering
+    from ml_recipe_distributed_pytorch_amd.models.config import get_config
+    from ml_recipe_distributed_pytorch_amd.models.losses import build_loss
+    from ml_recipe_distributed_pytorch_amd.parallel.reducer import GradReducer
+    from ml_recipe_distributed_pytorch_amd.train.engine import TrainEngine
+    from ml_recipe_distributed_pytorch_amd.train.optim import FusedAdamW
+    from ml_recipe_distributed_pytorch_amd.train.trainer import optimizer_groups
+    model = BertForQuestionAnswering(get_config("bert-base-uncased"), seed=seed).to(dev).train()
+    lp = SimpleNamespace(loss="smooth", smooth_alpha=0.01, focal_alpha=1, focal_gamma=2, w_start=1, w_end=1,
+                         w_start_reg=1, w_end_reg=1, w_cls=1)
+    opt = FusedAdamW(optimizer_groups(model.named_parameters(), 1e-4), model.store, lr=1e-4, eps=1e-6,
+                     correct_bias=False, zero_grad_fn=model.zero_grad)
+    red = GradReducer(model, force=True, **reducer_kw) if reducer_kw is not None else None
+    return model, red, TrainEngine(model, build_loss(lp), opt, reducer=red, max_grad_norm=1.0)
+
+
+def _batches(dev, n=2, B=8, L=128):
+    from ml_recipe_distributed_pytorch_amd.data.dummy import SpecialIds, synth_batch_native
+    from ml_recipe_distributed_pytorch_amd.train.engine import to_device
+    out = []
+    for i in range(n):
+        inputs, labels = synth_batch_native(B, L, 32, SpecialIds(), seed=100 + i)
+        out.append((to_device(inputs, dev), to_device(labels, dev)))
+    return out
+
+
+def _run(dev, reducer_kw, batches):
+    model, red, eng = _engine(dev, reducer_kw)
+    checks = []
+    for b in batches:
+        eng.step([b])
+        torch.cuda.synchronize()
+        if red is not None and red.verify:
+            checks.append(red.check_order())
+    master = model.store.master.clone()
+    kind, nb = (red.kind, red.n_buckets) if red is not None else ("none", 0)
+    if red is not None:
+        red.close()
+    return master, kind, nb, checks
+
+
+@pytest.mark.parametrize("bucket_mb", [32.0, 4.0])
+def test_forced_native_reducer_bitwise_equals_no_reducer(cuda, bucket_mb):
+    batches = _batches(cuda)
+    ref, _, _, _ = _run(cuda, None, batches)
+    got, kind, nb, _ = _run(cuda, dict(bucket_cap_mb=bucket_mb), batches)
+    assert kind == "native-rccl" and nb >= (3 if bucket_mb == 32.0 else 10)
+    assert torch.equal(got, ref), f"max diff {(got - ref).abs().max().item():.3e}"
+
+
+def test_reducer_stream_ordering_with_wgrad_side_stream(cuda, monkeypatch):
+    monkeypatch.setenv("HQ_WGRAD_STREAM", "1")
+    batches = _batches(cuda)
+    ref, _, _, _ = _run(cuda, None, batches)
+    got, kind, nb, checks = _run(cuda, dict(bucket_cap_mb=4.0, verify=True), batches)
+    assert kind == "native-rccl" and checks and all(len(c) == nb for c in checks)
+    for step, c in enumerate(checks):
+        bad = {i: v for i, v in c.items() if v != 0.0}
+        assert not bad, f"step {step}: comm stream read buckets {sorted(bad)} before their gradients were final"
+    assert torch.equal(got, ref)
+
+
+def test_reducer_timing_reports_comm_wait(cuda):
+    model, red, eng = _engine(cuda, dict(bucket_cap_mb=32.0, timing=True))
+    for b in _batches(cuda, n=3):
+        eng.step([b])
+    t = red.pop_timings()
+    red.close()
+    assert t["comm_wait_ms"] >= 0.0 and t["comm_span_ms"] > 0.0
