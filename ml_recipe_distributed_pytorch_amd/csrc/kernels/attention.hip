@@ -377,6 +377,337 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
   }
 }
 
+// ============================================================================ forward v3: LDS-DMA ring
+// The whole-head design above keeps K and V of a head resident (96 KB at L=384), so only ONE workgroup
+// fits a CU and its load prologue and store epilogue never overlap compute: measured 151 of 285 µs at
+// B=256 (profiles/s3_prof/attn_lab.txt).  v3 instead:
+// * a workgroup is 4 waves × 32 queries of one head; the head's K and V stream through an RNS-slot LDS
+//   ring of 32-key tiles by LDS-DMA (global_load_lds, 1 KiB per wave-instruction, source-swizzled so the
+//   lane-linear image is the conflict-free lds_off layout), RAHEAD tiles ahead of the consumer, with a
+//   COUNTED vmcnt + raw s_barrier per tile — three workgroups per CU, so one's loads overlap the others'
+//   MFMAs;
+// * blockIdx is remapped so the query blocks of one head are consecutive on ONE XCD (they run together
+//   and read K/V through the same L2);
+// * the key-mask bias and the running row max ride in a 5th MFMA per tile: K' = [K | b_hi, b_lo, 1, 0…]
+//   and Q' = [Q·c | 1, 1, −m, 0…] (bf16; b_hi + b_lo = bias·log2e to ~16 bits, m kept bf16-exact), so
+//   S' = c·QKᵀ + bias − m leaves the MFMA ready for exp2 — no accumulator init, no subtraction in VALU;
+// * no per-tile max and no rescale: m is the first tile's row max (a lower bound of the row max, so
+//   P ≤ 2^(rowmax − m) and l ≥ 1); bf16/fp32 relative precision does not depend on magnitude, and a
+//   workgroup with a row whose l exceeds 2^64 recomputes its rows on an in-kernel slow path (per-tile max
+//   + rescale, per-wave LDS staging) after the fast loop.  LSE = m + log2 l.
+constexpr int RW = 4;                    // waves per workgroup
+constexpr int RQ = RW * 32;              // queries per workgroup
+// ring slots: RAHEAD + 2 (tiles kt … kt+RAHEAD in flight plus one being drained); the Q staging block of
+// the prologue aliases slots RAHEAD, RAHEAD+1, which are first restaged after the first barrier
+constexpr int RTILE = 32 * D * 2;        // bytes of one 32-key tile of K (or V)
+typedef __attribute__((address_space(1))) void ag_void;
+typedef __attribute__((address_space(3))) void al_void;
+
+__device__ __forceinline__ uint16_t bf16_rne(float f) { return (uint16_t)(hq_pack2(f, 0.f) & 0xFFFFu); }
+// the key bias (log2 domain) exactly as the forward's 5th MFMA adds it: bf16 hi + bf16 lo
+__device__ __forceinline__ float bias_l2(float kb) {
+  const float x = kb * LOG2E;
+  const float hi = hq_bf2f(bf16_rne(x));
+  return hi + hq_bf2f(bf16_rne(x - hi));
+}
+
+// LDS-DMA of 8 rows × 128 B (rows row0..row0+7 of `src`, ld elements apart) into a lane-linear
+// [rows][64] image at `dst` (wave-uniform); the source chunk is pre-swizzled so the image is lds_off().
+// Inline asm on purpose (cdna_hip_programming.md §5.7): with the builtin, hipcc treats the DMA as a
+// pending LDS write and drains it (vmcnt(0)) before every later ds_read_b64_tr_b16 — which would wait
+// for the tiles being prefetched.  Completion is counted by hand (vmcnt(N) + barrier per tile).
+__device__ __forceinline__ void dma_piece(const uint16_t* g, char* dst) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(al_void*)dst);
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(lds)
+      : "memory");
+}
+// element offset of this lane's 16 B inside an 8-row piece starting at image row row0 (source-swizzled)
+__device__ __forceinline__ int dma_lane_off(int row0, size_t ld, int lane) {
+  const int r = row0 + (lane >> 3);
+  return (lane >> 3) * (int)ld + (((lane & 7) ^ swz(r)) << 3);
+}
+__device__ __forceinline__ void dma_rows8(const uint16_t* src, size_t ld, int row0, int rows_valid, char* dst,
+                                          int lane) {
+  const int r = row0 + (lane >> 3);
+  const int rs = r < rows_valid ? r : rows_valid - 1;   // clamp: padded keys are masked by bias = -inf
+  dma_piece(src + (size_t)rs * ld + (((lane & 7) ^ swz(r)) << 3), dst + row0 * 128);
+}
+
+// `vmcnt(n)` with a value that constant-folds once the tile loop is unrolled
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+  }
+}
+
+template <bool DROP, bool EVEN, int NT, int RAHEAD>
+__global__ __launch_bounds__(RW * 64, DROP ? 3 : 4) void attn_fwd_ring_kernel(const uint16_t* __restrict__ qkv,
+                                                                   const float* __restrict__ key_bias,
+                                                                   uint16_t* __restrict__ ctx, float* __restrict__ lse,
+                                                                   uint16_t* __restrict__ mbits, int L, int nh,
+                                                                   int n_qb, float c_scale, uint32_t key,
+                                                                   uint32_t thr, float kscale, int force_slow) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
+  constexpr int RNS = RAHEAD + 2;
+  static_assert(RAHEAD >= 1 && RAHEAD <= 4, "ring depth");
+  char* ring = reinterpret_cast<char*>(smem);                       // [RNS][K 4 KB | V 4 KB]
+  char* sQ = ring + RAHEAD * 2 * RTILE;                             // [RQ][64] bf16 = ring slots RAHEAD, +1
+  uint2* sA = reinterpret_cast<uint2*>(ring + RNS * 2 * RTILE);     // [2][Lp]: (pk(b_hi, b_lo), pk(1, 0)) | 0
+  // XCD-aware block order (bijective): blocks b, b+8, … share an XCD; give each XCD a contiguous run of
+  // (head, query-block) pairs with the query block fastest, so a head's blocks are co-resident on one L2
+  const int nblk = gridDim.x, ob = blockIdx.x, xcd = ob & 7, qq = nblk >> 3, rr = nblk & 7;
+  const int lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (ob >> 3);
+  const int bh = lin / n_qb, qb = lin - bh * n_qb;
+  const int b = bh / nh, h = bh - b * nh;
+  const int H = nh * D, ld = 3 * H;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, hh = lane >> 5;
+  const int qs = qb * RW + wave;                       // this wave's 32-query subtile (of the head)
+  const int qi = qs * 32 + (lane & 31);
+  const bool active = qs * 32 < L;                     // waves past L (last block) only help with DMA
+  const uint16_t* base = qkv + (size_t)b * L * ld + h * D;
+  HQ_DASSERT(L > 0 && L <= 512 && (NT == 0 || L == NT * 32) && bh < nblk / n_qb);
+
+  // ---- prologue: Q block (this wave's 8 row-pieces... 32 rows = 4 pieces) + the first RAHEAD tiles
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r0 = wave * 32 + p * 8;                  // row within the workgroup's 128 queries
+    const int rows = L - qb * RQ;                      // valid query rows of this block
+    dma_rows8(base + (size_t)qb * RQ * ld, ld, r0, rows > 0 ? rows : 1, sQ, lane);
+  }
+  const int kv_off = dma_lane_off(wave * 8, ld, lane) + wave * 8 * ld;
+  auto stage = [&](int kt) {                           // tile kt → slot kt % RNS: this wave's K and V piece
+    char* slot = ring + (kt % RNS) * 2 * RTILE;
+    const uint16_t* kb = base + H + (size_t)kt * 32 * ld;   // wave-uniform
+    if (EVEN || kt * 32 + 32 <= L) {
+      dma_piece(kb + kv_off, slot + wave * 8 * 128);
+      dma_piece(kb + H + kv_off, slot + RTILE + wave * 8 * 128);
+    } else {
+      dma_rows8(kb, ld, wave * 8, L - kt * 32, slot, lane);
+      dma_rows8(kb + H, ld, wave * 8, L - kt * 32, slot + RTILE, lane);
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < RAHEAD; ++t)
+    if (t < n32) stage(t);
+  for (int t = threadIdx.x; t < Lp; t += RW * 64) {
+    const float bl = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -INFINITY;
+    const uint16_t hi = bf16_rne(bl);
+    const uint16_t lo = t < L ? bf16_rne(bl - hq_bf2f(hi)) : 0;
+    sA[t] = make_uint2((uint32_t)hi | ((uint32_t)lo << 16), 0x3F80u);  // (b_hi, b_lo, 1.0, 0)
+    sA[Lp + t] = make_uint2(0u, 0u);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  LdsOffsets lo_;
+  lo_.init(lane);
+  bf16x8_t qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const bf16x8_t raw = *reinterpret_cast<const bf16x8_t*>(sQ + 2 * (wave * 32 * D + lo_.row[s]));
+    qf[s] = prescale8(raw, c_scale);
+  }
+  const uint2* aug_src = sA + hh * Lp + (lane & 31);     // hh = 1 lanes read zeros (k-dims 8..15)
+  float m_b = 0.f;                                        // bf16-exact running max (log2 domain)
+  const uint32_t qaug_w0 = hh ? 0u : 0x3F803F80u;         // (1, 1) against (b_hi, b_lo)
+  uint32_t qaug_w = 0u;                                   // (−m, 0) against (1, 0); −0 until the first tile
+  f32x16_t o[2];
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  f2_t l2 = {0.f, 0.f};
+  const uint32_t row_idx = ((uint32_t)bh * L + (uint32_t)min(qi, L - 1)) * (uint32_t)L;
+  uint16_t* my_bits = mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane;
+  const f32x16_t zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool stores = DROP && active;
+
+  // tile kt landed.  Iteration j issues stage(j + RAHEAD) (2 pieces, if it exists) then bits(j); tile kt
+  // was staged in iteration kt − RAHEAD, so younger than it are the RAHEAD bit stores of iterations
+  // kt − RAHEAD … kt − 1 and the stages of iterations kt − RAHEAD + 1 … kt − 1 that exist (prologue tiles
+  // kt < RAHEAD were drained before the loop: any count is safe for them)
+  auto wait_tile = [&](int kt, bool with_stores) {
+    const int later = kt + RAHEAD - 1 < n32 ? RAHEAD - 1 : n32 - 1 - kt;
+    wait_vm((with_stores ? RAHEAD : 0) + 2 * (later > 0 ? later : 0));
+  };
+  constexpr int UNR = NT > 0 ? NT : 1;
+  if (!active) {  // waves past L (last query block): their share of the DMA and every barrier, nothing else
+#pragma unroll UNR
+    for (int kt = 0; kt < n32; ++kt) {
+      wait_tile(kt, false);
+      __builtin_amdgcn_s_barrier();
+      if (kt + RAHEAD < n32) stage(kt + RAHEAD);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    (void)__syncthreads_or(0);                         // the workgroup's slow-path vote (below)
+    return;
+  }
+  // Branch-free tile loop: a per-tile rescale branch makes hipcc copy the 32 O registers across the join
+  // (43 v_mov_b64 per tile measured).  m stays the first tile's row max, so every P ≤ 2^(rowmax − m); a
+  // workgroup with a row whose l outgrew 2^64 redoes its rows on the slow path after the loop (never
+  // triggered by BERT activations; a left-padded row with a fully masked first tile is the realistic case).
+#pragma unroll UNR
+  for (int kt = 0; kt < n32; ++kt) {
+    wait_tile(kt, DROP);
+    __builtin_amdgcn_s_barrier();
+    if (kt + RAHEAD < n32) stage(kt + RAHEAD);         // its slot was last read two barriers ago
+    const char* sK = ring + (kt % RNS) * 2 * RTILE;
+    const uint16_t* tK = reinterpret_cast<const uint16_t*>(sK);
+    const uint16_t* tV = reinterpret_cast<const uint16_t*>(sK + RTILE);
+    bf16x8_t kf[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) kf[s] = row8(tK, 0, lo_, s);
+    const uint2 aw = aug_src[kt * 32];
+    typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+    const bf16x8_t ka = __builtin_bit_cast(bf16x8_t, u32x4{aw.x, aw.y, 0u, 0u});
+    const bf16x8_t qa = __builtin_bit_cast(bf16x8_t, u32x4{qaug_w0, qaug_w, 0u, 0u});
+    f32x16_t acc = mfma32(kf[0], qf[0], zero16);
+#pragma unroll
+    for (int s = 1; s < 4; ++s) acc = mfma32(kf[s], qf[s], acc);
+    acc = mfma32(ka, qa, acc);                          // + bias_k − m_q
+    float sc[16];
+    if (kt == 0) {                                      // first tile: the row max over the full tile
+      const float mx = xor32_max(max16(acc));
+      m_b = hq_bf2f(bf16_rne(mx == -INFINITY ? 0.f : mx));
+      qaug_w = hh ? 0u : (uint32_t)bf16_rne(-m_b);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[r] = __builtin_amdgcn_exp2f(acc[r] - m_b);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[r] = __builtin_amdgcn_exp2f(acc[r]);
+    }
+    {  // the softmax denominator counts every key (dropout only thins P·V); pairwise tree, not a chain
+      const f2_t a0 = f2_t{sc[0], sc[1]} + f2_t{sc[2], sc[3]}, a1 = f2_t{sc[4], sc[5]} + f2_t{sc[6], sc[7]};
+      const f2_t a2 = f2_t{sc[8], sc[9]} + f2_t{sc[10], sc[11]}, a3 = f2_t{sc[12], sc[13]} + f2_t{sc[14], sc[15]};
+      l2 += (a0 + a1) + (a2 + a3);
+    }
+    if constexpr (DROP) {
+      uint32_t bits = 0;
+      if constexpr (EVEN) {
+        const uint32_t pk = (((row_idx >> 1) + (uint32_t)kt * 16u) ^ key) ^ (2u * (uint32_t)hh);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+#pragma unroll
+          for (int ip = 0; ip < 2; ++ip) {
+            const uint32_t hsh = hq_mix24(pk ^ (uint32_t)(4 * g + ip));
+            const int r = 4 * g + 2 * ip;
+            const bool k0 = (hsh & 0xFFFFu) >= thr, k1 = (hsh >> 16) >= thr;
+            sc[r] = k0 ? sc[r] : 0.f;
+            sc[r + 1] = k1 ? sc[r + 1] : 0.f;
+            bits |= ((uint32_t)k0 << r) | ((uint32_t)k1 << (r + 1));
+          }
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t idx0 = row_idx + kt * 32 + 8 * g + 4 * hh;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bool k = hq_keep(idx0 + i, key, thr);
+            sc[4 * g + i] = k ? sc[4 * g + i] : 0.f;
+            bits |= (uint32_t)k << (4 * g + i);
+          }
+        }
+      }
+      my_bits[(size_t)kt * 64] = (uint16_t)bits;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8_t pb = pack_b(sc, s);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) o[d] = mfma32(tr8(tV, 0, lo_, s, d), pb, o[d]);
+    }
+  }
+  float l_tot = xor32_sum(l2.x + l2.y);
+  // slow-path vote: any row of the workgroup whose l left [1, 2^64) (P could have overflowed) — or every
+  // workgroup when force_slow (tests) — recomputes with a per-tile max and rescale.  The ring is idle now
+  // (every tile consumed; only bit stores may be in flight), so each wave stages K/V in a private 8 KB of it.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (__syncthreads_or(force_slow || (qi < L && !(l_tot < 0x1p64f)))) {
+    uint16_t* pK = reinterpret_cast<uint16_t*>(ring + wave * 2 * RTILE);
+    uint16_t* pV = pK + 32 * D;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+    l2 = f2_t{0.f, 0.f};
+    float m_run = -INFINITY;
+    const uint16_t* kbase = base + H;
+    for (int kt = 0; kt < n32; ++kt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {  // private staging: plain loads, ds_write; LDS is in order per wave
+        const int r = i * 8 + (lane >> 3), c = (lane & 7) * 8;
+        const int kr = min(kt * 32 + r, L - 1);
+        const uint4 kv = *reinterpret_cast<const uint4*>(kbase + (size_t)kr * ld + c);
+        const uint4 vv = *reinterpret_cast<const uint4*>(kbase + H + (size_t)kr * ld + c);
+        *reinterpret_cast<uint4*>(pK + lds_off(r, c)) = kv;
+        *reinterpret_cast<uint4*>(pV + lds_off(r, c)) = vv;
+      }
+      bf16x8_t kf[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) kf[s] = row8(pK, 0, lo_, s);
+      const uint2 aw = aug_src[kt * 32];
+      typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+      const bf16x8_t ka = __builtin_bit_cast(bf16x8_t, u32x4{aw.x, aw.y, 0u, 0u});
+      const bf16x8_t qa = __builtin_bit_cast(bf16x8_t, u32x4{qaug_w0, 0u, 0u, 0u});  // m = 0: exact scores
+      f32x16_t acc = mfma32(kf[0], qf[0], zero16);
+#pragma unroll
+      for (int s = 1; s < 4; ++s) acc = mfma32(kf[s], qf[s], acc);
+      acc = mfma32(ka, qa, acc);
+      const float m_new = fmaxf(m_run, xor32_max(max16(acc)));
+      const float ms = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = __builtin_amdgcn_exp2f(m_run - ms);
+      m_run = m_new;
+      l2 *= f2_t{alpha, alpha};
+#pragma unroll
+      for (int d = 0; d < 2; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[d][r] *= alpha;
+      float sc[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        sc[r] = __builtin_amdgcn_exp2f(acc[r] - ms);
+        l2.x += sc[r];
+      }
+      if constexpr (DROP) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint32_t idx0 = row_idx + kt * 32 + 8 * g + 4 * hh;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) sc[4 * g + i] = hq_keep(idx0 + i, key, thr) ? sc[4 * g + i] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8_t pb = pack_b(sc, s);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) o[d] = mfma32(tr8(pV, 0, lo_, s, d), pb, o[d]);
+      }
+    }
+    m_b = m_run == -INFINITY ? 0.f : m_run;
+    l_tot = xor32_sum(l2.x + l2.y);
+  }
+  const float inv = (DROP ? kscale : 1.f) / l_tot;
+  if (qi < L) {  // lanes q and q+32 share qi: the permlane partners are active together
+    store_row64(ctx + ((size_t)b * L + qi) * H + h * D, o, inv, hh);
+    if (hh == 0) lse[(size_t)bh * L + qi] = (m_b + __builtin_amdgcn_logf(l_tot)) * LN2;  // v_log_f32 = log2
+  }
+}
+
 // ============================================================================ backward: dQ (+ δ)
 template <int NWB, bool DROP, int NT>
 __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv,
@@ -430,7 +761,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* _
       if (t < n32 && qs < n32) mw[t] = gbits[(size_t)t * 64];
   }
   load_heads2<NWB * 64>(sK, base + H, ld, sV, base + 2 * H, ld, L, Lp);
-  for (int t = threadIdx.x; t < Lp; t += NWB * 64) sB[t] = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -INFINITY;
+  for (int t = threadIdx.x; t < Lp; t += NWB * 64) sB[t] = t < L ? bias_l2(key_bias[(size_t)b * L + t]) : -INFINITY;
   if constexpr (DROP) {
 #pragma unroll
     for (int t = 0; t < kMaxT; ++t)
@@ -526,7 +857,7 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
     kf[s] = kok ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)kj * ld + H + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
     vf[s] = kok ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)kj * ld + 2 * H + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
   }
-  const float kb = kok ? key_bias[(size_t)b * L + kj] * LOG2E : -INFINITY;
+  const float kb = kok ? bias_l2(key_bias[(size_t)b * L + kj]) : -INFINITY;
   constexpr int kMaxT = 16;
   uint16_t mw[kMaxT];
   if constexpr (DROP) {
@@ -716,6 +1047,16 @@ static void set_attn_prio() {
   (void)once;
 }
 
+static int attn_fwd_variant() {  // read per call: tools/attn_bench.py A/Bs the variants in one process
+  const char* e = getenv("HQ_ATTN_FWD");
+  return e ? atoi(e) : 3;
+}
+
+static int attn_force_slow() {  // tests: HQ_ATTN_FORCE_SLOW=1 sends every workgroup down the slow path
+  const char* e = getenv("HQ_ATTN_FORCE_SLOW");
+  return e && atoi(e) ? 1 : 0;
+}
+
 void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, float* lse, uint16_t* mbits, int B, int L,
                  int nh, int dh, float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s) {
   set_attn_prio();
@@ -723,6 +1064,41 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const uint32_t key = hq_op_key(seed, opid);
   const int Lp = (L + 31) & ~31, n32 = Lp / 32;
+  if (attn_fwd_variant() == 3) {
+    const int n_qb = (L + RQ - 1) / RQ;
+    const int force_slow = attn_force_slow();
+    const char* ea = getenv("HQ_ATTN_AHEAD");
+    const int ahead = ea ? atoi(ea) : 2;
+    const size_t lds = (size_t)(ahead == 2 ? 4 : 6) * 2 * RTILE + 2 * Lp * sizeof(uint2);
+    auto run = [&](auto cn) {
+      constexpr int NT = decltype(cn)::value;
+      auto launch1 = [&](auto kern) {
+        static bool attr =
+            (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess);
+        (void)attr;
+        hipLaunchKernelGGL(kern, dim3(B * nh * n_qb), dim3(RW * 64), lds, s, qkv, key_bias, ctx, lse,
+                           thr ? mbits : nullptr, L, nh, n_qb, scale * LOG2E, key, thr, hq_keep_scale(thr), force_slow);
+      };
+      auto launch = [&](auto k2, auto k4) { if (ahead == 2) launch1(k2); else launch1(k4); };
+      // EVEN (L % 32 == 0) also selects the unclamped DMA addressing: never pass it for a ragged L
+      // (NT > 0 implies L = 32·NT, so the ragged variants exist only for the rolled NT = 0 loop)
+      if constexpr (NT > 0) {
+        if (!thr) launch(attn_fwd_ring_kernel<false, true, NT, 2>, attn_fwd_ring_kernel<false, true, NT, 4>);
+        else launch(attn_fwd_ring_kernel<true, true, NT, 2>, attn_fwd_ring_kernel<true, true, NT, 4>);
+      } else {
+        if (!thr && (L & 31) == 0) launch(attn_fwd_ring_kernel<false, true, 0, 2>, attn_fwd_ring_kernel<false, true, 0, 4>);
+        else if (!thr) launch(attn_fwd_ring_kernel<false, false, 0, 2>, attn_fwd_ring_kernel<false, false, 0, 4>);
+        else if ((L & 31) == 0) launch(attn_fwd_ring_kernel<true, true, 0, 2>, attn_fwd_ring_kernel<true, true, 0, 4>);
+        else launch(attn_fwd_ring_kernel<true, false, 0, 2>, attn_fwd_ring_kernel<true, false, 0, 4>);
+      }
+    };
+    if (L == 384) run(std::integral_constant<int, 12>{});
+    else if (L == 512) run(std::integral_constant<int, 16>{});
+    else if (L == 256) run(std::integral_constant<int, 8>{});
+    else if (L == 128) run(std::integral_constant<int, 4>{});
+    else run(std::integral_constant<int, 0>{});
+    return;
+  }
   const int nw = waves_for(L);
   const size_t lds = (size_t)Lp * D * 2 * 2 + Lp * sizeof(float);
   auto run = [&](auto cw, auto cn) {

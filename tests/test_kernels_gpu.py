@@ -105,7 +105,7 @@ def test_gelu_and_bias_grad(cuda):
     _close(g2, d.float().sum(0), 1e-2, 1e-4, "bias_grad")
 
 
-def _attn_case(cuda, B, L, nh, p, masked, ramp=0.0, amp=1.0, ctx_tol=2e-2):
+def _attn_case(cuda, B, L, nh, p, masked, ramp=0.0, amp=1.0, ctx_tol=2e-2, left_pad=0):
     k = _native.kernels()
     torch.manual_seed(3)
     H = nh * 64
@@ -114,6 +114,8 @@ def _attn_case(cuda, B, L, nh, p, masked, ramp=0.0, amp=1.0, ctx_tol=2e-2):
     if masked:
         for b in range(B):
             kb[b, L - 1 - 7 * b:] = -10000.0
+    if left_pad:
+        kb[:, :left_pad] = -10000.0
     scale = 1.0 / 8.0
     ctx, lse, bits = k.attn_fwd(qkv.to(cuda), kb.to(cuda), B, L, nh, p, 555, 3, scale)
     ctxr, lser = ref.attn_fwd(qkv, kb, B, L, nh, p, 555, 3, scale)
@@ -136,13 +138,27 @@ def test_attention_bert_base_shape(cuda):
 
 
 @pytest.mark.parametrize("ramp", [0.05, 0.3, -0.05])
-def test_attention_deferred_rescale(cuda, ramp):
+def test_attention_growing_row_max(cuda, ramp):
     """Row maxima that keep growing across key tiles (a key-bias ramp: +2.3 / +14 log2 units per tile, or
-    falling): exercises the forward's deferred rescale (HQ_ATTN_DEFER, P <= 2^8
-    between rescales) against the fp32 reference, forward and backward.  (Scaling the scores up 2x instead
-    fails the bf16-vs-fp32 tolerances with the rescale deferred or not — HQ_ATTN_DEFER=0 measured worse,
-    6.3e-2 vs 4.7e-2 ctx max err — so that is the bf16 P / pre-scaled Q precision, not the deferral.)"""
+    falling).  The ring forward keeps m at the first tile's max, so P grows to 2^25 (ramp 0.05) or 2^150
+    (ramp 0.3: l overflows 2^64 → the workgroup's in-kernel slow path); both against the fp32 reference,
+    forward and backward.  The ramp also checks that the bias rides the 5th MFMA as bf16 hi + lo."""
     _attn_case(cuda, 2, 384, 2, 0.1, masked=True, ramp=ramp)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("L", [384, 100])
+def test_attention_slow_path_forced(cuda, monkeypatch, p, L):
+    """HQ_ATTN_FORCE_SLOW=1 sends every workgroup of the ring forward down its slow path (per-tile max and
+    rescale, per-wave LDS staging): rule 26 of the kernel playbook — the rare branch gets its own test."""
+    monkeypatch.setenv("HQ_ATTN_FORCE_SLOW", "1")
+    _attn_case(cuda, 2, L, 2, p, masked=True)
+
+
+def test_attention_left_padded(cuda):
+    """Left padding of 40 keys: the first key tile is fully masked, so the forward's m comes from masked
+    scores (−10000·log2e) and the real keys overflow P — the natural trigger of the slow path."""
+    _attn_case(cuda, 2, 384, 2, 0.1, masked=False, left_pad=40)
 
 
 def test_adamw_and_norm(cuda):
