@@ -467,7 +467,7 @@ __global__ __launch_bounds__(RW * 64, DROP ? 3 : 4) void attn_fwd_ring_kernel(co
   static_assert(RAHEAD >= 1 && RAHEAD <= 4, "ring depth");
   char* ring = reinterpret_cast<char*>(smem);                       // [RNS][K 4 KB | V 4 KB]
   char* sQ = ring + RAHEAD * 2 * RTILE;                             // [RQ][64] bf16 = ring slots RAHEAD, +1
-  uint2* sA = reinterpret_cast<uint2*>(ring + RNS * 2 * RTILE);     // [2][Lp]: (pk(b_hi, b_lo), pk(1, 0)) | 0
+  uint2* sA = reinterpret_cast<uint2*>(ring + RNS * 2 * RTILE);     // [Lp]: (pk(b_hi, b_lo), pk(1, 0))
   // XCD-aware block order (bijective): blocks b, b+8, … share an XCD; give each XCD a contiguous run of
   // (head, query-block) pairs with the query block fastest, so a head's blocks are co-resident on one L2
   const int nblk = gridDim.x, ob = blockIdx.x, xcd = ob & 7, qq = nblk >> 3, rr = nblk & 7;
@@ -504,12 +504,13 @@ __global__ __launch_bounds__(RW * 64, DROP ? 3 : 4) void attn_fwd_ring_kernel(co
 #pragma unroll
   for (int t = 0; t < RAHEAD; ++t)
     if (t < n32) stage(t);
+  // keys past L get a FINITE −1e30 (exp2 → 0): the hh = 1 lanes read these same words as k-dims 8..15,
+  // which meet zeros in Q' — finite × 0 = 0, where −inf × 0 would be NaN
   for (int t = threadIdx.x; t < Lp; t += RW * 64) {
-    const float bl = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -INFINITY;
+    const float bl = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -1e30f;
     const uint16_t hi = bf16_rne(bl);
     const uint16_t lo = t < L ? bf16_rne(bl - hq_bf2f(hi)) : 0;
     sA[t] = make_uint2((uint32_t)hi | ((uint32_t)lo << 16), 0x3F80u);  // (b_hi, b_lo, 1.0, 0)
-    sA[Lp + t] = make_uint2(0u, 0u);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -522,7 +523,7 @@ __global__ __launch_bounds__(RW * 64, DROP ? 3 : 4) void attn_fwd_ring_kernel(co
     const bf16x8_t raw = *reinterpret_cast<const bf16x8_t*>(sQ + 2 * (wave * 32 * D + lo_.row[s]));
     qf[s] = prescale8(raw, c_scale);
   }
-  const uint2* aug_src = sA + hh * Lp + (lane & 31);     // hh = 1 lanes read zeros (k-dims 8..15)
+  const uint2* aug_src = sA + (lane & 31);               // hh = 1 lanes: meets zeros in Q' (k-dims 8..15)
   float m_b = 0.f;                                        // bf16-exact running max (log2 domain)
   const uint32_t qaug_w0 = hh ? 0u : 0x3F803F80u;         // (1, 1) against (b_hi, b_lo)
   uint32_t qaug_w = 0u;                                   // (−m, 0) against (1, 0); −0 until the first tile
@@ -997,6 +998,354 @@ __global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t*
   }
 }
 
+// ============================================================================ backward v3
+// Same ideas as the ring forward, for the two backward kernels (dQ first — it also produces δ — then
+// dK/dV, which reads δ):
+// * dQ: 4-wave workgroups of 32 queries each; K and V tiles stream through the LDS-DMA ring; Q·c, dO
+//   and the dropout words of the wave's rows are loaded before the ring starts; bias and −LSE ride in the
+//   5th MFMA (A' = [K | b_hi, b_lo, 1, 1, 1], B' = [Q·c | 1, 1, −l_hi, −l_mid, −l_lo]: LSE to ~24 bits).
+// * dK/dV: ONE pass (S, dP, dV, dK per tile: 17 MFMAs instead of the two-pass 20) in 4-wave workgroups
+//   of 32 keys each; Q·c, dO, LSE and δ of each 32-query tile are register-staged into a 2-slot LDS
+//   ring (issue the loads before the tile's MFMAs, write after: T14) — Q must be prescaled on its way
+//   into LDS to reproduce the forward's rounded Q·c, which an LDS-DMA cannot do.
+__device__ __forceinline__ void split3(float x, uint16_t& hi, uint16_t& mid, uint16_t& lo) {
+  hi = bf16_rne(x);
+  const float r = x - hq_bf2f(hi);
+  mid = bf16_rne(r);
+  lo = bf16_rne(r - hq_bf2f(mid));
+}
+
+template <bool DROP, int NT, int RAHEAD>
+__global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
+    const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dctx, const uint16_t* __restrict__ ctx,
+    const float* __restrict__ lse, const float* __restrict__ key_bias, const uint16_t* __restrict__ mbits,
+    float* __restrict__ delta, uint16_t* __restrict__ dqkv, int L, int nh, int n_qb, float c_scale, float scale,
+    float kscale) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int RNS = RAHEAD + 2;
+  const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
+  char* ring = reinterpret_cast<char*>(smem);                       // [RNS][K 4 KB | V 4 KB]
+  uint4* sA = reinterpret_cast<uint4*>(ring + RNS * 2 * RTILE);     // [Lp] A' words (b_hi,b_lo|1,1|1,0|0)
+  uint16_t* sM = reinterpret_cast<uint16_t*>(sA + Lp);              // [RW][n32][64] dropout words
+  const int nblk = gridDim.x, ob = blockIdx.x, xcd = ob & 7, qq = nblk >> 3, rr = nblk & 7;
+  const int lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (ob >> 3);
+  const int bh = lin / n_qb, qb = lin - bh * n_qb;
+  const int b = bh / nh, h = bh - b * nh;
+  const int H = nh * D, ld = 3 * H;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, hh = lane >> 5;
+  const int qs = qb * RW + wave;
+  const int qi = qs * 32 + (lane & 31);
+  const bool active = qs * 32 < L;
+  const bool qok = qi < L;
+  const uint16_t* base = qkv + (size_t)b * L * ld + h * D;
+  HQ_DASSERT(L > 0 && L <= 512 && (NT == 0 || L == NT * 32));
+
+  // ---- prologue (plain loads, issued before any LDS-DMA): Q·c, dO, δ = rowsum(dO·O), −LSE words, bits
+  const int qr = qok ? qi : L - 1;
+  const size_t orow = ((size_t)b * L + qr) * H + h * D;
+  bf16x8_t qf[4], of[4];
+  float dpart = 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = prescale8(*reinterpret_cast<const bf16x8_t*>(base + (size_t)qr * ld + 16 * s + 8 * hh), c_scale);
+    of[s] = *reinterpret_cast<const bf16x8_t*>(dctx + orow + 16 * s + 8 * hh);
+    float x[8], y[8];
+    hq_unpack8(__builtin_bit_cast(uint4, of[s]), x);
+    hq_unpack8(*reinterpret_cast<const uint4*>(ctx + orow + 16 * s + 8 * hh), y);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dpart += x[j] * y[j];
+  }
+  const float dlt = xor32_sum(dpart);  // δ over all 64 dims (lanes q and q+32 hold 32 each)
+  if (active && qok && hh == 0) delta[(size_t)bh * L + qi] = dlt;
+  const float lq = lse[(size_t)bh * L + qr] * LOG2E;
+  uint16_t lh, lm, ll;
+  split3(-lq, lh, lm, ll);
+  typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+  const u32x4 qaw = hh ? u32x4{0u, 0u, 0u, 0u}
+                       : u32x4{0x3F803F80u, (uint32_t)lh | ((uint32_t)lm << 16), (uint32_t)ll, 0u};
+  const bf16x8_t qa = __builtin_bit_cast(bf16x8_t, qaw);
+  if constexpr (DROP) {
+    constexpr int kMaxT = 16;
+    uint16_t mw[kMaxT];
+    const uint16_t* gbits = mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane;
+#pragma unroll
+    for (int t = 0; t < kMaxT; ++t)
+      if (active && t < n32) mw[t] = gbits[(size_t)t * 64];
+#pragma unroll
+    for (int t = 0; t < kMaxT; ++t)
+      if (active && t < n32) sM[(wave * n32 + t) * 64 + lane] = mw[t];
+  }
+  for (int t = threadIdx.x; t < Lp; t += RW * 64) {  // finite −1e30 past L: see the forward
+    const float bl = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -1e30f;
+    const uint16_t hi = bf16_rne(bl);
+    const uint16_t lo = t < L ? bf16_rne(bl - hq_bf2f(hi)) : 0;
+    sA[t] = make_uint4((uint32_t)hi | ((uint32_t)lo << 16), 0x3F803F80u, 0x3F80u, 0u);
+  }
+  const int kv_off = dma_lane_off(wave * 8, ld, lane) + wave * 8 * ld;
+  auto stage = [&](int kt) {
+    char* slot = ring + (kt % RNS) * 2 * RTILE;
+    const uint16_t* kb = base + H + (size_t)kt * 32 * ld;
+    if (NT > 0 || kt * 32 + 32 <= L) {
+      dma_piece(kb + kv_off, slot + wave * 8 * 128);
+      dma_piece(kb + H + kv_off, slot + RTILE + wave * 8 * 128);
+    } else {
+      dma_rows8(kb, ld, wave * 8, L - kt * 32, slot, lane);
+      dma_rows8(kb + H, ld, wave * 8, L - kt * 32, slot + RTILE, lane);
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < RAHEAD; ++t)
+    if (t < n32) stage(t);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  auto wait_tile = [&](int kt) {  // only the two DMA pieces of each later staged tile are younger
+    const int later = kt + RAHEAD - 1 < n32 ? RAHEAD - 1 : n32 - 1 - kt;
+    wait_vm(2 * (later > 0 ? later : 0));
+  };
+  constexpr int UNR = NT > 0 ? NT : 1;
+  if (!active) {
+#pragma unroll UNR
+    for (int kt = 0; kt < n32; ++kt) {
+      wait_tile(kt);
+      __builtin_amdgcn_s_barrier();
+      if (kt + RAHEAD < n32) stage(kt + RAHEAD);
+    }
+    return;
+  }
+  LdsOffsets lo_;
+  lo_.init(lane);
+  const uint4* aug_src = sA + (lane & 31);
+  const uint16_t* my_bits = sM + wave * n32 * 64 + lane;
+  const f32x16_t zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  f32x16_t dq[2] = {zero16, zero16};
+  const f2_t dl2 = {dlt, dlt};
+#pragma unroll UNR
+  for (int kt = 0; kt < n32; ++kt) {
+    wait_tile(kt);
+    __builtin_amdgcn_s_barrier();
+    if (kt + RAHEAD < n32) stage(kt + RAHEAD);
+    const char* sK = ring + (kt % RNS) * 2 * RTILE;
+    const uint16_t* tK = reinterpret_cast<const uint16_t*>(sK);
+    const uint16_t* tV = reinterpret_cast<const uint16_t*>(sK + RTILE);
+    const uint4 aw = aug_src[kt * 32];
+    const bf16x8_t ka = __builtin_bit_cast(bf16x8_t, u32x4{aw.x, aw.y, aw.z, aw.w});
+    f32x16_t s_acc = mfma32(row8(tK, 0, lo_, 0), qf[0], zero16);
+#pragma unroll
+    for (int s = 1; s < 4; ++s) s_acc = mfma32(row8(tK, 0, lo_, s), qf[s], s_acc);
+    s_acc = mfma32(ka, qa, s_acc);                      // S' = c·q·k + bias − lse (log2 domain)
+    f32x16_t p_acc = mfma32(row8(tV, 0, lo_, 0), of[0], zero16);
+#pragma unroll
+    for (int s = 1; s < 4; ++s) p_acc = mfma32(row8(tV, 0, lo_, s), of[s], p_acc);
+    uint32_t bits = 0xFFFFu;
+    float ksc = 1.f;
+    if constexpr (DROP) {
+      bits = (uint32_t)my_bits[kt * 64];
+      ksc = kscale;
+    }
+    float ds[16];
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {  // dS = P·(dP·mask − δ)
+      const f2_t P = {__builtin_amdgcn_exp2f(s_acc[r]), __builtin_amdgcn_exp2f(s_acc[r + 1])};
+      const f2_t mk = {((bits >> r) & 1u) ? ksc : 0.f, ((bits >> (r + 1)) & 1u) ? ksc : 0.f};
+      const f2_t dp = {p_acc[r], p_acc[r + 1]};
+      const f2_t v = (dp * mk - dl2) * P;
+      ds[r] = v.x; ds[r + 1] = v.y;
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8_t sb = pack_b(ds, s);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) dq[d] = mfma32(tr8(tK, 0, lo_, s, d), sb, dq[d]);
+    }
+  }
+  if (qok) store_row64(dqkv + ((size_t)b * L + qi) * ld + h * D, dq, scale, hh);
+}
+
+// dK/dV: keys on the lanes.  Per 32-query tile: S = Q'·Kᵀ (+ aug: −LSE, bias), dP = dO·Vᵀ, then
+// dVᵀ += dOᵀ·(P∘mask) and dKᵀ += Q'ᵀ·dS with P/dS fed from the accumulators (no LDS round trip).
+template <bool DROP, int NT>
+__global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
+    const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dctx, const float* __restrict__ lse,
+    const float* __restrict__ delta, const float* __restrict__ key_bias, const uint16_t* __restrict__ mbits,
+    uint16_t* __restrict__ dqkv, int L, int nh, int n_kb, float c_scale, float scale, float kscale) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // slot: Q' [32][64] 4 KB | dO [32][64] 4 KB | A' words [32] uint4 512 B | δ [32] f32 128 B | bits [RW][64] u16
+  constexpr int SLOT = 2 * RTILE + 512 + 128 + RW * 128;
+  const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
+  const int nblk = gridDim.x, ob = blockIdx.x, xcd = ob & 7, qq = nblk >> 3, rr = nblk & 7;
+  const int lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (ob >> 3);
+  const int bh = lin / n_kb, kbk = lin - bh * n_kb;
+  const int b = bh / nh, h = bh - b * nh;
+  const int H = nh * D, ld = 3 * H;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, hh = lane >> 5;
+  const int tid = threadIdx.x;
+  const int ks_idx = kbk * RW + wave;                  // this wave's 32-key subtile
+  const int kj = ks_idx * 32 + (lane & 31);
+  const bool active = ks_idx * 32 < L;
+  const bool kok = kj < L;
+  const uint16_t* base = qkv + (size_t)b * L * ld + h * D;
+  HQ_DASSERT(L > 0 && L <= 512 && (NT == 0 || L == NT * 32));
+
+  // per-wave key fragments (B operands of S and dP) and the B' words (1,1,1,b_hi | b_lo,0,…)
+  const int kr = kok ? kj : L - 1;
+  bf16x8_t kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = *reinterpret_cast<const bf16x8_t*>(base + (size_t)kr * ld + H + 16 * s + 8 * hh);
+    vf[s] = *reinterpret_cast<const bf16x8_t*>(base + (size_t)kr * ld + 2 * H + 16 * s + 8 * hh);
+  }
+  typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+  bf16x8_t kaug;
+  {
+    const float bl = kok ? key_bias[(size_t)b * L + kj] * LOG2E : -1e30f;
+    const uint16_t bhi = bf16_rne(bl), blo = kok ? bf16_rne(bl - hq_bf2f(bhi)) : 0;
+    const u32x4 w = hh ? u32x4{0u, 0u, 0u, 0u}
+                       : u32x4{0x3F803F80u, 0x3F80u | ((uint32_t)bhi << 16), (uint32_t)blo, 0u};
+    kaug = __builtin_bit_cast(bf16x8_t, w);
+  }
+  // register staging of query tile t: thread tid → row tid>>3, 16-B chunk tid&7 of Q and dO; threads
+  // 0..31 the A' words (−l_hi,−l_mid | −l_lo,1 | 1,0 | 0) of query tid, 32..63 δ; each wave its bit words.
+  // Three tiles in flight in registers (HBM latency under load ≈ 2-3 tile bodies); two LDS slots.
+  const int srow = tid >> 3, schunk = tid & 7;
+  struct Stage {
+    uint4 q, o;
+    float l;
+    uint16_t bits;
+  };
+  auto issue = [&](int t, Stage& st) {
+    const int q = min(t * 32 + srow, L - 1);
+    st.q = *reinterpret_cast<const uint4*>(base + (size_t)q * ld + schunk * 8);
+    st.o = *reinterpret_cast<const uint4*>(dctx + ((size_t)b * L + q) * H + h * D + schunk * 8);
+    // every thread issues every load (wave 0's lse/δ values are the ones committed; the other waves load
+    // them redundantly): exec-masked loads would make hipcc's vmcnt counting assume they were skipped and
+    // wait for a tile too many
+    {
+      const int qq2 = min(t * 32 + (lane & 31), L - 1);
+      st.l = (lane < 32 ? lse : delta)[(size_t)bh * L + qq2];
+      if (t * 32 + (lane & 31) >= L) st.l = lane < 32 ? 1e30f : 0.f;  // queries past L: P = 0 (finite: split3)
+    }
+    st.bits = 0;
+    if constexpr (DROP) st.bits = mbits[(((size_t)bh * n32 + t) * n32 + min(ks_idx, n32 - 1)) * 64 + lane];
+  };
+  auto commit = [&](int t, const Stage& st) {
+    char* slot = reinterpret_cast<char*>(smem) + (t & 1) * SLOT;
+    uint16_t* sq = reinterpret_cast<uint16_t*>(slot);
+    uint16_t* so = sq + 32 * D;
+    float f[8];
+    hq_unpack8(st.q, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= c_scale;       // Q·c rounded exactly as the forward's prescale8
+    *reinterpret_cast<uint4*>(sq + lds_off(srow, schunk * 8)) = hq_pack8(f);
+    *reinterpret_cast<uint4*>(so + lds_off(srow, schunk * 8)) = st.o;
+    if (tid < 32) {
+      uint16_t lh, lm, ll;
+      split3(-st.l * LOG2E, lh, lm, ll);
+      reinterpret_cast<uint4*>(slot + 2 * RTILE)[tid] =
+          make_uint4((uint32_t)lh | ((uint32_t)lm << 16), (uint32_t)ll | (0x3F80u << 16), 0x3F80u, 0u);
+    } else if (tid < 64) {
+      reinterpret_cast<float*>(slot + 2 * RTILE + 512)[tid - 32] = st.l;
+    }
+    if constexpr (DROP) reinterpret_cast<uint16_t*>(slot + 2 * RTILE + 640)[wave * 64 + lane] = st.bits;
+  };
+  // Tile t lives in register set st[t % 3] (compile-time index in the unrolled NT > 0 loop: a rotation by
+  // copies would make hipcc wait for the NEWER tile's loads before each copy); the rolled NT = 0 loop
+  // rotates by copies (one tile less lookahead).
+  Stage st[3];
+  issue(0, st[0]);
+  if (n32 > 1) issue(1, st[1]);
+  if (n32 > 2) issue(2, st[2]);
+  commit(0, st[0]);
+  __syncthreads();
+  if constexpr (NT > 0) {
+    if (n32 > 3) issue(3, st[0]);
+  } else {
+    st[0] = st[1];
+    st[1] = st[2];
+    if (n32 > 3) issue(3, st[2]);
+  }
+
+  LdsOffsets lo_;
+  lo_.init(lane);
+  const f32x16_t zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  f32x16_t dv[2] = {zero16, zero16}, dk[2] = {zero16, zero16};
+  const int krel = lane & 31;
+  const int hh_f = (krel >> 2) & 1;
+  const int r_f = (krel & 3) + 4 * (krel >> 3);
+  const float ksc = DROP ? kscale : 1.f;
+  constexpr int UNR = NT > 0 ? NT : 1;
+#pragma unroll UNR
+  for (int t = 0; t < n32; ++t) {
+    const char* slot = reinterpret_cast<const char*>(smem) + (t & 1) * SLOT;
+    const uint16_t* tq = reinterpret_cast<const uint16_t*>(slot);
+    const uint16_t* to = tq + 32 * D;
+    if (active) {
+      const uint4 aw = reinterpret_cast<const uint4*>(slot + 2 * RTILE)[hh ? 0 : krel];
+      const bf16x8_t qa = hh ? bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0} : __builtin_bit_cast(bf16x8_t, u32x4{aw.x, aw.y, aw.z, aw.w});
+      f32x16_t s_acc = mfma32(row8(tq, 0, lo_, 0), kf[0], zero16);
+#pragma unroll
+      for (int s = 1; s < 4; ++s) s_acc = mfma32(row8(tq, 0, lo_, s), kf[s], s_acc);
+      s_acc = mfma32(qa, kaug, s_acc);                   // + bias_k − lse_q
+      f32x16_t p_acc = mfma32(row8(to, 0, lo_, 0), vf[0], zero16);
+#pragma unroll
+      for (int s = 1; s < 4; ++s) p_acc = mfma32(row8(to, 0, lo_, s), vf[s], p_acc);
+      // mask: the forward word of fwd-lane l' = q + 32·hh' holds bit r' for key acc_row(r', hh'); this lane
+      // (key krel) needs, for query rows acc_row(r, hh) = 8g + 4hh + i, bit r_f of the words of fwd-lanes
+      // 8g + 4hh + i + 32·hh_f: four consecutive words per g, one 8-byte LDS read per g
+      const uint16_t* wsrc = reinterpret_cast<const uint16_t*>(slot + 2 * RTILE + 640) + wave * 64 + 4 * hh + 32 * hh_f;
+      const float* sdl = reinterpret_cast<const float*>(slot + 2 * RTILE + 512);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float pd[8], dsv[8];
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg) {
+          const int g = 2 * s + gg;
+          uint32_t lo = 0xFFFFFFFFu, hi = 0xFFFFFFFFu;
+          if constexpr (DROP) {
+            const uint64_t w = *reinterpret_cast<const uint64_t*>(wsrc + 8 * g);
+            lo = (uint32_t)w >> r_f;
+            hi = (uint32_t)(w >> 32) >> r_f;
+          }
+          const float4 d4 = *reinterpret_cast<const float4*>(sdl + 8 * g + 4 * hh);
+          const float mk[4] = {(lo & 1u) ? ksc : 0.f, ((lo >> 16) & 1u) ? ksc : 0.f, (hi & 1u) ? ksc : 0.f,
+                               ((hi >> 16) & 1u) ? ksc : 0.f};
+          const float dl[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 4 * g + i;
+            const float P = __builtin_amdgcn_exp2f(s_acc[r]);
+            pd[4 * gg + i] = P * mk[i];
+            dsv[4 * gg + i] = (p_acc[r] * mk[i] - dl[i]) * P;
+          }
+        }
+        const bf16x8_t pb = pack_b(pd, 0), sb = pack_b(dsv, 0);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          dv[d] = mfma32(tr8(to, 0, lo_, s, d), pb, dv[d]);
+          dk[d] = mfma32(tr8(tq, 0, lo_, s, d), sb, dk[d]);
+        }
+      }
+    }
+    if (t + 1 < n32) {                                  // the other slot: last read before this barrier
+      if constexpr (NT > 0) {
+        commit(t + 1, st[(t + 1) % 3]);
+        __syncthreads();
+        if (t + 4 < n32) issue(t + 4, st[(t + 1) % 3]);
+      } else {
+        commit(t + 1, st[0]);
+        __syncthreads();
+        st[0] = st[1];
+        st[1] = st[2];
+        if (t + 4 < n32) issue(t + 4, st[2]);
+      }
+    }
+  }
+  if (active && kok) {
+    uint16_t* out = dqkv + ((size_t)b * L + kj) * ld + h * D;
+    store_row64(out + 2 * H, dv, 1.f, hh);
+    store_row64(out + H, dk, LN2, hh);                   // Q' = c·Q with c = scale·log2e: dK = Σ dS·Q'/log2e
+  }
+}
+
 // waves per workgroup for a sequence of L: all 32-row subtiles of a head in one workgroup up to
 // 12 waves (L <= 384: 3 waves/SIMD), else 8 waves with the head split over grid.y.
 int waves_for(int L) {
@@ -1069,7 +1418,7 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
     const int force_slow = attn_force_slow();
     const char* ea = getenv("HQ_ATTN_AHEAD");
     const int ahead = ea ? atoi(ea) : 2;
-    const size_t lds = (size_t)(ahead == 2 ? 4 : 6) * 2 * RTILE + 2 * Lp * sizeof(uint2);
+    const size_t lds = (size_t)(ahead == 2 ? 4 : 6) * 2 * RTILE + Lp * sizeof(uint2);
     auto run = [&](auto cn) {
       constexpr int NT = decltype(cn)::value;
       auto launch1 = [&](auto kern) {
@@ -1132,6 +1481,33 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
   const float ks = hq_keep_scale(thr);
   const uint16_t* bits = thr ? mbits : nullptr;
   const int Lp = (L + 31) & ~31, n32 = Lp / 32;
+  const char* ev = getenv("HQ_ATTN_BWD");
+  if (!ev || atoi(ev) == 3) {
+    const int nb = (L + RQ - 1) / RQ;                 // 128-row blocks (queries for dQ, keys for dK/dV)
+    constexpr int AH = 3;
+    const size_t lds_dq = (size_t)(AH + 2) * 2 * RTILE + Lp * sizeof(uint4) + (bits ? (size_t)RW * n32 * 128 : 0);
+    const size_t lds_kv = 2 * (size_t)(2 * RTILE + 512 + 128 + RW * 128);
+    auto run = [&](auto cn) {
+      constexpr int NT = decltype(cn)::value;
+      auto launch = [&](auto kdq, auto kkv) {
+        static bool attr =
+            (hipFuncSetAttribute((const void*)kdq, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess);
+        (void)attr;
+        hipLaunchKernelGGL(kdq, dim3(B * nh * nb), dim3(RW * 64), lds_dq, s, qkv, dctx, ctx, lse, key_bias, bits, delta,
+                           dqkv, L, nh, nb, scale * LOG2E, scale, ks);
+        hipLaunchKernelGGL(kkv, dim3(B * nh * nb), dim3(RW * 64), lds_kv, s, qkv, dctx, lse, delta, key_bias, bits, dqkv,
+                           L, nh, nb, scale * LOG2E, scale, ks);
+      };
+      if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH>, attn_bwd_dkdv_ring_kernel<true, NT>);
+      else launch(attn_bwd_dq_ring_kernel<false, NT, AH>, attn_bwd_dkdv_ring_kernel<false, NT>);
+    };
+    if (L == 384) run(std::integral_constant<int, 12>{});
+    else if (L == 512) run(std::integral_constant<int, 16>{});
+    else if (L == 256) run(std::integral_constant<int, 8>{});
+    else if (L == 128) run(std::integral_constant<int, 4>{});
+    else run(std::integral_constant<int, 0>{});
+    return;
+  }
   const int nw = waves_for(L);
   const size_t lds_bits = bits ? (size_t)nw * n32 * 64 * sizeof(uint16_t) : 0;  // staged keep-bit words
   const size_t lds_dq = (size_t)Lp * D * 2 * 2 + Lp * sizeof(float) + lds_bits;

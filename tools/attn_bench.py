@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--nh", type=int, default=12)
     ap.add_argument("--fwd", default="2,3:2,3:4", help="variants: HQ_ATTN_FWD[:HQ_ATTN_AHEAD], comma-separated")
     ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--bwd", default="2,3", help="backward variants (HQ_ATTN_BWD), comma-separated")
     a = ap.parse_args()
     k = kernels()
     dev = torch.device("cuda")
@@ -65,8 +66,20 @@ def main():
                 print(f"p={p} v{v} vs v{variants[0]}: max|dctx| {dc:.3e} max|dlse| {dl:.3e} bits_equal {same_bits}")
         ctx, lse, bits = outs[variants[-1]]
         os.environ.pop("HQ_ATTN_AHEAD", None)
-        tb = timeit(lambda: k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125))
-        print(f"p={p}: bwd {tb:8.1f} us ({2.5 * fl_fwd / tb / 1e6:6.1f} TF)", flush=True)
+        grads = {}
+        for rnd in range(a.rounds):
+            for v in [x for x in a.bwd.split(",") if x]:
+                os.environ["HQ_ATTN_BWD"] = v
+                grads[v] = k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125)
+                tb = timeit(lambda: k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125))
+                print(f"p={p} bwd v{v} round {rnd}: {tb:8.1f} us ({2.5 * fl_fwd / tb / 1e6:6.1f} TF)", flush=True)
+        vs = list(grads)
+        for v in vs[1:]:
+            d = (grads[v].float() - grads[vs[0]].float()).abs()
+            H3 = grads[v].shape[1] // 3
+            print(f"p={p} bwd v{v} vs v{vs[0]}: max|d dq| {d[:, :H3].max().item():.3e} "
+                  f"max|d dk| {d[:, H3:2 * H3].max().item():.3e} max|d dv| {d[:, 2 * H3:].max().item():.3e}")
+        os.environ.pop("HQ_ATTN_BWD", None)
 
 
 if __name__ == "__main__":
