@@ -97,8 +97,12 @@ def main():
     reducer = None
     if world > 1 or args.force_reducer:
         reducer = GradReducer(model, bucket_cap_mb=args.bucket_cap_mb, allreduce_dtype=args.allreduce_dtype,
-                              force=args.force_reducer, timing=True)
-    engine = TrainEngine(model, loss_fn, opt, scheduler=sched, reducer=reducer, max_grad_norm=1.0, profile=args.profile)
+                              force=args.force_reducer, timing=os.environ.get("HQ_BENCH_COMM_TIMING", "1") == "1")
+    # HQ_BENCH_REDUCER_IDLE=1 (diagnostic): the reducer and its RCCL communicator exist but the engine never
+    # uses them — separates the cost of the communicator's presence from that of its all-reduces
+    idle = os.environ.get("HQ_BENCH_REDUCER_IDLE", "0") == "1"
+    engine = TrainEngine(model, loss_fn, opt, scheduler=sched, reducer=None if idle else reducer, max_grad_norm=1.0,
+                         profile=args.profile)
 
     sp = SpecialIds(cfg.vocab_size, cfg.pad_token_id, cfg.unk_token_id, cfg.cls_token_id, cfg.sep_token_id,
                     "bert" if cfg.family == "bert" else "roberta")

@@ -3,4 +3,27 @@
 Capability parity with neuro-inc/ml-recipe-distributed-pytorch: distributed BERT/RoBERTa QA fine-tuning
 (train.py / validate.py CLI, .cfg configs, checkpoints, dummy + Natural Questions data paths).
 """
+import os as _os
+
 __version__ = "0.1.0"
+
+
+def _reserve_hw_queues(minimum: int = 8):
+    """Give every HIP stream of the process its own hardware queue (set before HIP initialises).
+
+    The training step uses up to 5 streams (compute, weight-gradient side stream, the reducer's comm
+    stream and RCCL's internal streams).  With HIP's default of 4 hardware queues two of them share one
+    in-order AQL queue, so the compute stream's kernels queue up behind the all-reduce's cross-stream
+    waits: measured on MI355X with the RCCL reducer active, 80.8 ms/step with 4 queues vs 69.6 ms with 8
+    (69.1 ms without a reducer; profiles/r2_reducer/).  HQ_KEEP_HW_QUEUES=1 leaves the setting alone."""
+    if _os.environ.get("HQ_KEEP_HW_QUEUES") == "1":
+        return
+    try:
+        cur = int(_os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        cur = 4
+    if cur < minimum:
+        _os.environ["GPU_MAX_HW_QUEUES"] = str(minimum)
+
+
+_reserve_hw_queues()

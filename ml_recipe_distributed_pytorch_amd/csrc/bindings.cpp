@@ -5,6 +5,7 @@
 #include <torch/extension.h>
 
 #include <limits>
+#include <map>
 
 #include "hq_kernels.h"
 #include "hq_reducer.h"
@@ -431,6 +432,114 @@ void cast_f32_bf16(Tensor src, Tensor dst, double scale) {
   hq_cast_f32_bf16(ptr<float>(src), ptr<uint16_t>(dst), src.numel(), (float)scale, cur_stream());
 }
 
+// ------------------------------------------------------------------------ fused QA heads + losses
+// Ticket words of the in-launch hand-offs (heads.hip), one zeroed int32[4] per (device, stream): [0] fwd,
+// [1] loss.  The last-arriving block resets its word, so a buffer is zeroed exactly once.
+unsigned* ticket(const Tensor& like, int slot) {
+  static std::map<std::pair<int, hipStream_t>, Tensor> words;
+  const auto key = std::make_pair((int)like.get_device(), cur_stream());
+  auto it = words.find(key);
+  if (it == words.end()) it = words.emplace(key, at::zeros({4}, like.options().dtype(at::kInt))).first;
+  return reinterpret_cast<unsigned*>(it->second.data_ptr<int>()) + slot;
+}
+
+HqHeadWeights head_weights(const std::vector<Tensor>& w, int64_t H, int64_t NL) {
+  TORCH_CHECK(w.size() == 10, "head weights: wp, bp, wc, bc, wrs, brs, wre, bre, wsp, bsp");
+  const int64_t numel[10] = {H * H, H, NL * H, NL, H, 1, H, 1, 2 * H, 2};
+  for (int i = 0; i < 10; ++i) {
+    check(w[i], F32, "head weight");
+    TORCH_CHECK(w[i].numel() == numel[i], "head weight ", i, ": ", w[i].numel(), " elements, expected ", numel[i]);
+  }
+  return HqHeadWeights{ptr<float>(w[0]), ptr<float>(w[1]), ptr<float>(w[2]), ptr<float>(w[3]), ptr<float>(w[4]),
+                       ptr<float>(w[5]), ptr<float>(w[6]), ptr<float>(w[7]), ptr<float>(w[8]), ptr<float>(w[9])};
+}
+
+void check_heads_shape(const Tensor& seq, int64_t L, int64_t NL) {
+  check(seq, BF16, "seq");
+  const int64_t H = seq.size(-1), T = seq.numel() / H;
+  TORCH_CHECK(L > 0 && T % L == 0, "seq rows must be B*L");
+  TORCH_CHECK(H % 64 == 0 && H <= 2048, "fused heads need hidden % 64 == 0 and <= 2048, got ", H);
+  TORCH_CHECK(NL >= 1 && NL <= 8, "fused heads support 1..8 classes, got ", NL);
+  TORCH_CHECK(T * H < (int64_t)std::numeric_limits<int32_t>::max(), "T*H exceeds 32-bit indexing");
+}
+
+// returns logits [T,2], pooled [B,H], cls [B,NL], reg [B,2] (sigmoid outputs)
+std::vector<Tensor> qa_heads_fwd(Tensor seq, int64_t L, std::vector<Tensor> w, double p, int64_t seed, int64_t opid) {
+  const int64_t H = seq.size(-1), NL = w.size() > 3 ? w[3].numel() : 0;
+  check_heads_shape(seq, L, NL);
+  const int64_t T = seq.numel() / H, B = T / L;
+  const HqHeadWeights hw = head_weights(w, H, NL);
+  c10::DeviceGuard g(seq.device());
+  auto f = w[0].options();
+  auto logits = at::empty({T, 2}, f);
+  auto pooled = at::empty({B, H}, f);
+  auto cls = at::empty({B, NL}, f);
+  auto reg = at::empty({B, 2}, f);
+  auto hpart = at::empty({(int64_t)hq_qa_heads_fwd_scratch((int)B, (int)H)}, f);
+  hq_qa_heads_fwd(ptr<uint16_t>(seq), hw, ptr<float>(logits), ptr<float>(pooled), ptr<float>(cls), ptr<float>(reg),
+                  ptr<float>(hpart), ticket(seq, 0), (int)B, (int)L, (int)H, (int)NL, (float)p, u32(seed), u32(opid),
+                  cur_stream());
+  return {logits, pooled, cls, reg};
+}
+
+// returns losses [6], dlog [T,2], dheads [B,16]
+std::vector<Tensor> qa_loss(Tensor logits, Tensor cls, Tensor reg, Tensor t_start, Tensor t_end, Tensor t_rs, Tensor t_re,
+                            Tensor t_cls, c10::optional<Tensor> lw, int64_t kind, int64_t ignore_cls,
+                            std::vector<double> weights, double alpha, double gamma, double conf, double fill) {
+  check(logits, F32, "logits"); check(cls, F32, "cls"); check(reg, F32, "reg");
+  check(t_start, I64, "start_class"); check(t_end, I64, "end_class"); check(t_cls, I64, "cls target");
+  check(t_rs, F32, "start_reg"); check(t_re, F32, "end_reg"); check_opt(lw, F32, "label_weights");
+  const int64_t B = cls.size(0), NL = cls.size(1), T = logits.size(0);
+  TORCH_CHECK(logits.dim() == 2 && logits.size(1) == 2 && B > 0 && T % B == 0, "logits [B*L, 2]");
+  TORCH_CHECK(NL >= 1 && NL <= 8 && reg.numel() == 2 * B, "cls [B, NL<=8], reg [B, 2]");
+  TORCH_CHECK(t_start.numel() == B && t_end.numel() == B && t_cls.numel() == B && t_rs.numel() == B &&
+                  t_re.numel() == B, "targets must have B elements");
+  TORCH_CHECK(!lw.has_value() || !lw->defined() || lw->numel() == NL, "label weights [NL]");
+  TORCH_CHECK(weights.size() == 5 && kind >= 0 && kind <= 2, "loss config");
+  c10::DeviceGuard g(logits.device());
+  auto f = logits.options();
+  auto losses = at::empty({6}, f);
+  auto dlog = at::empty({T, 2}, f);
+  auto dheads = at::empty({B, 16}, f);
+  auto part = at::empty({(int64_t)hq_qa_loss_partials((int)B), 4}, f);
+  HqLossCfg cfg;
+  cfg.kind = (int)kind;
+  cfg.ignore_cls = (int)ignore_cls;
+  for (int i = 0; i < 5; ++i) cfg.w[i] = (float)weights[i];
+  cfg.alpha = (float)alpha; cfg.gamma = (float)gamma; cfg.conf = (float)conf; cfg.fill = (float)fill;
+  hq_qa_loss(ptr<float>(logits), ptr<float>(cls), ptr<float>(reg), ptr<int64_t>(t_start), ptr<int64_t>(t_end),
+             ptr<int64_t>(t_cls), ptr<float>(t_rs), ptr<float>(t_re), optr<float>(lw), ptr<float>(dlog), ptr<float>(dheads),
+             ptr<float>(losses), ptr<float>(part), ticket(logits, 1), (int)B, (int)(T / B), (int)NL, cfg, cur_stream());
+  return {losses, dlog, dheads};
+}
+
+// writes the 10 head gradients (wp, bp, wc, bc, wrs, brs, wre, bre, wsp, bsp) (+)=; returns dseq (bf16, seq's shape)
+Tensor qa_heads_bwd(Tensor seq, int64_t L, Tensor dlog, Tensor dheads, c10::optional<Tensor> gscale, Tensor pooled,
+                    Tensor reg, std::vector<Tensor> w, std::vector<Tensor> grads, bool accumulate, double p, int64_t seed,
+                    int64_t opid) {
+  const int64_t H = seq.size(-1), NL = w.size() > 3 ? w[3].numel() : 0;
+  check_heads_shape(seq, L, NL);
+  const int64_t T = seq.numel() / H, B = T / L;
+  check(dlog, F32, "dlog"); check(dheads, F32, "dheads"); check(pooled, F32, "pooled"); check(reg, F32, "reg");
+  check_opt(gscale, F32, "gscale");
+  TORCH_CHECK(dlog.numel() == 2 * T && dheads.numel() == 16 * B && pooled.numel() == B * H && reg.numel() == 2 * B,
+              "qa_heads_bwd: operand shapes");
+  TORCH_CHECK(!gscale.has_value() || !gscale->defined() || gscale->numel() == 1, "gscale is a scalar");
+  const HqHeadWeights hw = head_weights(w, H, NL);
+  const HqHeadWeights hg = head_weights(grads, H, NL);  // same shapes / dtype checks for the gradients
+  HqHeadGrads gg{const_cast<float*>(hg.wp), const_cast<float*>(hg.bp), const_cast<float*>(hg.wc),
+                 const_cast<float*>(hg.bc), const_cast<float*>(hg.wrs), const_cast<float*>(hg.brs),
+                 const_cast<float*>(hg.wre), const_cast<float*>(hg.bre), const_cast<float*>(hg.wsp),
+                 const_cast<float*>(hg.bsp)};
+  c10::DeviceGuard g(seq.device());
+  auto dseq = at::empty_like(seq);
+  auto part = at::empty({(int64_t)hq_qa_heads_bwd_span_blocks((int)T), 2 * H + 2}, pooled.options());
+  hq_qa_heads_bwd(ptr<uint16_t>(seq), ptr<float>(dlog), ptr<float>(dheads), optr<float>(gscale), ptr<float>(pooled),
+                  ptr<float>(reg), hw, gg, ptr<uint16_t>(dseq), ptr<float>(part), (int)B, (int)L, (int)H, (int)NL,
+                  accumulate, (float)p, u32(seed), u32(opid), cur_stream());
+  return dseq;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_hq_kernels, m) {
@@ -460,6 +569,9 @@ PYBIND11_MODULE(_hq_kernels, m) {
         py::arg("pre") = py::none(), py::arg("out8") = py::none(), py::arg("state") = py::none(), py::arg("phase") = 0);
   m.def("span_fwd", &span_fwd);
   m.def("span_bwd", &span_bwd);
+  m.def("qa_heads_fwd", &qa_heads_fwd);
+  m.def("qa_loss", &qa_loss);
+  m.def("qa_heads_bwd", &qa_heads_bwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("bias_grad", &bias_grad);
   m.def("attn_fwd", &attn_fwd);
@@ -481,7 +593,8 @@ PYBIND11_MODULE(_hq_kernels, m) {
       .def(py::init([](int rank, int world, py::bytes uid, int device) {
              return new HqReducer(rank, world, std::string(uid), device);
            }))
-      .def("allreduce_f32", &HqReducer::allreduce_f32, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_f32", &HqReducer::allreduce_f32, py::arg("ptr"), py::arg("count"), py::arg("stream"),
+           py::arg("op") = 0, py::call_guard<py::gil_scoped_release>())
       .def("allreduce_bf16", &HqReducer::allreduce_bf16, py::call_guard<py::gil_scoped_release>())
       .def("broadcast", &HqReducer::broadcast, py::call_guard<py::gil_scoped_release>())
       .def("wait", &HqReducer::wait)

@@ -108,3 +108,34 @@ void hq_span_fwd(const uint16_t* seq, const float* w, const float* b, float* log
 // part: [hq_ln_bwd_partials(T)][2][H] scratch; dw: [2][H] (+)=
 void hq_span_bwd(const uint16_t* seq, const float* w, const float* g, uint16_t* dseq, float* part, float* dw, int T,
                  int H, bool accumulate, hipStream_t s);
+// out_q[c] (+)= Σ_p part[p][q·Hq + c] for the (≤ 4) destinations of outs, part f32 [P][N]
+void hq_colsum_outs(const float* part, int P, int N, HqOuts outs, int Hq, bool accumulate, hipStream_t s);
+
+// ------------------------------------------------------------------ fused QA heads + losses (heads.hip)
+struct HqHeadWeights {  // fp32 master weights: pooler, classifier [NL,H], reg start/end [1,H], span [2,H]
+  const float *wp, *bp, *wc, *bc, *wrs, *brs, *wre, *bre, *wsp, *bsp;
+};
+struct HqHeadGrads {    // fp32 arena gradients (null = not trainable)
+  float *gwp, *gbp, *gwc, *gbc, *gwrs, *gbrs, *gwre, *gbre, *gwsp, *gbsp;
+};
+struct HqLossCfg {
+  int kind;             // 0 = CE (optional class weights, ignore_cls), 1 = focal (ignore -1), 2 = label smoothing
+  int ignore_cls;
+  float w[5];           // start, end, start_reg, end_reg, cls
+  float alpha, gamma;   // focal
+  float conf, fill;     // label smoothing target distribution
+};
+size_t hq_qa_heads_fwd_scratch(int B, int H);   // floats of the fwd head-partial scratch
+// logits [B·L, 2], pooled [B, H], cls [B, NL], reg [B, 2] (sigmoid); cnt: a zeroed device word, one per stream
+void hq_qa_heads_fwd(const uint16_t* seq, const HqHeadWeights& w, float* logits, float* pooled, float* cls, float* reg,
+                     float* hpart, unsigned* cnt, int B, int L, int H, int NL, float p, uint32_t seed, uint32_t opid,
+                     hipStream_t s);
+int hq_qa_loss_partials(int B);                 // rows of the [rows][4] loss scratch
+// losses[6] = start, end, start_reg, end_reg, cls, total; dlog [B·L, 2] and dheads [B, 16] = d total / d preds
+void hq_qa_loss(const float* logits, const float* cls, const float* reg, const int64_t* t_start, const int64_t* t_end,
+                const int64_t* t_cls, const float* t_rs, const float* t_re, const float* lw, float* dlog, float* dheads,
+                float* losses, float* part, unsigned* cnt, int B, int L, int NL, const HqLossCfg& cfg, hipStream_t s);
+int hq_qa_heads_bwd_span_blocks(int T);         // rows of the [rows][2H + 2] span partial scratch
+void hq_qa_heads_bwd(const uint16_t* seq, const float* dlog, const float* dheads, const float* gscale, const float* pooled,
+                     const float* reg, const HqHeadWeights& w, const HqHeadGrads& g, uint16_t* dseq, float* span_part,
+                     int B, int L, int H, int NL, bool accumulate, float p, uint32_t seed, uint32_t opid, hipStream_t s);

@@ -14,7 +14,7 @@ class HqReducer {
   HqReducer(const HqReducer&) = delete;
   HqReducer& operator=(const HqReducer&) = delete;
 
-  void allreduce_f32(int64_t ptr, int64_t count, int64_t compute_stream);
+  void allreduce_f32(int64_t ptr, int64_t count, int64_t compute_stream, int op = 0);  // op 0 = avg, 1 = sum
   void allreduce_bf16(int64_t ptr_f32, int64_t scratch_bf16, int64_t count, int64_t compute_stream);
   void broadcast(int64_t ptr, int64_t count, int dtype, int root, int64_t compute_stream);
   void wait(int64_t compute_stream);

@@ -879,7 +879,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   }
 }
 
-int g_gemm_variant = 0;   // 0 = auto (v3 for K <= 2304, else v2), 1 = force v1, 2 = force v2, 3 = force v3
+// 0 = auto (v3 for K <= 2304, else v2), 1 = force v1, 2 = force v2, 3 = force v3; HQ_GEMM_VARIANT sets it
+int g_gemm_variant = [] {
+  const char* e = getenv("HQ_GEMM_VARIANT");
+  return e ? atoi(e) : 0;
+}();
 
 constexpr size_t epi_lds(int bn) {
   const size_t stage = 2 * (size_t)(BM * 128 + bn * 128);

@@ -735,6 +735,10 @@ void hq_colsum(const float* part, int P, int N, float* out, bool accumulate, hip
   colsum(part, P, N, HqOuts{{out, nullptr, nullptr, nullptr}}, N, accumulate, s);
 }
 
+void hq_colsum_outs(const float* part, int P, int N, HqOuts outs, int Hq, bool accumulate, hipStream_t s) {
+  colsum(part, P, N, outs, Hq, accumulate, s);
+}
+
 void hq_span_fwd(const uint16_t* seq, const float* w, const float* b, float* logits, int T, int H, hipStream_t s) {
   dispatch_nch(H, [&](auto nch) {
     hipLaunchKernelGGL(span_fwd_kernel<decltype(nch)::value>, dim3((T + kWaves - 1) / kWaves), dim3(256), 0, s, seq, w, b,

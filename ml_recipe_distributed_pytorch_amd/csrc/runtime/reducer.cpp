@@ -1,7 +1,7 @@
 // Flat-bucket gradient reducer over RCCL (native replacement for torch DDP's Reducer).
 //
 // * Owns its own RCCL communicator (bootstrapped with a unique id that Python ships through the
-//   torch.distributed TCPStore) and a high-priority HIP stream for communication.
+//   torch.distributed TCPStore) and a normal-priority HIP stream for communication.
 // * allreduce(ptr, count, …, compute_stream): records an event on the compute stream, makes the comm
 //   stream wait on it, then ncclAllReduce(ncclAvg) in place on a contiguous slice of the fp32 grad
 //   arena — the bucket IS the arena slice, so there is no copy-in/copy-out.
@@ -15,6 +15,7 @@
 #include <rccl/rccl.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -48,8 +49,13 @@ HqReducer::HqReducer(int rank, int world, const std::string& uid, int device) : 
   comm_ = comm;
   int lo = 0, hi = 0;
   HIP_CHECK_THROW(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  // The comm stream runs at NORMAL priority: measured on MI355X (tools/stream_overlap_bench.py), a
+  // high-priority comm queue slows every kernel of the compute stream while an all-reduce is in flight
+  // (+1.9 ms per 48 GEMMs against +0.5 ms at normal priority).  HQ_COMM_PRIO=1 restores the high priority.
+  const char* pe = getenv("HQ_COMM_PRIO");
+  const int prio = (pe && atoi(pe) == 1) ? hi : lo;
   hipStream_t st;
-  HIP_CHECK_THROW(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, hi));
+  HIP_CHECK_THROW(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio));
   stream_ = st;
   for (int i = 0; i < kEvents; ++i) {
     hipEvent_t e;
@@ -78,9 +84,10 @@ void HqReducer::fence_from(int64_t compute_stream) {
   HIP_CHECK_THROW(hipStreamWaitEvent((hipStream_t)stream_, e, 0));
 }
 
-void HqReducer::allreduce_f32(int64_t ptr, int64_t count, int64_t compute_stream) {
+void HqReducer::allreduce_f32(int64_t ptr, int64_t count, int64_t compute_stream, int op) {
   fence_from(compute_stream);
-  NCCL_CHECK(ncclAllReduce((const void*)ptr, (void*)ptr, (size_t)count, ncclFloat32, ncclAvg, (ncclComm_t)comm_,
+  NCCL_CHECK(ncclAllReduce((const void*)ptr, (void*)ptr, (size_t)count, ncclFloat32, op == 1 ? ncclSum : ncclAvg,
+                           (ncclComm_t)comm_,
                            (hipStream_t)stream_));
 }
 

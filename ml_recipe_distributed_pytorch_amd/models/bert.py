@@ -11,8 +11,8 @@ Capability parity with the reference model (``modules/model/model/model.py:13-73
   layer then signals the gradient reducer, which overlaps its RCCL all-reduce with the rest of
   the backward (replaces DDP's per-parameter autograd hooks).
 * Dropout masks are regenerated from a counter hash (``ops.rng``) — nothing is stored.
-* Pooler + the four heads are tiny (B×H); they run as ordinary fp32 autograd on the master
-  parameters.
+* Pooler + the four heads (``heads.py``): on the GPU one fused fp32 kernel each way plus one fused
+  loss kernel (``csrc/kernels/heads.hip``); elsewhere ordinary fp32 autograd on the master parameters.
 * ``state_dict()`` keys are the HF names under ``transformer.`` plus the reference head names, so
   reference checkpoints load and ours load into the reference (``embeddings.position_ids`` kept).
 """
@@ -24,10 +24,10 @@ from typing import Callable, Dict, List, Optional
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .. import ops
 from .config import EncoderConfig
+from .heads import fused_heads, fused_heads_available, reference_heads
 from .params import Entry, ParamStore
 
 LABELS = ["yes", "no", "short", "long", "unknown"]
@@ -333,6 +333,7 @@ class BertForQuestionAnswering(nn.Module):
         self._fresh: Dict[str, bool] = {}
         self._grad_listener: Optional[Callable[[str], None]] = None
         self._head_pending = 0
+        self._head_range = next((s, e) for g, s, e in self.store.group_ranges() if g == "head")
         for prm in self._head_params:
             prm.register_post_accumulate_grad_hook(self._head_hook)
         self.zero_grad()
@@ -398,12 +399,10 @@ class BertForQuestionAnswering(nn.Module):
 
     # -------------------------------------------------------------------- grads / reducer hooks
     def zero_grad(self, set_to_none: bool = False):
-        """Mark every gradient group "fresh": the next backward overwrites instead of accumulating
-        (no memset of the encoder arena).  Autograd-managed head grads are zeroed for real."""
+        """Mark every gradient group "fresh": the next backward overwrites instead of accumulating (no
+        memset of the arena).  The autograd heads path clears the head range lazily in ``forward``."""
         for g, s, e in self.store.group_ranges():
             self._fresh[g] = True
-        for prm in self._head_params:
-            prm.grad.zero_()
         self._head_pending = len([p for p in self._head_params if p.requires_grad])
 
     def _take_accumulate(self, group: str) -> bool:
@@ -418,7 +417,6 @@ class BertForQuestionAnswering(nn.Module):
     def _head_hook(self, _p):
         self._head_pending -= 1
         if self._head_pending == 0:
-            self._fresh["head"] = False
             self._group_ready("head")
             self._head_pending = len([p for p in self._head_params if p.requires_grad])
 
@@ -446,6 +444,9 @@ class BertForQuestionAnswering(nn.Module):
         return self.transformer.embeddings.position_ids[:, :L].expand(B, L)
 
     def encode(self, input_ids, attention_mask=None, token_type_ids=None, position_ids=None):
+        return self._encode(input_ids, attention_mask, token_type_ids, position_ids)[0]
+
+    def _encode(self, input_ids, attention_mask=None, token_type_ids=None, position_ids=None):
         cfg = self.config
         B, L = input_ids.shape
         if L > cfg.max_position_embeddings - cfg.position_offset:
@@ -466,26 +467,21 @@ class BertForQuestionAnswering(nn.Module):
         for i in range(cfg.num_hidden_layers):
             anchor = self.store.params[f"transformer.encoder.layer.{i}.attention.self.query.weight"]
             h = _LayerFn.apply(h, anchor, key_bias, i, info)
-        return h.view(B, L, cfg.hidden_size)
+        return h.view(B, L, cfg.hidden_size), seed
 
     def forward(self, input_ids, attention_mask=None, token_type_ids=None, position_ids=None, head_mask=None):
         if head_mask is not None:
             raise NotImplementedError("head_mask is not supported by the fused encoder")
-        seq = self.encode(input_ids, attention_mask, token_type_ids, position_ids)
-        P = self.store.params
-        pooled = torch.tanh(F.linear(seq[:, 0].float(), P["transformer.pooler.dense.weight"],
-                                     P["transformer.pooler.dense.bias"]))
-        if seq.is_cuda and seq.dtype == torch.bfloat16:  # fused span head straight from bf16 (no fp32 copy)
-            pos_logits = _SpanHeadFn.apply(seq, P["position_outputs.weight"], P["position_outputs.bias"])
-        else:
-            pos_logits = F.linear(seq.float(), P["position_outputs.weight"], P["position_outputs.bias"])
-        start_logits, end_logits = pos_logits.split(1, dim=-1)
-        cls_in = F.dropout(pooled, self.config.hidden_dropout_prob, self.training)
-        cls = F.linear(cls_in, P["classifier.1.weight"], P["classifier.1.bias"])
-        reg_start = torch.sigmoid(F.linear(pooled, P["reg_start.0.weight"], P["reg_start.0.bias"])).squeeze(-1)
-        reg_end = torch.sigmoid(F.linear(pooled, P["reg_end.0.weight"], P["reg_end.0.bias"])).squeeze(-1)
-        return {"start_class": start_logits.squeeze(-1), "end_class": end_logits.squeeze(-1),
-                "start_reg": reg_start, "end_reg": reg_end, "cls": cls}
+        seq, seed = self._encode(input_ids, attention_mask, token_type_ids, position_ids)
+        if fused_heads_available(self, seq):
+            return fused_heads(self, seq, seed, self.training)
+        if torch.is_grad_enabled() and self._fresh.get("head", True):
+            # autograd accumulates into the arena views: clear the head range once per fresh step
+            s, e = self._head_range
+            self.store.grad[s:e].zero_()
+            self._fresh["head"] = False
+        span = _SpanHeadFn.apply if seq.is_cuda and seq.dtype == torch.bfloat16 else None
+        return reference_heads(self, seq, seed, self.training, span_fn=span)
 
 
 def load_pretrained(model: BertForQuestionAnswering, path: str) -> List[str]:

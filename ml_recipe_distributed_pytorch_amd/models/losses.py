@@ -8,6 +8,7 @@ Differences by design:
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -81,13 +82,27 @@ class LossRecord(dict):
 class WeightedLoss:
     """Σ_k w_k · loss_k(pred[k], target[k]) over {start_class, end_class, start_reg, end_reg, cls}."""
 
+    _KEYS = ("start_class", "end_class", "start_reg", "end_reg", "cls")
+
     def __init__(self, init_losses: Dict[str, Tuple[nn.Module, float]]):
+        from .heads import fused_loss_config
         self._losses = init_losses
         self.last: Optional[LossRecord] = None
+        # predictions from the fused GPU heads + this exact loss set: one kernel for all five terms
+        self._fused_cfg = fused_loss_config(init_losses) if os.environ.get("HQ_FUSED_LOSS", "1") != "0" else None
 
     def __call__(self, preds, targets, *, avg_meters=None):
         assert set(preds) >= set(self._losses), "missing predictions"
         assert set(targets) >= set(self._losses), "missing targets"
+        from .heads import fused_loss, fused_loss_usable
+        if fused_loss_usable(preds, self._fused_cfg):
+            full, vals = fused_loss(preds, targets, self._fused_cfg)
+            rec = LossRecord({k: vals[i] for i, k in enumerate(self._KEYS)})
+            rec["loss"] = vals[5]
+            self.last = rec
+            if avg_meters is not None:
+                avg_meters.update(rec.to_floats())
+            return full
         rec = LossRecord()
         full = 0.0
         for key, (fn, weight) in self._losses.items():

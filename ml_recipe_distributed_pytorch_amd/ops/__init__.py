@@ -1,7 +1,10 @@
 """Fused-op API used by the model.  Dispatch is by device, not by a backend registry:
 
-* CUDA (ROCm/HIP) tensors → hand-written gfx950 kernels in ``_hq_kernels.so`` (fail loudly if absent);
-  plain GEMMs go to hipBLASLt through ``torch.addmm/mm`` (library GEMMs, no fused epilogue needed).
+* CUDA (ROCm/HIP) tensors → hand-written gfx950 kernels in ``_hq_kernels.so`` (fail loudly if absent):
+  embedding, LayerNorm, attention, optimizer, and the MFMA GEMMs (``gemm.hip`` NT with fused epilogues
+  for every encoder projection forward and dgrad, ``gemm_tn.hip`` split-K weight gradients).  hipBLASLt
+  (``torch.addmm/mm``) is only the fallback for shapes the MFMA kernels do not tile (see ``_mfma``) and
+  for the tiny pooler / QA-head GEMMs.
 * CPU tensors → ``ops.reference`` (pure PyTorch, fp32), which is also the numerics oracle.
 """
 from __future__ import annotations

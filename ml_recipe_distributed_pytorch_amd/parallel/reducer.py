@@ -6,7 +6,7 @@ layer N-1 … layer 0, embeddings — the order backward produces them), merged 
 bucket has reported, the bucket's all-reduce is issued immediately, so communication overlaps
 the remaining backward.  ``finalize()`` makes the compute stream wait for the last bucket.
 
-* GPU + nccl: the native C++ ``Reducer`` owns an RCCL communicator and a high-priority comm
+* GPU + nccl: the native C++ ``Reducer`` owns an RCCL communicator and a normal-priority comm
   stream; ncclAvg in place on the arena slice (fp32) or through a bf16 scratch (``allreduce_dtype``).
 * CPU / gloo (and GPU when ``native=False``): ``torch.distributed.all_reduce(async_op=True)``.
 * ``prepare(sync=False)`` = DDP ``no_sync``: no communication during accumulation micro-batches

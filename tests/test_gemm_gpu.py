@@ -1,12 +1,13 @@
-"""MFMA NT GEMM (gemm.hip) vs an fp32 torch reference, every epilogue, both kernel variants
-(v2 = deep LDS-DMA pipeline, the default for 256-wide tiles with K >= 128; v1 = whole-tile staging)."""
+"""MFMA NT GEMM (gemm.hip) vs an fp32 torch reference, every epilogue, every kernel variant:
+auto (0: the persistent v3 for K <= 2304, v2 above), v1 (whole-tile staging), forced v2 (deep LDS-DMA
+pipeline, also at K <= 2304) and forced v3 (persistent, also at K = 3072)."""
 import pytest
 import torch
 
 from ml_recipe_distributed_pytorch_amd import _native
 
 
-@pytest.fixture(params=[0, 1], ids=["v2", "v1"], autouse=True)
+@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "v1", "v2", "v3"], autouse=True)
 def variant(request):
     if not torch.cuda.is_available():
         yield request.param

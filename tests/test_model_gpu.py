@@ -47,9 +47,7 @@ def _tiny_parity(cuda, train, B, side=False):
     torch.manual_seed(11)
     og = gpu(ids.to(cuda), mask.to(cuda), tt.to(cuda))
     for key in oc:
-        a, b = og[key].float().cpu(), oc[key].float()
-        if key == "cls" and train:
-            continue  # classifier dropout uses torch's (device-specific) RNG
+        a, b = og[key].float().cpu(), oc[key].float()  # classifier dropout: same counter-hash mask on both
         assert (a - b).abs().max().item() < 5e-2 * (1 + b.abs().max().item()), key
     # backward through both paths
     lc = sum(v.float().sum() for k, v in oc.items() if k != "cls")
