@@ -138,7 +138,7 @@ Tensor gemm_nt(Tensor A, Tensor B, int64_t epi, c10::optional<Tensor> bias, c10:
   const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
   TORCH_CHECK(M < (1ll << 31) / 4 && N * K < (1ll << 31) && M * N < (1ll << 40), "gemm_nt: shape too large");
   const int bn = hq_gemm_nt_supported((int)M, (int)N, (int)K);
-  TORCH_CHECK(bn > 0, "gemm_nt: unsupported shape M=", M, " N=", N, " K=", K, " (need M%256, N%128, K%64 == 0)");
+  TORCH_CHECK(bn > 0, "gemm_nt: unsupported shape M=", M, " N=", N, " K=", K, " (need N%128, K%64 == 0)");
   TORCH_CHECK(epi >= HQ_EPI_NONE && epi <= HQ_EPI_DMUL, "gemm_nt: bad epilogue");
   c10::DeviceGuard g(A.device());
   Tensor C = (out.has_value() && out->defined()) ? *out : at::empty({M, N}, A.options());
@@ -162,7 +162,8 @@ Tensor gemm_nt(Tensor A, Tensor B, int64_t epi, c10::optional<Tensor> bias, c10:
   if (epi == HQ_EPI_DGELU || epi == HQ_EPI_DMUL) {
     TORCH_CHECK(part.has_value() && part->defined(), "gemm_nt: part required");
     check(*part, F32, "part");
-    TORCH_CHECK(part->numel() == (M / 256) * N, "gemm_nt: part must hold [M/256, N]");
+    TORCH_CHECK(part->numel() == (int64_t)hq_gemm_nt_part_rows((int)M, (int)N, (int)K) * N,
+                "gemm_nt: part must hold [gemm_nt_part_rows(M, N, K), N]");
   }
   hq_gemm_nt(ptr<uint16_t>(A), ptr<uint16_t>(B), ptr<uint16_t>(C), optr<float>(bias), optr<uint16_t>(pre),
              optr<uint16_t>(resid), optr<float>(part), (int)M, (int)N, (int)K, (int)K, (int)K, (int)N, (int)epi, bn,
@@ -179,9 +180,9 @@ void gemm_tn(Tensor dy, Tensor x, Tensor out, bool accumulate, int64_t splits, c
   const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
   TORCH_CHECK(out.numel() == N * K, "gemm_tn: out must hold N*K");
   const int auto_s = hq_gemm_tn_splits((int)T, (int)N, (int)K);
-  TORCH_CHECK(auto_s > 0, "gemm_tn: unsupported shape T=", T, " N=", N, " K=", K, " (need T%64, N%256, K%256 == 0)");
+  TORCH_CHECK(auto_s > 0, "gemm_tn: unsupported shape T=", T, " N=", N, " K=", K, " (need N%256, K%256 == 0, T >= 128)");
   const int S = splits > 0 ? (int)splits : auto_s;
-  TORCH_CHECK(T / 64 / S >= 2, "gemm_tn: too many splits");
+  TORCH_CHECK((T + 63) / 64 / S >= 2, "gemm_tn: too many splits");
   const bool has_bias = bias_out.has_value() && bias_out->defined();
   if (has_bias) {
     check(*bias_out, F32, "bias_out");
@@ -556,7 +557,11 @@ PYBIND11_MODULE(_hq_kernels, m) {
         py::arg("pre") = py::none(), py::arg("resid") = py::none(), py::arg("part") = py::none(),
         py::arg("out") = py::none());
   m.def("gemm_nt_supported", &gemm_nt_supported);
+  m.def("gemm_nt_part_rows", [](int64_t M, int64_t N, int64_t K) {
+    return (int64_t)hq_gemm_nt_part_rows((int)M, (int)N, (int)K);
+  });
   m.def("gemm_set_variant", [](int64_t v) { hq_gemm_set_variant((int)v); });
+  m.def("gemm_set_stagger", [](int64_t v) { hq_gemm_set_stagger((int)v); });
   m.def("gemm_tn", &gemm_tn, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("accumulate") = false,
         py::arg("splits") = 0, py::arg("bias_out") = py::none());
   m.def("gemm_tn_splits", &gemm_tn_splits);

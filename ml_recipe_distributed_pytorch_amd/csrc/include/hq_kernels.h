@@ -67,11 +67,15 @@ void hq_cast_bf16_f32(const uint16_t* src, float* dst, int64_t n, float scale, h
 
 // ------------------------------------------------------------------ MFMA GEMM (gemm.hip)
 enum { HQ_EPI_NONE = 0, HQ_EPI_BIAS = 1, HQ_EPI_GELU = 2, HQ_EPI_DGELU = 3, HQ_EPI_RESID = 4, HQ_EPI_GELUD = 5, HQ_EPI_DMUL = 6 };
-// returns the block N-width the kernel will use for this shape (256 / 128), 0 = unsupported
+// kernel family for this shape: 256 / 128 = the 256-row kernels with that block width, 1 = the 128²-tile
+// kernel (M tails, low-fill grids), 0 = unsupported (need N % 128 == 0, K % 64 == 0)
 int hq_gemm_nt_supported(int M, int N, int K);
-// 0 = auto (v3 persistent kernel for K <= 2304, v2 deep-pipeline kernel otherwise), 1 = v1 only,
-// 2 = v2 only, 3 = v3 wherever supported (A/B and fallback)
+// rows of the DGELU / DMUL column-partial buffer for this shape ([rows][N])
+int hq_gemm_nt_part_rows(int M, int N, int K);
+// 0 = auto (128² tiles for M % 256 != 0 or < 80 % CU fill; else the persistent v3 kernel for K <= 2304,
+// v2 above), 1 = v1, 2 = v2, 3 = v3 (the 256-row kernels wherever M % 256 == 0), 4 = 128² tiles always
 void hq_gemm_set_variant(int v);
+void hq_gemm_set_stagger(int v);   // v3 start offset of half the workgroups (units of s_sleep(127))
 // C[M,N] = A[M,K]·B[N,K]^T (+epilogue); P = GELU pre-activation (out for EPI_GELU, in for EPI_DGELU)
 // or its derivative gelu'(pre) (out for EPI_GELUD, in for EPI_DMUL);
 // R = residual (EPI_RESID); part = [M/256][N] column partial sums (EPI_DGELU)
@@ -81,7 +85,8 @@ void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
 // Weight-gradient GEMM (gemm_tn.hip): out[N,K] (+)= Aᵀ·B, A = dy [T,N] bf16, B = x [T,K] bf16 (token-major),
 // split-K over T into S fp32 slabs part[S][N][K] (caller-provided) reduced into out; with bout != null
 // also the fused bias gradient bout[N] (+)= Σ_t A[t, n] through slabs bpart[S][N].
-// hq_gemm_tn_splits: the split count for this shape, 0 = unsupported (need T%64, N%256, K%256 == 0).
+// hq_gemm_tn_splits: the split count for this shape, 0 = unsupported (need N%256, K%256 == 0, T >= 128;
+// a token tail T % 64 != 0 stages zero rows through the buffer descriptors' bounds).
 int hq_gemm_tn_splits(int T, int N, int K);
 void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, float* bpart, float* bout, int T, int N, int K,
                 int S, bool accumulate, hipStream_t s);

@@ -274,6 +274,185 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
 
 
 // ============================================================================================
+// vS — 128×128 tiles for the shapes the 256-row kernels do not cover well: M % 256 != 0 (dynamically
+// padded NQ batches, the reference micro-batch of 2 × 512 tokens) and grids that fill the 256 CUs
+// poorly with 256² tiles (batch 64: N = 768 gives 288 tiles = 1.1 waves).  4 waves (2 M × 2 N, 64×64
+// each), two 32 KiB LDS-DMA stages (buffer_load … lds, same source swizzle as the big kernels), so two
+// workgroups share a CU.  The M tail costs nothing extra: the A descriptor's num_records ends at row M,
+// the out-of-range rows stage as zeros, and the epilogue stores only rows < M.  Same epilogues as v1;
+// DGELU / DMUL column partials are per 128-row block (part has ceil(M/128) rows).
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_nts_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                                                          uint16_t* __restrict__ C, const float* __restrict__ bias,
+                                                          uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
+                                                          float* __restrict__ part, int M, int N, int K, int lda, int ldb,
+                                                          int ldc) {
+  constexpr int SB = 128;                  // tile rows = tile cols
+  constexpr int PANEL = SB * 128;          // one operand panel: 128 rows × 64 bf16
+  constexpr int STAGE = 2 * PANEL;
+  constexpr int RS = 64 * 2 + 16;          // epilogue staging row stride (bytes)
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tiles_n = N / SB;
+  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  const int m0 = tm * SB, n0 = tn * SB;
+  const int rows_a = min(SB, M - m0);
+  const int nt = K / BK;
+  HQ_DASSERT(rows_a > 0 && n0 + SB <= N && K % BK == 0);
+
+  const __amdgpu_buffer_rsrc_t ra =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), (short)0, rows_a * lda * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(B + (size_t)n0 * ldb), (short)0, SB * ldb * 2, 0x00020000);
+  int voA[4], voB[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = wave * 32 + i * 8 + (lane >> 3);
+    const int src_slot = (lane & 7) ^ ((row >> 1) & 7);
+    voA[i] = (row * lda + src_slot * 8) * 2;
+    voB[i] = (row * ldb + src_slot * 8) * 2;
+  }
+  auto stage = [&](int t, int buf) {
+    char* base = smem + buf * STAGE + wave_u * 32 * 128;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(base + i * 8 * 128), 16, voA[i], t * BK * 2, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(base + PANEL + i * 8 * 128), 16, voB[i], t * BK * 2, 0, 0);
+  };
+  auto bar = []() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fq = lane >> 4;
+  stage(0, 0);
+  for (int t = 0; t < nt; ++t) {
+    if (t + 1 < nt) {
+      stage(t + 1, (t + 1) & 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // this wave's 8 pieces of stage t landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    bar();                                               // ... and every other wave's
+    const char* pa = smem + (t & 1) * STAGE;
+    const char* pb = pa + PANEL;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t af[4], bf[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = frag(pb, wn * 64 + j * 16 + fr, ks * 4 + fq);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = frag(pa, wm * 64 + i * 16 + fr, ks * 4 + fq);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bf[j], af[i], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();                                               // WAR: stage t+2 reuses this buffer
+  }
+
+  // ---- epilogue: acc (+bias) -> bf16 in this wave's LDS region [64][64], then row-coalesced 16-B pieces
+  char* wreg = smem + wave * 64 * RS;
+  constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int nl = j * 16 + fq * 4;
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + wn * 64 + nl);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
+      *reinterpret_cast<uint2*>(wreg + (i * 16 + fr) * RS + nl * 2) = hq_pack4(v);
+    }
+  }
+  constexpr int SEGS = 8, ROWS_PER_IT = 64 / SEGS;
+  const int seg = lane % SEGS, rsub = lane / SEGS;
+  const int gcol = n0 + wn * 64 + seg * 8;
+  float csum[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+#pragma unroll 2
+  for (int it = 0; it < 64 / ROWS_PER_IT; ++it) {
+    const int row = it * ROWS_PER_IT + rsub;
+    const int grow = m0 + wm * 64 + row;
+    if (grow >= M) continue;
+    uint4 piece = *reinterpret_cast<const uint4*>(wreg + row * RS + seg * 16);
+    const size_t goff = (size_t)grow * ldc + gcol;
+    if constexpr (EPI == HQ_EPI_GELU) {
+      *reinterpret_cast<uint4*>(P + goff) = piece;
+      float x[8];
+      hq_unpack8(piece, x);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) x[e] = gelu_erf(x[e]);
+      piece = hq_pack8(x);
+    } else if constexpr (EPI == HQ_EPI_GELUD) {
+      float x[8], g[8];
+      hq_unpack8(piece, x);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float c, d;
+        hq_normal_cdf_pdf(x[e], c, d);
+        g[e] = fmaf(x[e], d, c);
+        x[e] *= c;
+      }
+      *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
+      piece = hq_pack8(x);
+    } else if constexpr (EPI == HQ_EPI_DMUL) {
+      float d[8], gd[8];
+      hq_unpack8(piece, d);
+      hq_unpack8(*reinterpret_cast<const uint4*>(P + goff), gd);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { d[e] *= gd[e]; csum[e] += d[e]; }
+      piece = hq_pack8(d);
+    } else if constexpr (EPI == HQ_EPI_DGELU) {
+      float d[8], pr[8];
+      hq_unpack8(piece, d);
+      hq_unpack8(*reinterpret_cast<const uint4*>(P + goff), pr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { d[e] *= gelu_grad(pr[e]); csum[e] += d[e]; }
+      piece = hq_pack8(d);
+    } else if constexpr (EPI == HQ_EPI_RESID) {
+      float d[8], rr[8];
+      hq_unpack8(piece, d);
+      hq_unpack8(*reinterpret_cast<const uint4*>(R + goff), rr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] += rr[e];
+      piece = hq_pack8(d);
+    }
+    *reinterpret_cast<uint4*>(C + goff) = piece;
+  }
+  if constexpr (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      for (int o = SEGS; o < 64; o <<= 1) csum[e] += __shfl_xor(csum[e], o, 64);
+    float* red = reinterpret_cast<float*>(smem + 4 * 64 * RS);  // [2][128], past the staging regions
+    if (rsub == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wm * SB + wn * 64 + seg * 8 + e] = csum[e];
+    }
+    __syncthreads();
+    if (tid < SB) part[(size_t)tm * N + n0 + tid] = red[tid] + red[SB + tid];
+  }
+}
+
+// ============================================================================================
 // v2 — deep LDS-DMA pipeline (CDNA4 playbook §5 "8-phase" structure, re-derived for this tile).
 //
 // Same 256×256×64 tile, 8 waves, swizzle and swapped-operand MFMA as v1, but the K-tile is split
@@ -596,7 +775,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
                                                                uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                                uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
                                                                float* __restrict__ part, int M, int N, int K, int lda,
-                                                               int ldb, int ldc) {
+                                                               int ldb, int ldc, int stagger) {
   constexpr int BN = 256;
   constexpr int PANEL = 256 * 128;
   constexpr int STAGE = 2 * PANEL;
@@ -687,6 +866,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
 
   int tile = id;
   if (tile >= ntiles) return;   // whole workgroup
+  // Phase offset for half of each XCD's workgroups (stagger × 8128 cycles): the tile seams of all CUs
+  // otherwise coincide, and every epilogue's stores / aux loads hit HBM in one chip-wide burst that the
+  // next K-tile's counted wait (vmcnt counts stores too) then stalls on.
+  if (stagger > 0 && ((bid >> 3) & 1))
+    for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(127);
   __amdgpu_buffer_rsrc_t ca = rsrc_a(tile), cb = rsrc_b(tile);
   int p0 = 0;                   // LDS buffer of this tile's K-tile 0
   // prologue of the first tile (as v2): K-tile 0 (A0 B0 B1 A1) and the first two halves of K-tile 1
@@ -884,6 +1068,11 @@ int g_gemm_variant = [] {
   const char* e = getenv("HQ_GEMM_VARIANT");
   return e ? atoi(e) : 0;
 }();
+// v3 start offset of odd workgroups per XCD, in units of s_sleep(127); HQ_GEMM_STAGGER sets it
+int g_gemm_stagger = [] {
+  const char* e = getenv("HQ_GEMM_STAGGER");
+  return e ? atoi(e) : 0;
+}();
 
 constexpr size_t epi_lds(int bn) {
   const size_t stage = 2 * (size_t)(BM * 128 + bn * 128);
@@ -894,6 +1083,18 @@ constexpr size_t epi_lds(int bn) {
 template <int EPI>
 void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,
                 float* part, int M, int N, int K, int lda, int ldb, int ldc, int bn, hipStream_t s) {
+  if (bn == 1) {   // vS: 128×128 tiles, M tail
+    constexpr size_t lds = 2 * 2 * 128 * 128;
+    static bool init = [] {
+      (void)hipFuncSetAttribute((const void*)gemm_nts_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      return true;
+    }();
+    (void)init;
+    const int grid_s = ((M + 127) / 128) * (N / 128);
+    hipLaunchKernelGGL((gemm_nts_kernel<EPI>), dim3(grid_s), dim3(256), lds, s, A, B, C, bias, P, R, part, M, N, K, lda,
+                       ldb, ldc);
+    return;
+  }
   const int grid = (M / BM) * (N / bn);
   const bool srd_ok = (size_t)BM * lda * 2 < (1ull << 31) && (size_t)256 * ldb * 2 < (1ull << 31);
   // v3 (persistent, pipelined across tiles) where the per-tile fixed cost matters: K <= 2304 (+2-6 % at
@@ -909,7 +1110,7 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
       return n > 0 ? n : 256;
     }();
     hipLaunchKernelGGL((gemm_nt3_kernel<EPI>), dim3(std::min(grid, ncu)), dim3(kThreads), lds, s, A, B, C, bias, P, R, part,
-                       M, N, K, lda, ldb, ldc);
+                       M, N, K, lda, ldb, ldc, g_gemm_stagger);
   } else if (bn == 256 && (g_gemm_variant == 0 || g_gemm_variant == 2 || g_gemm_variant == 3) && K >= 2 * BK && srd_ok) {
     // production v2: buffer_load…lds staging (+8-12 % over global_load_lds on the BERT shapes,
     // tools/gemm_lab); grouped 8-row-panel tile order only for wide N (+15 % at 8192², neutral at
@@ -951,12 +1152,30 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
 }  // namespace
 
 void hq_gemm_set_variant(int v) { g_gemm_variant = v; }
+void hq_gemm_set_stagger(int v) { g_gemm_stagger = v; }
 
+// Kernel family for a shape: 256 / 128 = the 256-row kernels with that block width, 1 = vS (128² tiles),
+// 0 = unsupported.  Variants 1-3 force the 256-row kernels where they apply, 4 forces vS; auto takes the
+// 256-row kernels when M % 256 == 0 and their grid fills >= 80 % of the CUs' last wave, else vS.
 int hq_gemm_nt_supported(int M, int N, int K) {
-  if (M % BM || K % BK || K < BK) return 0;
-  if (N % 256 == 0) return 256;
-  if (N % 128 == 0) return 128;
-  return 0;
+  if (M <= 0 || K % BK || K < BK || N % 128) return 0;
+  const int big = (M % BM == 0) ? (N % 256 == 0 ? 256 : 128) : 0;
+  if (g_gemm_variant == 4 || !big) return 1;
+  if (g_gemm_variant != 0) return big;
+  static int ncu = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  const long tiles = (long)(M / BM) * (N / big);
+  const long waves = (tiles + ncu - 1) / ncu;
+  return tiles * 5 >= waves * ncu * 4 ? big : 1;
+}
+
+int hq_gemm_nt_part_rows(int M, int N, int K) {
+  const int k = hq_gemm_nt_supported(M, N, K);
+  return k == 1 ? (M + 127) / 128 : M / BM;
 }
 
 void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,

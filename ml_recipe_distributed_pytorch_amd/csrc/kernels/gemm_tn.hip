@@ -74,15 +74,16 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const uint16_t* __
   const int tiles = nwg / S;
   const int split = id / tiles, tile = id % tiles;
   const int n0 = (tile / tiles_k) * 256, k0 = (tile % tiles_k) * 256;
-  const int nkt = T / BT;
+  const int nkt = (T + BT - 1) / BT;      // a partial last K-tile (T % 64 != 0) stages zero rows
   const int kt0 = (int)((long)split * nkt / S), kt1 = (int)((long)(split + 1) * nkt / S);
   const int nt = kt1 - kt0;
-  HQ_DASSERT(n0 + 256 <= N && k0 + 256 <= K && nt >= 2);
+  const int rows = min(nt * BT, T - kt0 * BT);  // tokens of this split that exist: the descriptors end there
+  HQ_DASSERT(n0 + 256 <= N && k0 + 256 <= K && nt >= 2 && rows > 0);
 
   const uint16_t* Ab = A + (size_t)kt0 * BT * N + n0;
   const uint16_t* Bb = B + (size_t)kt0 * BT * K + k0;
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, nt * BT * N * 2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, nt * BT * K * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, rows * N * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, rows * K * 2, 0x00020000);
 
   // staging: wave w moves rows (2w + i)·4 … +3 of a half (1 KiB per instruction, lane-linear:
   // lane L → row +L/16, 16-B slot L%16), loading the source chunk that the swizzle places there
@@ -266,12 +267,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float4* __rest
 }  // namespace
 
 int hq_gemm_tn_splits(int T, int N, int K) {
-  if (T % BT || N % 256 || K % 256 || N < 256 || K < 256) return 0;
+  if (T <= 0 || N % 256 || K % 256 || N < 256 || K < 256) return 0;
   if ((size_t)T * N * 2 >= (1ull << 31) || (size_t)T * K * 2 >= (1ull << 31)) return 0;
   const int tiles = (N / 256) * (K / 256);
   int S = 256 / tiles;                     // one full round of the 256 CUs
   if (S < 1) S = 1;
-  const int nkt = T / BT;
+  const int nkt = (T + BT - 1) / BT;
   while (S > 1 && nkt / S < 8) --S;        // keep >= 8 K-tiles per block (prologue amortised)
   if (nkt < 2) return 0;
   return S;

@@ -93,8 +93,8 @@ def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale
 #   HQ_GEMM=auto (default): the GEMMs whose epilogue fuses an elementwise pass — FFN1 + GELU,
 #     FFN2-dgrad + dGELU + FFN1 bias-grad (1.08x / 1.40x vs hipBLASLt + separate kernel at b256,
 #     profiles/) and the QKV dgrad + residual-gradient add (torch.addmm first copies the residual
-#     into the output: +56 µs at b256), plus the plain dgrads — when the 256-row tile grid fills the
-#     256 CUs to >= 85 %.  Weight gradients always take the split-K TN kernel (gemm_tn.hip).
+#     into the output: +56 µs at b256), plus the plain dgrads, for every M (gemm.hip picks 256-row or
+#     128² tiles by M alignment and CU fill).  Weight gradients take the split-K TN kernel (gemm_tn.hip).
 #     Plain forward projections follow FWD_MFMA below (all three on the MFMA kernel by default);
 #   HQ_GEMM=mfma: every supported shape;  HQ_GEMM=blas: none.
 _EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID, _EPI_GELUD, _EPI_DMUL = range(7)
@@ -106,7 +106,6 @@ _GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
 # GEMMs stay in torch).
 FWD_MFMA = {k for k in os.environ.get("HQ_FWD_MFMA", "qkv,out,ffn2").split(",") if k}
 GELU_DERIV = os.environ.get("HQ_GELU_DERIV", "1") == "1"   # FFN1 stores gelu'(pre) (linear_gelu_fwd_d)
-_CUS = 256
 
 
 def set_gemm_mode(mode: str) -> str:
@@ -117,18 +116,21 @@ def set_gemm_mode(mode: str) -> str:
 
 
 def _mfma(M: int, N: int, K: int, kind: str = "plain") -> bool:
+    """Every projection shape with N % 128 == 0 and K % 64 == 0 runs on the own MFMA kernels: the
+    256-row kernels where M % 256 == 0 and the grid fills the CUs, the 128²-tile kernel otherwise
+    (M tails of dynamically padded batches, small micro-batches, low-fill grids) — gemm.hip picks."""
     if _GEMM_MODE == "blas":
         return False
-    bn = _k().gemm_nt_supported(int(M), int(N), int(K))
-    if bn <= 0:
+    if _k().gemm_nt_supported(int(M), int(N), int(K)) <= 0:
         return False
     if _GEMM_MODE == "mfma":
         return True
-    tiles = (M // 256) * (N // bn)
-    fill = tiles / (-(-tiles // _CUS) * _CUS)
-    # plain dgrads (dy·W through the Wᵀ copy): v2 is 1.04x hipBLASLt's NT kernel on long K and beats the
-    # NN kernel torch.mm(dy, W) dispatches at K = 768 (123 vs 136 µs at b256, profiles/s2_*)
-    return fill >= 0.85 and (kind in ("dgelu", "gelu", "resid", "dgrad") or kind in FWD_MFMA)
+    return kind in ("dgelu", "gelu", "resid", "dgrad") or kind in FWD_MFMA
+
+
+def _part(M: int, N: int, K: int, device):
+    """Column-partial buffer of a DGELU / DMUL GEMM (one row per M-block of the kernel that runs)."""
+    return torch.empty(_k().gemm_nt_part_rows(int(M), int(N), int(K)), N, dtype=torch.float32, device=device)
 
 
 def linear_fwd(x, w, b, b32=None, kind: str = "plain"):
@@ -238,7 +240,7 @@ def linear_dgrad_gelu_d(dy, w, saved, is_deriv, g_bias, accumulate, wt=None):
         return linear_dgrad_gelu(dy, w, saved, g_bias, accumulate, wt)
     M, N = dy.shape[0], w.shape[1]
     assert wt is not None, "stored-derivative GELU backward needs the MFMA path (Wᵀ working copy)"
-    part = torch.empty(M // 256, N, dtype=torch.float32, device=dy.device)
+    part = _part(M, N, dy.shape[1], dy.device)
     dpre = _k().gemm_nt(dy, wt, _EPI_DMUL, pre=saved, part=part)
     if g_bias is not None:
         _k().colsum_into(part, g_bias, bool(accumulate))
@@ -268,7 +270,7 @@ def linear_dgrad_gelu(dy, w, pre, g_bias, accumulate, wt=None):
     fused with the GELU backward and the bias gradient of the layer before it."""
     if dy.is_cuda and wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1], "dgelu"):
         M, N = dy.shape[0], w.shape[1]
-        part = torch.empty(M // 256, N, dtype=torch.float32, device=dy.device)
+        part = _part(M, N, dy.shape[1], dy.device)
         dpre = _k().gemm_nt(dy, wt, _EPI_DGELU, pre=pre, part=part)
         if g_bias is not None:
             _k().colsum_into(part, g_bias, bool(accumulate))

@@ -1,13 +1,14 @@
 """MFMA NT GEMM (gemm.hip) vs an fp32 torch reference, every epilogue, every kernel variant:
-auto (0: the persistent v3 for K <= 2304, v2 above), v1 (whole-tile staging), forced v2 (deep LDS-DMA
-pipeline, also at K <= 2304) and forced v3 (persistent, also at K = 3072)."""
+auto (0: 128² tiles for M tails / low CU fill, else the persistent v3 for K <= 2304 and v2 above),
+v1 (whole-tile staging), forced v2 (deep LDS-DMA pipeline, also at K <= 2304), forced v3 (persistent,
+also at K = 3072) and forced vS (the 128²-tile kernel everywhere)."""
 import pytest
 import torch
 
 from ml_recipe_distributed_pytorch_amd import _native
 
 
-@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "v1", "v2", "v3"], autouse=True)
+@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["auto", "v1", "v2", "v3", "vS"], autouse=True)
 def variant(request):
     if not torch.cuda.is_available():
         yield request.param
@@ -40,7 +41,7 @@ def test_gemm_nt_plain_and_bias(cuda, M, N, K):
     A = torch.randn(M, K, device=cuda, generator=g).bfloat16()
     B = torch.randn(N, K, device=cuda, generator=g).bfloat16()
     bias = torch.randn(N, device=cuda, generator=g)
-    assert k.gemm_nt_supported(M, N, K) in (128, 256)
+    assert k.gemm_nt_supported(M, N, K) in (1, 128, 256)
     _close(k.gemm_nt(A, B, EPI_NONE), _ref(A, B))
     _close(k.gemm_nt(A, B, EPI_BIAS, bias=bias), _ref(A, B) + bias)
 
@@ -70,7 +71,7 @@ def test_gemm_nt_gelu_dgelu_resid(cuda, M, N, K):
     _close(pre, ref_pre)
     _close(act, torch.nn.functional.gelu(pre.float()))
     # dgelu: C = (A·Bᵀ) * gelu'(pre), part = column sums per 256-row block
-    part = torch.empty(M // 256, N, device=cuda)
+    part = torch.empty(k.gemm_nt_part_rows(M, N, K), N, device=cuda)
     d = k.gemm_nt(A, B, EPI_DGELU, pre=pre, part=part)
     x = pre.float().requires_grad_(True)
     torch.nn.functional.gelu(x).backward(_ref(A, B).bfloat16().float())
@@ -84,10 +85,55 @@ def test_gemm_nt_gelu_dgelu_resid(cuda, M, N, K):
 def test_gemm_nt_rejects_bad_shapes(cuda):
     k = _native.kernels()
     A = torch.randn(100, 64, device=cuda).bfloat16()
-    B = torch.randn(128, 64, device=cuda).bfloat16()
-    assert k.gemm_nt_supported(100, 128, 64) == 0
+    B = torch.randn(100, 64, device=cuda).bfloat16()
+    assert k.gemm_nt_supported(100, 100, 64) == 0    # N % 128 != 0
+    assert k.gemm_nt_supported(100, 128, 96) == 0    # K % 64 != 0
     with pytest.raises(RuntimeError):
         k.gemm_nt(A, B, EPI_NONE)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(100, 256, 64), (1000, 768, 768), (1152, 768, 3072), (4 * 317, 2304, 768),
+                                   (24576, 768, 768)])
+def test_gemm_nt_m_tail_and_low_fill_all_epilogues(cuda, M, N, K, variant):
+    """M % 256 != 0 (dynamically padded batches: 4 × 317 tokens; the reference micro-batch 2 × 512 = 1024
+    is aligned but fills 12 tiles) and the batch-64 low-fill grid (24576 × 768) on the 128²-tile kernel,
+    every epilogue; rows past M must stay untouched."""
+    if variant not in (0, 4):
+        pytest.skip("the 256-row kernels need M % 256 == 0")
+    EPI_GELUD, EPI_DMUL = 5, 6
+    k = _native.kernels()
+    assert k.gemm_nt_supported(M, N, K) == 1 or (M % 256 == 0 and variant == 0)
+    g = torch.Generator(device=cuda).manual_seed(M + N)
+    A = (torch.randn(M, K, device=cuda, generator=g) * 0.5).bfloat16()
+    B = (torch.randn(N, K, device=cuda, generator=g) * 0.1).bfloat16()
+    bias = torch.randn(N, device=cuda, generator=g) * 0.1
+    ref = _ref(A, B)
+    big = torch.full((M + 64, N), 7.0, device=cuda, dtype=torch.bfloat16)
+    out = big[:M]
+    k.gemm_nt(A, B, EPI_BIAS, bias=bias, out=out)
+    _close(out, ref + bias)
+    assert torch.equal(big[M:].float(), torch.full((64, N), 7.0, device=cuda)), "rows past M were written"
+    _close(k.gemm_nt(A, B, EPI_NONE), ref)
+    resid = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+    _close(k.gemm_nt(A, B, EPI_RESID, resid=resid), ref + resid.float())
+    pre = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    act = k.gemm_nt(A, B, EPI_GELU, bias=bias, pre=pre)
+    _close(pre, ref + bias)
+    _close(act, torch.nn.functional.gelu(pre.float()))
+    rows = k.gemm_nt_part_rows(M, N, K)
+    part = torch.empty(rows, N, device=cuda)
+    d = k.gemm_nt(A, B, EPI_DGELU, pre=pre, part=part)
+    x = pre.float().requires_grad_(True)
+    torch.nn.functional.gelu(x).backward(ref.bfloat16().float())
+    _close(d, x.grad)
+    torch.testing.assert_close(part.sum(0), d.float().sum(0), atol=5e-2 * (1 + d.float().abs().sum(0).max().item() / M),
+                               rtol=2e-2)
+    gd = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    act2 = k.gemm_nt(A, B, EPI_GELUD, bias=bias, pre=gd)
+    _close(act2, act.float())
+    dm = k.gemm_nt(A, B, EPI_DMUL, pre=gd, part=part)
+    _close(dm, ref.bfloat16().float() * gd.float())
 
 
 @pytest.mark.gpu
@@ -107,10 +153,10 @@ def test_gemm_nt_repeatable_large(cuda, M, N, K):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("T,N,K", [(128, 256, 256), (1024, 768, 256), (4096, 2304, 768), (2048, 768, 3072),
-                                   (24576, 768, 768)])
+                                   (24576, 768, 768), (4 * 317, 768, 768), (200, 256, 512), (24576 - 37, 3072, 768)])
 def test_gemm_tn_wgrad(cuda, T, N, K, variant):
     """dW = dyᵀ·x (split-K TN kernel, fp32 out) vs fp32 torch, default and forced split counts,
-    plain and accumulating; bitwise repeatable."""
+    plain and accumulating; bitwise repeatable; token tails (T % 64 != 0) included."""
     if variant:
         pytest.skip("TN kernel has a single variant")
     k = _native.kernels()
@@ -180,7 +226,7 @@ def test_gemm_nt_gelu_derivative_epilogues(cuda, M, N, K):
     y.backward(torch.ones_like(y))
     _close(act, y.detach())
     _close(gd, x.grad, tol=1e-2)
-    part = torch.empty(M // 256, N, device=cuda)
+    part = torch.empty(k.gemm_nt_part_rows(M, N, K), N, device=cuda)
     d = k.gemm_nt(A, B, EPI_DMUL, pre=gd, part=part)
     exp = _ref(A, B).bfloat16().float() * gd.float()
     _close(d, exp)

@@ -42,7 +42,7 @@ def main():
         bias = torch.rand(N, device=dev)
         P = torch.randn(T, N, device=dev).bfloat16()
         R = torch.randn(T, N, device=dev).bfloat16()
-        part = torch.empty(T // 256, N, device=dev)
+        part = torch.empty(k.gemm_nt_part_rows(T, N, K), N, device=dev)
         C = torch.empty(T, N, device=dev, dtype=torch.bfloat16)
         fl = 2.0 * T * N * K
         for name in epis:

@@ -87,7 +87,7 @@ def main():
         bias = torch.rand(N, device=dev)
         P = torch.randn(T, N, device=dev).bfloat16()
         R = torch.randn(T, N, device=dev).bfloat16()
-        part = torch.empty(T // 256, N, device=dev)
+        part = torch.empty(k.gemm_nt_part_rows(T, N, K), N, device=dev)
         fl = 2.0 * T * N * K
         for name in epis:
             e = EPI[name]

@@ -68,7 +68,7 @@ def main():
             pre = (torch.randn(T, N, device=dev)).bfloat16()
             gb = torch.zeros(N, device=dev)
             Bt = B.t().contiguous()
-            part = torch.empty(T // 256, N, device=dev)
+            part = torch.empty(k.gemm_nt_part_rows(T, N, K), N, device=dev)
             if "gelu" in name and "dgelu" not in name:
                 P = torch.empty(T, N, device=dev, dtype=torch.bfloat16)
                 ours = lambda: k.gemm_nt(A, B, 2, bias=bias, pre=P)
