@@ -90,17 +90,28 @@ void embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tenso
 }
 
 // ------------------------------------------------------------------ residual + dropout + LayerNorm
-std::vector<Tensor> ln_fwd(Tensor a, Tensor resid, Tensor gamma, Tensor beta, double eps, double p, int64_t seed, int64_t opid) {
+// With q8 (f32[4] delayed-scaling state of the consuming fp8 GEMM's input): also returns y as e4m3.
+std::vector<Tensor> ln_fwd(Tensor a, Tensor resid, Tensor gamma, Tensor beta, double eps, double p, int64_t seed, int64_t opid,
+                           c10::optional<Tensor> q8, int64_t phase) {
   check(a, BF16, "a"); check(resid, BF16, "resid"); check(gamma, F32, "gamma"); check(beta, F32, "beta");
   TORCH_CHECK(a.dim() == 2 && a.sizes() == resid.sizes(), "a/resid shape");
   const int64_t T = a.size(0), H = a.size(1);
   TORCH_CHECK(gamma.numel() == H && beta.numel() == H && H % 4 == 0 && H <= 2048, "hidden size");
   TORCH_CHECK(T * H < (int64_t)std::numeric_limits<uint32_t>::max(), "T*H exceeds 32-bit dropout index");
+  const bool want8 = q8.has_value() && q8->defined();
+  if (want8) {
+    check(*q8, F32, "q8");
+    TORCH_CHECK(q8->numel() == 4, "q8 must be the f32[4] delayed-scaling state");
+  }
   c10::DeviceGuard g(a.device());
   auto y = at::empty_like(a), z = at::empty_like(a);
   auto mean = at::empty({T}, gamma.options()), rstd = at::empty({T}, gamma.options());
+  Tensor y8 = want8 ? at::empty({T, H}, a.options().dtype(at::kFloat8_e4m3fn)) : Tensor();
   hq_ln_fwd(ptr<uint16_t>(a), ptr<uint16_t>(resid), ptr<float>(gamma), ptr<float>(beta), ptr<uint16_t>(y), ptr<uint16_t>(z),
-            ptr<float>(mean), ptr<float>(rstd), (int)T, (int)H, (float)eps, (float)p, u32(seed), u32(opid), cur_stream());
+            ptr<float>(mean), ptr<float>(rstd), (int)T, (int)H, (float)eps, (float)p, u32(seed), u32(opid), cur_stream(),
+            want8 ? reinterpret_cast<uint8_t*>(y8.data_ptr()) : nullptr, want8 ? ptr<float>(*q8) : nullptr,
+            (int)(phase % 3));
+  if (want8) return {y, z, mean, rstd, y8};
   return {y, z, mean, rstd};
 }
 
@@ -550,7 +561,8 @@ PYBIND11_MODULE(_hq_kernels, m) {
         py::arg("wp"), py::arg("wt"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"), py::arg("p"), py::arg("seed"),
         py::arg("opid"), py::arg("g_word"), py::arg("g_pos"), py::arg("g_type"), py::arg("g_gamma"), py::arg("g_beta"),
         py::arg("accumulate"), py::arg("pad_word"), py::arg("pad_pos"), py::arg("seq_len") = 0);
-  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_fwd", &ln_fwd, py::arg("a"), py::arg("resid"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("p"),
+        py::arg("seed"), py::arg("opid"), py::arg("q8") = py::none(), py::arg("phase") = 0);
   m.def("ln_bwd", &ln_bwd);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("epi"), py::arg("bias") = py::none(),

@@ -14,8 +14,10 @@ struct HqOuts {  // up to 4 fp32 column-sum destinations (null = skip), passed b
 // ---- norm.hip --------------------------------------------------------------------------------
 int hq_ln_bwd_partials(int T);
 int hq_rowblock_partials(int T);
+// y8 != null (fp8 path): y also as e4m3 under the delayed-scaling state q8 [4] at `phase` (see hq_common.h)
 void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, const float* beta, uint16_t* y, uint16_t* z,
-               float* mean, float* rstd, int T, int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s);
+               float* mean, float* rstd, int T, int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s,
+               uint8_t* y8 = nullptr, float* q8 = nullptr, int phase = 0);
 void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const float* gamma, const float* mean,
                const float* rstd, uint16_t* dz, uint16_t* da, float* part, HqOuts outs, int T, int H, float p,
                uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s);

@@ -763,6 +763,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
 // EPI-dependent, all issued between the next tile's K-tile-0 halves and its K-tile-1 halves) are
 // counted into the first K-tile's vmcnt waits.  Raw barriers only (a __syncthreads fence would drain
 // the in-flight DMA).
+// Epilogue A/B knobs (HQ_GEMM_EPIFLAGS, v3 only): nontemporal stores of P / C; diagnostics that drop the
+// GELU math or every store (values kept alive) to price the epilogue's parts.
+constexpr int kNtP = 1, kNtC = 2, kDbgNoMath = 4, kDbgNoStore = 8;
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store16(uint16_t* dst, const uint4& v, int nt) {
+  if (nt) {
+    const u32x4_t w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(dst));
+  } else {
+    *reinterpret_cast<uint4*>(dst) = v;
+  }
+}
+
 template <int EPI>
 struct NT3Epi {
   static constexpr int kStores = 16 * (1 + (EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD ? 1 : 0));
@@ -785,6 +798,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   constexpr int SPARE = 2 * STAGE;           // past both stage buffers: wave 7's region, then csum scratch
   constexpr int E = NT3Epi<EPI>::E;
   static_assert(7 * REGION <= STAGE && SPARE + REGION + 2 * BN * 4 <= 160 * 1024, "LDS plan");
+  const int epi_flags = stagger >> 8;   // HQ_GEMM_EPIFLAGS (A/B knobs; 0 in production)
+  stagger &= 0xFF;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1002,17 +1017,23 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
           for (int e = 0; e < 8; ++e) x[e] = gelu_erf(x[e]);
           piece = hq_pack8(x);
         } else if constexpr (EPI == HQ_EPI_GELUD) {
-          float x[8], g[8];
-          hq_unpack8(piece, x);
+          if (epi_flags & kDbgNoMath) {   // diagnostic: stores only
+            if (!(epi_flags & kDbgNoStore)) store16(P + goff, piece, epi_flags & kNtP);
+          } else {
+            float x[8], g[8];
+            hq_unpack8(piece, x);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            float c, d;
-            hq_normal_cdf_pdf(x[e], c, d);
-            g[e] = fmaf(x[e], d, c);
-            x[e] *= c;
+            for (int e = 0; e < 8; ++e) {
+              float c, d;
+              hq_normal_cdf_pdf(x[e], c, d);
+              g[e] = fmaf(x[e], d, c);
+              x[e] *= c;
+            }
+            const uint4 gp = hq_pack8(g);
+            if (!(epi_flags & kDbgNoStore)) store16(P + goff, gp, epi_flags & kNtP);
+            else asm volatile("" :: "v"(gp.x), "v"(gp.y), "v"(gp.z), "v"(gp.w));
+            piece = hq_pack8(x);
           }
-          *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
-          piece = hq_pack8(x);
         } else if constexpr (EPI == HQ_EPI_DMUL) {
           float d[8], gd[8];
           hq_unpack8(piece, d);
@@ -1035,7 +1056,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
           for (int e = 0; e < 8; ++e) d[e] += rr[e];
           piece = hq_pack8(d);
         }
-        *reinterpret_cast<uint4*>(C + goff) = piece;
+        if (!(epi_flags & kDbgNoStore)) store16(C + goff, piece, epi_flags & kNtC);
+        else asm volatile("" :: "v"(piece.x), "v"(piece.y), "v"(piece.z), "v"(piece.w));
       }
     }
     if constexpr (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL) {
@@ -1068,10 +1090,12 @@ int g_gemm_variant = [] {
   const char* e = getenv("HQ_GEMM_VARIANT");
   return e ? atoi(e) : 0;
 }();
-// v3 start offset of odd workgroups per XCD, in units of s_sleep(127); HQ_GEMM_STAGGER sets it
+// v3 start offset of odd workgroups per XCD, in units of s_sleep(127) (HQ_GEMM_STAGGER, bits 0-7) and
+// the epilogue A/B knobs (HQ_GEMM_EPIFLAGS, bits 8-15); both 0 in production
 int g_gemm_stagger = [] {
   const char* e = getenv("HQ_GEMM_STAGGER");
-  return e ? atoi(e) : 0;
+  const char* f = getenv("HQ_GEMM_EPIFLAGS");
+  return (e ? atoi(e) & 0xFF : 0) | ((f ? atoi(f) & 0xFF : 0) << 8);
 }();
 
 constexpr size_t epi_lds(int bn) {

@@ -55,8 +55,8 @@ __device__ __forceinline__ i32x8 frag32(uint32_t panel, int row, int fq) {
 }
 
 __device__ __forceinline__ float delayed_scale(const float* st, int phase) {
-  const float prev = __uint_as_float(reinterpret_cast<const unsigned*>(st)[(phase + 2) % 3]);
-  return prev > 0.f ? prev * kMargin / kFp8Max : 1.f;   // first step: unit scale
+  static_assert(kMargin == 2.f && kFp8Max == kHqFp8Max, "one delayed-scaling rule (hq_common.h)");
+  return hq_fp8_delayed_scale(st, phase);   // first step: unit scale
 }
 
 template <int EPI, bool Q8>

@@ -20,15 +20,24 @@ namespace {
 constexpr int kRowsPerWave = 8;   // rows a wave walks in the backward kernels
 constexpr int kWaves = 4;         // 256-thread blocks
 
-template <int NCH>
+// Q8 (--precision fp8): y is also written as e4m3 under the delayed scale of the consuming GEMM's input
+// state q8 (the next QKV / FFN1 projection reads it instead of a separate quantisation pass over y);
+// grid-stride rows so the amax needs one atomic per block (<= 2048 per call).
+template <int NCH, bool Q8>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict__ a, const uint16_t* __restrict__ resid,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      uint16_t* __restrict__ y, uint16_t* __restrict__ z,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out, int T,
-                                                     int H, float eps, uint32_t key, uint32_t thr, float kscale) {
+                                                     int H, float eps, uint32_t key, uint32_t thr, float kscale,
+                                                     uint8_t* __restrict__ y8, float* __restrict__ q8, int phase) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int row = blockIdx.x * kWaves + wave;
-  if (row >= T) return;
+  float amax = 0.f, inv8 = 1.f, s8 = 1.f;
+  if constexpr (Q8) {
+    s8 = hq_fp8_delayed_scale(q8, phase);
+    inv8 = 1.f / s8;
+  }
+  const int stride = Q8 ? gridDim.x * kWaves : T;
+  for (int row = blockIdx.x * kWaves + wave; row < T; row += stride) {
   const size_t base = (size_t)row * H;
   float v[NCH][4];
   float sum = 0.f;
@@ -72,10 +81,32 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict_
       const float4 b = *reinterpret_cast<const float4*>(beta + col);
       float o[4] = {(v[c][0] - mean) * rstd * g.x + b.x, (v[c][1] - mean) * rstd * g.y + b.y,
                     (v[c][2] - mean) * rstd * g.z + b.z, (v[c][3] - mean) * rstd * g.w + b.w};
-      *reinterpret_cast<uint2*>(y + base + col) = hq_pack4(o);
+      const uint2 packed = hq_pack4(o);
+      *reinterpret_cast<uint2*>(y + base + col) = packed;
+      if constexpr (Q8) {
+        hq_unpack4(packed, o);   // quantise the bf16-rounded y, exactly what the bf16 copy holds
+#pragma unroll
+        for (int i = 0; i < 4; ++i) amax = fmaxf(amax, fabsf(o[i]));
+        *reinterpret_cast<uint32_t*>(y8 + base + col) = hq_pack_fp8x4(o, inv8);
+      }
     }
   }
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
+  }
+  if constexpr (Q8) {
+    __shared__ float red[kWaves];
+    amax = hq_wave_max(amax);
+    if (lane == 0) red[wave] = amax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      atomicMax(reinterpret_cast<unsigned*>(q8) + phase, __float_as_uint(m));
+      if (blockIdx.x == 0) {
+        reinterpret_cast<unsigned*>(q8)[(phase + 1) % 3] = 0u;   // cleared for the step after next
+        q8[3] = s8;                                              // dequant scale of this step's y8
+      }
+    }
+  }
 }
 
 // Reduce NQ per-lane column accumulators over the 4 waves of the block into part[block][q][H].
@@ -647,13 +678,19 @@ void colsum(const float* part, int P, int N, HqOuts outs, int Hq, bool accumulat
 
 // ================================================================================== launchers
 void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, const float* beta, uint16_t* y, uint16_t* z,
-               float* mean, float* rstd, int T, int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s) {
+               float* mean, float* rstd, int T, int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s,
+               uint8_t* y8, float* q8, int phase) {
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const uint32_t key = hq_op_key(seed, opid);
   const float ks = hq_keep_scale(thr);
+  const int blocks = (T + kWaves - 1) / kWaves;
   dispatch_nch(H, [&](auto nch) {
-    hipLaunchKernelGGL(ln_fwd_kernel<decltype(nch)::value>, dim3((T + kWaves - 1) / kWaves), dim3(256), 0, s, a, resid,
-                       gamma, beta, y, z, mean, rstd, T, H, eps, key, thr, ks);
+    if (y8)
+      hipLaunchKernelGGL((ln_fwd_kernel<decltype(nch)::value, true>), dim3(std::min(blocks, 2048)), dim3(256), 0, s, a,
+                         resid, gamma, beta, y, z, mean, rstd, T, H, eps, key, thr, ks, y8, q8, phase);
+    else
+      hipLaunchKernelGGL((ln_fwd_kernel<decltype(nch)::value, false>), dim3(blocks), dim3(256), 0, s, a, resid, gamma,
+                         beta, y, z, mean, rstd, T, H, eps, key, thr, ks, nullptr, nullptr, 0);
   });
 }
 

@@ -114,6 +114,7 @@ class _Ctx:
 
     def __init__(self, B, L, seed, training, model):
         self.B, self.L, self.seed, self.training, self.model = B, L, seed, training, model
+        self.x8 = {}   # fp8 path: layer index -> its QKV input in e4m3 (written by the previous layer's LN)
 
 
 class _EmbeddingFn(torch.autograd.Function):
@@ -176,39 +177,49 @@ class _LayerFn(torch.autograd.Function):
         def proj(inp, name):  # bf16 forward projection
             return ops.linear_fwd(inp, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), kinds[name])
 
-        # --precision fp8 (BASELINE config #5): QKV and FFN2 on hipBLASLt's fp8 GEMM with one-pass
-        # delayed-scaling quantisation of their inputs, FFN1 on the own block-scaled MFMA kernel whose
-        # epilogue also emits FFN2's e4m3 input; the out-projection stays bf16 (its separate input
-        # quantisation would cost what the fp8 GEMM saves).  Backward GEMMs are bf16 throughout.
+        # --precision fp8 (BASELINE config #5): QKV, FFN1 and FFN2 run on the own block-scaled fp8 MFMA
+        # kernel (gemm_fp8.hip) with e4m3 inputs written by their PRODUCERS under delayed scaling — QKV's by
+        # the previous layer's second LayerNorm (layer 0: one quantisation pass over the embeddings), FFN1's
+        # by this layer's first LayerNorm, FFN2's by FFN1's epilogue — so no standalone quantiser runs per
+        # layer.  The out-projection stays bf16 (its input, the attention context, would need its own pass:
+        # about what the fp8 GEMM saves).  Backward GEMMs are bf16 throughout.
+        fp8 = fp8 and ops.fp8_gemm_ok(x.shape[0], 3 * cfg.hidden_size, cfg.hidden_size)
         s8 = m.fp8_states(idx) if fp8 else None
-        qkv = ops.linear_fwd_fp8_delayed(x, W8("qkv"), Bb("qkv"), s8["qkv"]) if fp8 else proj(x, "qkv")
+        if fp8:
+            x8 = info.x8.pop(idx, None)
+            if x8 is None:
+                x8 = s8["qkv"].quantize(x)
+            qkv = ops.linear_fwd_fp8_own(x8, s8["qkv"], W8("qkv"), Bm("qkv.bias"))
+        else:
+            qkv = proj(x, "qkv")
         ctxv, lse, bits = ops.attn_fwd(qkv, key_bias, B, L, nh, pa, info.seed, op0, scale)
         a1 = proj(ctxv, "attention.output.dense")
-        h1, z1, m1, r1 = ops.ln_fwd(a1, x, st.view(p + "attention.output.LayerNorm.weight", "master"),
-                                    st.view(p + "attention.output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph,
-                                    info.seed, op0 + 1)
+        ln1 = (st.view(p + "attention.output.LayerNorm.weight", "master"),
+               st.view(p + "attention.output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph, info.seed, op0 + 1)
+        h1_8 = None
+        if fp8:
+            h1, z1, m1, r1, h1_8 = ops.ln_fwd_q8(a1, x, *ln1, s8["ffn1"])
+        else:
+            h1, z1, m1, r1 = ops.ln_fwd(a1, x, *ln1)
         act8 = None
         r8 = (ops.linear_gelu_fwd_fp8(h1, W8("intermediate.dense"), Bm("intermediate.dense.bias"), s8["ffn1"],
-                                      s8["ffn2"]) if fp8 else None)
+                                      s8["ffn2"], x8=h1_8) if fp8 else None)
         if r8 is not None:
             pre, act, act8 = r8
             ctx.gelu_deriv = True
-        elif fp8:  # shape the fp8 kernel does not tile: hipBLASLt fp8 + separate GELU
-            pre = ops.linear_fwd_fp8(h1, W8("intermediate.dense"), Bb("intermediate.dense"))
-            act = ops.gelu_fwd(pre)
-            ctx.gelu_deriv = False
         else:  # `pre` holds gelu'(pre) when the fused MFMA epilogue ran (ctx.gelu_deriv)
             pre, act, ctx.gelu_deriv = ops.linear_gelu_fwd_d(h1, st.view(p + "intermediate.dense.weight"),
                                                              Bb("intermediate.dense"), Bm("intermediate.dense.bias"))
         if act8 is not None:
-            a2 = ops.linear_fwd_fp8_prequant(act8, s8["ffn2"], W8("output.dense"), Bb("output.dense"))
-        elif fp8:
-            a2 = ops.linear_fwd_fp8(act, W8("output.dense"), Bb("output.dense"))
+            a2 = ops.linear_fwd_fp8_own(act8, s8["ffn2"], W8("output.dense"), Bm("output.dense.bias"))
         else:
             a2 = proj(act, "output.dense")
-        h2, z2, m2, r2 = ops.ln_fwd(a2, h1, st.view(p + "output.LayerNorm.weight", "master"),
-                                    st.view(p + "output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph,
-                                    info.seed, op0 + 2)
+        ln2 = (st.view(p + "output.LayerNorm.weight", "master"), st.view(p + "output.LayerNorm.bias", "master"),
+               cfg.layer_norm_eps, ph, info.seed, op0 + 2)
+        if fp8 and idx + 1 < cfg.num_hidden_layers:  # the next layer's QKV input, in e4m3
+            h2, z2, m2, r2, info.x8[idx + 1] = ops.ln_fwd_q8(a2, h1, *ln2, m.fp8_states(idx + 1)["qkv"])
+        else:
+            h2, z2, m2, r2 = ops.ln_fwd(a2, h1, *ln2)
         ctx.save_for_backward(x, key_bias, qkv, ctxv, lse, z1, m1, r1, h1, pre, act, z2, m2, r2)
         ctx.bits = bits
         ctx.info, ctx.idx, ctx.ph, ctx.pa, ctx.scale = info, idx, ph, pa, scale

@@ -50,6 +50,13 @@ def ln_fwd(a, resid, gamma, beta, eps, p, seed, opid):
     return ref.ln_fwd(a, resid, gamma, beta, eps, p, seed, opid)
 
 
+def ln_fwd_q8(a, resid, gamma, beta, eps, p, seed, opid, state: "Fp8DelayedState"):
+    """``ln_fwd`` that also writes y in e4m3 under ``state`` — the delayed-scaling state of the fp8 GEMM
+    that consumes y — so that GEMM needs no separate quantisation pass: (y, z, mean, rstd, y8)."""
+    return tuple(_k().ln_fwd(a, resid, gamma, beta, float(eps), float(p), int(seed), int(opid), q8=state.buf,
+                             phase=state.next_phase()))
+
+
 def ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate):
     if dy.is_cuda:
         return tuple(_k().ln_bwd(dy, dy2, z, gamma, mean, rstd, float(p), int(seed), int(opid),
@@ -144,11 +151,13 @@ def linear_fwd(x, w, b, b32=None, kind: str = "plain"):
 
 
 def linear_fwd_fp8(x, w8s, b):
-    """y = x·Wᵀ + b with both operands in OCP fp8 e4m3 (per-tensor current scaling) on hipBLASLt's
-    fp8 MFMA path (torch._scaled_mm), bf16 out.  ``w8s`` = (W fp8 [N,K], scale) from ParamStore.view_fp8."""
+    """y = x·Wᵀ + b with both operands in OCP fp8 e4m3 (x under per-tensor current scaling, one amax pass +
+    one quantisation pass) on the own fp8 MFMA kernel (gemm_fp8.hip), bf16 out.  ``w8s`` = (W fp8 [N,K],
+    dequant scale) from ParamStore.view_fp8.  The training step uses the producer-quantised form
+    (``linear_fwd_fp8_own``); this is the standalone op."""
     x8, sx = _k().fp8_quantize(x)
     w8, sw = w8s
-    return torch._scaled_mm(x8, w8.t(), scale_a=sx, scale_b=sw.reshape(()), bias=b, out_dtype=torch.bfloat16)
+    return _k().gemm_fp8(x8, w8, _EPI_BIAS, b.float().contiguous(), sx.reshape(1).float(), sw.reshape(1).float())
 
 
 class Fp8DelayedState:
@@ -179,30 +188,27 @@ class Fp8DelayedState:
         return _k().fp8_quant_delayed(x, self.buf, ph)
 
 
-def linear_fwd_fp8_delayed(x, w8s, b, state: Fp8DelayedState):
-    """y = x·Wᵀ + b with x quantised in ONE pass under delayed scaling (scale from the previous
-    step's amax, this step's amax recorded on device) and hipBLASLt's fp8 MFMA GEMM."""
-    x8 = state.quantize(x)
+def fp8_gemm_ok(M: int, N: int, K: int) -> bool:
+    return bool(_k().gemm_fp8_supported(int(M), int(N), int(K)))
+
+
+def linear_fwd_fp8_own(x8, x_state: Fp8DelayedState, w8s, b32):
+    """y = x8·W8ᵀ·s_x·s_w + b on the own block-scaled fp8 MFMA kernel (gemm_fp8.hip, bias epilogue) for an
+    e4m3 input written by its producer under ``x_state`` (LN forward, FFN1 epilogue, or ``quantize``)."""
     w8, sw = w8s
-    return torch._scaled_mm(x8, w8.t(), scale_a=state.scale.reshape(()), scale_b=sw.reshape(()), bias=b,
-                            out_dtype=torch.bfloat16)
+    return _k().gemm_fp8(x8, w8, _EPI_BIAS, b32, x_state.scale, sw.reshape(1).float())
 
 
-def linear_fwd_fp8_prequant(x8, x_state: Fp8DelayedState, w8s, b):
-    """y = x8·Wᵀ·s + b for an input already in e4m3 (written by the producer under ``x_state``)."""
-    w8, sw = w8s
-    return torch._scaled_mm(x8, w8.t(), scale_a=x_state.scale.reshape(()), scale_b=sw.reshape(()), bias=b,
-                            out_dtype=torch.bfloat16)
-
-
-def linear_gelu_fwd_fp8(x, w8s, b32, in_state: Fp8DelayedState, out_state: Fp8DelayedState):
+def linear_gelu_fwd_fp8(x, w8s, b32, in_state: Fp8DelayedState, out_state: Fp8DelayedState, x8=None):
     """FFN1 in fp8 on the own block-scaled MFMA kernel (gemm_fp8.hip): returns (gelu'(pre), act, act8)
     — act in bf16 (saved for the FFN2 weight gradient) and in e4m3 under ``out_state``'s delayed scale
-    for the FFN2 fp8 GEMM; None when the shape does not tile (caller falls back)."""
+    for the FFN2 fp8 GEMM; None when the shape does not tile (caller falls back).  ``x8``: the input
+    already in e4m3 under ``in_state`` (LN forward's fp8 output), else it is quantised here."""
     M, K, N = x.shape[0], x.shape[1], w8s[0].shape[0]
     if not _k().gemm_fp8_supported(M, N, K):
         return None
-    x8 = in_state.quantize(x)
+    if x8 is None:
+        x8 = in_state.quantize(x)
     w8, sw = w8s
     gd = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
     act8 = torch.empty(M, N, dtype=torch.float8_e4m3fn, device=x.device)

@@ -260,6 +260,8 @@ class Trainer:
         avg = {}
         last_t, last_step = time.perf_counter(), self.global_step
         samples_per_step = self.train_batch_size * self.world
+        steady = [0, 0.0]  # optimizer steps and seconds after the first two logged intervals (warm-up)
+        logged = 0
         loader, skip = self.train_dataloader, self._resume_skip
         self._resume_skip = 0
         if skip:
@@ -289,6 +291,10 @@ class Trainer:
                 if steps > 0:
                     avg["perf/samples_per_sec"] = samples_per_step * steps / max(now - last_t, 1e-9)
                     avg["perf/step_ms"] = (now - last_t) / steps * 1e3
+                    logged += 1
+                    if logged > 2:
+                        steady[0] += steps
+                        steady[1] += now - last_t
                 last_t, last_step = now, self.global_step
                 tb = {k: v for k, v in avg.items() if not k.startswith("perf/")}
                 self._update_writer(tb, prefix="train")
@@ -306,6 +312,10 @@ class Trainer:
             if self.debug:
                 logger.info("Training was interrupted because of debug mode.")
                 break
+        if steady[0] > 0 and self.rank == 0:  # comparable with bench.py's samples/s (same step, host clock)
+            logger.info(f"Train throughput (epoch {epoch_i}, {steady[0]} steady-state steps): "
+                        f"{samples_per_step * steady[0] / steady[1]:.1f} samples/sec, "
+                        f"{steady[1] / steady[0] * 1e3:.2f} ms/step.")
 
     # ------------------------------------------------------------------ torch.profiler export
     def _torch_profiler_step(self):

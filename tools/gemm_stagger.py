@@ -1,9 +1,10 @@
 #!/usr/bin/env python
-"""Persistent NT GEMM (v3) at the b256 projection shapes vs the start offset of half of each XCD's
-workgroups (``gemm_set_stagger``, units of s_sleep(127) ≈ 8128 cycles).  Interleaved rounds in one
-process; prints the median per (shape, epilogue, stagger).
+"""Persistent NT GEMM (v3) at the b256 projection shapes vs its launch knobs (``gemm_set_stagger``): the
+start offset of half of each XCD's workgroups (bits 0-7, units of s_sleep(127) ≈ 8128 cycles) and the
+epilogue flags (bits 8-15: 1 nontemporal P stores, 2 nontemporal C stores, 4 no GELU math, 8 no stores —
+the last two are diagnostics).  Interleaved rounds in one process; prints the median per (shape, knob).
 
-    python tools/gemm_stagger.py [--T 98304] [--staggers 0,1,2,3,4,6] [--rounds 3]
+    python tools/gemm_stagger.py [--T 98304] [--knobs 0,1,2,4] [--rounds 3]     # knob = stagger | flags << 8
 """
 import argparse
 import json
@@ -21,7 +22,7 @@ EPI = {"none": 0, "bias": 1, "resid": 4, "gelud": 5, "dmul": 6}
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--T", type=int, default=98304)
-    ap.add_argument("--staggers", default="0,1,2,3,4,6")
+    ap.add_argument("--knobs", default="0,1,2,4")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()
@@ -29,9 +30,12 @@ def main():
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     T = a.T
-    stg = [int(s) for s in a.staggers.split(",")]
+    stg = [int(s, 0) for s in a.knobs.split(",")]
     shapes = [(3072, 768, "gelud"), (3072, 768, "dmul"), (3072, 768, "bias"), (768, 768, "resid"),
               (2304, 768, "bias"), (768, 2304, "resid")]
+    if os.environ.get("KNOB_SHAPES"):
+        keep = set(os.environ["KNOB_SHAPES"].split(","))
+        shapes = [sh for sh in shapes if sh[2] in keep]
     k.gemm_set_variant(3)
     for N, K, name in shapes:
         e = EPI[name]
@@ -68,10 +72,10 @@ def main():
         row = {"N": N, "K": K, "epi": name}
         for s in stg:
             us = sorted(res[s])[len(res[s]) // 2]
-            row[f"s{s}_us"] = round(us, 1)
-        best = min(stg, key=lambda s: row[f"s{s}_us"])
-        row["best"] = best
-        row["best_tflops"] = round(fl / row[f"s{best}_us"] / 1e6, 1)
+            row[f"k{s:#x}_us"] = round(us, 1)
+        best = min(stg, key=lambda s: row[f"k{s:#x}_us"])
+        row["best"] = hex(best)
+        row["best_tflops"] = round(fl / row[f"k{best:#x}_us"] / 1e6, 1)
         print(json.dumps(row), flush=True)
         del A, B, P, R, part, out
     k.gemm_set_stagger(0)
