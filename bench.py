@@ -40,6 +40,8 @@ def parse():
                     help="compute precision; fp8 = OCP e4m3 forward projections (BASELINE config #5)")
     ap.add_argument("--bucket_cap_mb", type=float, default=32.0)
     ap.add_argument("--profile", action="store_true", help="per-phase timers (adds syncs; not for the headline)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the forward+backward from a captured HIP graph (single process, no reducer)")
     ap.add_argument("--force_reducer", action="store_true",
                     help="keep the gradient reducer active at 1 GPU (1-rank RCCL communicator): rehearses the "
                          "multi-GPU fence → ncclAllReduce → wait path on every bucket of the real backward")
@@ -102,7 +104,7 @@ def main():
     # uses them — separates the cost of the communicator's presence from that of its all-reduces
     idle = os.environ.get("HQ_BENCH_REDUCER_IDLE", "0") == "1"
     engine = TrainEngine(model, loss_fn, opt, scheduler=sched, reducer=None if idle else reducer, max_grad_norm=1.0,
-                         profile=args.profile)
+                         profile=args.profile, graph=args.graph)
 
     sp = SpecialIds(cfg.vocab_size, cfg.pad_token_id, cfg.unk_token_id, cfg.cls_token_id, cfg.sep_token_id,
                     "bert" if cfg.family == "bert" else "roberta")
@@ -168,6 +170,7 @@ def main():
                       "parallelism": f"dp{world}", "allreduce_dtype": args.allreduce_dtype,
                       "bucket_cap_mb": args.bucket_cap_mb,
                       "rccl_channels": os.environ.get("NCCL_MIN_NCHANNELS")},
+           "graph_replays": engine.graph_replays,
            "reducer": reducer.kind if reducer is not None else "none",
            "reducer_buckets": reducer.n_buckets if reducer is not None else 0,
            "comm_wait_ms": round(comm["comm_wait_ms"], 3) if "comm_wait_ms" in comm else None,

@@ -68,6 +68,7 @@ def build_trainer(params, model_params, device, *, rank: int, local_idx: int, us
                    train_weights=weights, drop_optimizer=params.drop_optimizer, debug=params.debug,
                    bucket_cap_mb=params.bucket_cap_mb, allreduce_dtype=params.allreduce_dtype,
                    no_sync_accum=bool(params.no_sync_accum), log_every=params.log_every, profile=params.profile,
+                   cuda_graph=bool(getattr(params, "cuda_graph", False)),
                    eval_shard=params.eval_shard, precision=params.precision,
                    torch_profile_dir=params.torch_profile_dir, torch_profile_steps=params.torch_profile_steps)
 

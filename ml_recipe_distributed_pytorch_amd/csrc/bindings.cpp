@@ -586,6 +586,14 @@ PYBIND11_MODULE(_hq_kernels, m) {
         py::arg("pre") = py::none(), py::arg("out8") = py::none(), py::arg("state") = py::none(), py::arg("phase") = 0);
   m.def("span_fwd", &span_fwd);
   m.def("span_bwd", &span_bwd);
+  m.def("set_dropout_seed", [](c10::optional<Tensor> t) {
+    if (t.has_value() && t->defined()) {
+      TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->numel() >= 1, "seed must be a GPU int32 tensor");
+      hq_set_dropout_seed_ptr(reinterpret_cast<const uint32_t*>(t->data_ptr()));
+    } else {
+      hq_set_dropout_seed_ptr(nullptr);
+    }
+  });
   m.def("qa_heads_fwd", &qa_heads_fwd);
   m.def("qa_loss", &qa_loss);
   m.def("qa_heads_bwd", &qa_heads_bwd);

@@ -84,7 +84,18 @@ __device__ __forceinline__ float hq_wave_max(float v) {
 __host__ __device__ __forceinline__ uint32_t hq_fmix32(uint32_t h) {
   h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16; return h;
 }
-static inline uint32_t hq_op_key(uint32_t seed, uint32_t opid) { return hq_fmix32(seed ^ (opid * 0x9E3779B9u)); }
+__host__ __device__ __forceinline__ uint32_t hq_op_key(uint32_t seed, uint32_t opid) {
+  return hq_fmix32(seed ^ (opid * 0x9E3779B9u));
+}
+// Dropout stream of one op, passed by value to the kernels: the host-derived key, or — when a device seed
+// word is registered (hq_set_dropout_seed_ptr: captured HIP graphs, whose replays must draw new masks
+// without re-launching from the host) — the key derived in-kernel from *seedp.
+struct HqDropKey {
+  uint32_t key;
+  uint32_t opid;
+  const uint32_t* seedp;
+  __device__ __forceinline__ uint32_t get() const { return seedp ? hq_op_key(*seedp, opid) : key; }
+};
 static inline uint32_t hq_threshold(float p) { return (uint32_t)__builtin_rintf(p * 65536.0f); }
 static inline float hq_keep_scale(uint32_t thr) { return thr < 65536u ? 65536.0f / (float)(65536u - thr) : 0.f; }
 

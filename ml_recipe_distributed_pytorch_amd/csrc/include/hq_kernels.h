@@ -11,6 +11,13 @@ struct HqOuts {  // up to 4 fp32 column-sum destinations (null = skip), passed b
   float* p[4];
 };
 
+// ---- dropout streams ---------------------------------------------------------------------------
+// Register (or clear with nullptr) a device uint32 seed that every dropout kernel launched afterwards reads
+// instead of its host seed argument (norm.hip).
+void hq_set_dropout_seed_ptr(const uint32_t* p);
+struct HqDropKey;
+HqDropKey hq_drop_key(uint32_t seed, uint32_t opid);
+
 // ---- norm.hip --------------------------------------------------------------------------------
 int hq_ln_bwd_partials(int T);
 int hq_rowblock_partials(int T);

@@ -226,7 +226,8 @@ __global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __re
                                                             const float* __restrict__ key_bias,
                                                             uint16_t* __restrict__ ctx, float* __restrict__ lse,
                                                             uint16_t* __restrict__ mbits, int L, int nh, float c_scale,
-                                                            uint32_t key, uint32_t thr, float kscale) {
+                                                            HqDropKey kd_, uint32_t thr, float kscale) {
+  const uint32_t key = kd_.get();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int UNR = NT > 0 ? NT : 1;
   const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
@@ -459,8 +460,9 @@ __global__ __launch_bounds__(RW * 64, DROP ? 3 : 4) void attn_fwd_ring_kernel(co
                                                                    const float* __restrict__ key_bias,
                                                                    uint16_t* __restrict__ ctx, float* __restrict__ lse,
                                                                    uint16_t* __restrict__ mbits, int L, int nh,
-                                                                   int n_qb, float c_scale, uint32_t key,
+                                                                   int n_qb, float c_scale, HqDropKey kd_,
                                                                    uint32_t thr, float kscale, int force_slow) {
+  const uint32_t key = kd_.get();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
   constexpr int RNS = RAHEAD + 2;
@@ -1411,7 +1413,7 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
   set_attn_prio();
   if (dh != D || L > 512) { fprintf(stderr, "hq_attn_fwd: head_dim %d / L %d unsupported\n", dh, L); abort(); }
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
-  const uint32_t key = hq_op_key(seed, opid);
+  const HqDropKey key = hq_drop_key(seed, opid);
   const int Lp = (L + 31) & ~31, n32 = Lp / 32;
   if (attn_fwd_variant() == 3) {
     const int n_qb = (L + RQ - 1) / RQ;

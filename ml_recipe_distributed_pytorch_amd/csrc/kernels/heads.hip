@@ -74,13 +74,15 @@ struct FwdArgs {
   float *logits, *pooled, *cls, *reg, *hpart;  // hpart [H/64][B][kHS] scratch
   unsigned* cnt;
   int B, L, H, NL, T, npool;
-  uint32_t key, thr;
+  HqDropKey kd;
+  uint32_t thr;
   float ks;
 };
 
 template <int NCH>
 __global__ __launch_bounds__(256) void qa_heads_fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  const uint32_t key = a.kd.get();
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int H = a.H;
   if ((int)blockIdx.x >= a.npool) {  // ---------------------------------------------- span rows
@@ -152,7 +154,7 @@ __global__ __launch_bounds__(256) void qa_heads_fwd_kernel(FwdArgs a) {
     if (b >= a.B) break;  // wave-uniform
     const float pv = tanhf(acc[s] + bj);
     a.pooled[(size_t)b * H + j] = pv;
-    const float pm = pv * keep_mult((uint32_t)((size_t)b * H + j), a.key, a.thr, a.ks);
+    const float pm = pv * keep_mult((uint32_t)((size_t)b * H + j), key, a.thr, a.ks);
     float* hp = a.hpart + ((size_t)jb * a.B + b) * kHS;
 #pragma unroll
     for (int c = 0; c < kMaxNL; ++c) {
@@ -362,7 +364,8 @@ struct BwdArgs {
   float *gwp, *gbp, *gwc, *gbc, *gwrs, *gbrs, *gwre, *gbre;
   int B, L, H, NL, T, acc;
   int nA, nW, nS;
-  uint32_t key, thr;
+  HqDropKey kd;
+  uint32_t thr;
   float ks;
 };
 
@@ -377,10 +380,10 @@ __device__ __forceinline__ float sample_scalar(const BwdArgs& a, int b, int c, f
 }
 
 // dL/d(pooler pre-activation)[b, k] from the per-sample scalars sc[kHS]
-__device__ __forceinline__ float dpre_at(const BwdArgs& a, int b, int k, const float* sc) {
+__device__ __forceinline__ float dpre_at(const BwdArgs& a, uint32_t key, int b, int k, const float* sc) {
   float d = 0.f;
   for (int c = 0; c < a.NL; ++c) d = fmaf(sc[c], a.wc[(size_t)c * a.H + k], d);
-  d *= keep_mult((uint32_t)((size_t)b * a.H + k), a.key, a.thr, a.ks);
+  d *= keep_mult((uint32_t)((size_t)b * a.H + k), key, a.thr, a.ks);
   d = fmaf(sc[8], a.wrs[k], fmaf(sc[9], a.wre[k], d));
   const float pv = a.pooled[(size_t)b * a.H + k];
   return d * (1.f - pv * pv);
@@ -391,6 +394,7 @@ __device__ __forceinline__ void put(float* p, float v, int acc) { *p = acc ? *p 
 template <int NCH>
 __global__ __launch_bounds__(256) void qa_heads_bwd_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
+  const uint32_t key = a.kd.get();
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int H = a.H, B = a.B, nj = H / 64;
   const float gs = a.gscale ? *a.gscale : 1.f;
@@ -412,7 +416,7 @@ __global__ __launch_bounds__(256) void qa_heads_bwd_kernel(BwdArgs a) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int s = wv + 4 * q, b = sb * 32 + s;
-        dp[s * 64 + lane] = b < B ? dpre_at(a, b, k0 + lane, scs + s * kHS) : 0.f;
+        dp[s * 64 + lane] = b < B ? dpre_at(a, key, b, k0 + lane, scs + s * kHS) : 0.f;
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -464,7 +468,7 @@ __global__ __launch_bounds__(256) void qa_heads_bwd_kernel(BwdArgs a) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int s = wv + 4 * q, b = b0 + s;
-        dp[s * 64 + lane] = b < B ? dpre_at(a, b, kb * 64 + lane, scs + s * kHS) : 0.f;
+        dp[s * 64 + lane] = b < B ? dpre_at(a, key, b, kb * 64 + lane, scs + s * kHS) : 0.f;
         xs[s * 64 + lane] = b < B ? hq_bf2f(a.seq[(size_t)b * a.L * H + ib * 64 + lane]) : 0.f;
       }
       __syncthreads();
@@ -504,7 +508,7 @@ __global__ __launch_bounds__(256) void qa_heads_bwd_kernel(BwdArgs a) {
       for (int c = 0; c < kMaxNL; ++c) sc[c] = c < a.NL ? gs * a.dheads[(size_t)b * kHS + c] : 0.f;
       const float s8 = sample_scalar(a, b, 8, gs), s9 = sample_scalar(a, b, 9, gs);
       const float pv = a.pooled[(size_t)b * H + k];
-      const float m = keep_mult((uint32_t)((size_t)b * H + k), a.key, a.thr, a.ks);
+      const float m = keep_mult((uint32_t)((size_t)b * H + k), key, a.thr, a.ks);
       float d = 0.f;
 #pragma unroll
       for (int c = 0; c < kMaxNL; ++c) d = fmaf(sc[c], wck[c], d);
@@ -642,7 +646,7 @@ void hq_qa_heads_fwd(const uint16_t* seq, const HqHeadWeights& w, float* logits,
   a.B = B; a.L = L; a.H = H; a.NL = NL; a.T = B * L;
   a.npool = ((B + 31) / 32) * (H / 64);
   a.thr = p > 0.f ? hq_threshold(p) : 0u;
-  a.key = hq_op_key(seed, opid);
+  a.kd = hq_drop_key(seed, opid);
   a.ks = hq_keep_scale(a.thr);
   const int nspan = (a.T + 3) / 4;
   const size_t lds = (32 * 64 + 64 * 65) * sizeof(float);
@@ -684,7 +688,7 @@ void hq_qa_heads_bwd(const uint16_t* seq, const float* dlog, const float* dheads
   a.nW = nj * nj;
   a.nS = nj;
   a.thr = p > 0.f ? hq_threshold(p) : 0u;
-  a.key = hq_op_key(seed, opid);
+  a.kd = hq_drop_key(seed, opid);
   a.ks = hq_keep_scale(a.thr);
   const int nspan = hq_qa_heads_bwd_span_blocks(a.T);
   size_t lds = (32 * kHS + 32 * 64 + 64 * 64) * sizeof(float);                     // R1

@@ -28,8 +28,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict_
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      uint16_t* __restrict__ y, uint16_t* __restrict__ z,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out, int T,
-                                                     int H, float eps, uint32_t key, uint32_t thr, float kscale,
+                                                     int H, float eps, HqDropKey kd_, uint32_t thr, float kscale,
                                                      uint8_t* __restrict__ y8, float* __restrict__ q8, int phase) {
+  const uint32_t key = kd_.get();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float amax = 0.f, inv8 = 1.f, s8 = 1.f;
   if constexpr (Q8) {
@@ -151,8 +152,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
                                                      const uint16_t* __restrict__ z, const float* __restrict__ gamma,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      uint16_t* __restrict__ dz_out, uint16_t* __restrict__ da_out,
-                                                     float* __restrict__ part, int T, int H, uint32_t key, uint32_t thr,
+                                                     float* __restrict__ part, int T, int H, HqDropKey kd_, uint32_t thr,
                                                      float kscale) {
+  const uint32_t key = kd_.get();
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float acc[3][NCH][4];
@@ -328,8 +330,9 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
                                                         const uint16_t* __restrict__ wp, const uint16_t* __restrict__ wt,
                                                         const float* __restrict__ gamma, const float* __restrict__ beta,
                                                         uint16_t* __restrict__ y, float* __restrict__ mean_out,
-                                                        float* __restrict__ rstd_out, int T, int H, float eps, uint32_t key,
+                                                        float* __restrict__ rstd_out, int T, int H, float eps, HqDropKey kd_,
                                                         uint32_t thr, float kscale, int V, int P, int NTY) {
+  const uint32_t key = kd_.get();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int row = blockIdx.x * kWaves + wave;
   if (row >= T) return;
@@ -421,8 +424,9 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
     const int64_t* __restrict__ tids, const uint16_t* __restrict__ ww, const uint16_t* __restrict__ wp,
     const uint16_t* __restrict__ wt, const float* __restrict__ gamma, const float* __restrict__ mean,
     const float* __restrict__ rstd, float* __restrict__ g_word, float* __restrict__ g_pos, float* __restrict__ g_type,
-    float* __restrict__ part, int T, int H, int n_types, int pad_word, int pad_pos, uint32_t key, uint32_t thr,
+    float* __restrict__ part, int T, int H, int n_types, int pad_word, int pad_pos, HqDropKey kd_, uint32_t thr,
     float kscale, int V, int P, int B, int L) {
+  const uint32_t key = kd_.get();
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][H] reduction scratch, reused as dx rows
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   float acc[4][NCH][4];
@@ -677,11 +681,17 @@ void colsum(const float* part, int P, int N, HqOuts outs, int Hq, bool accumulat
 }  // namespace
 
 // ================================================================================== launchers
+namespace {
+const uint32_t* g_seed_ptr = nullptr;
+}
+void hq_set_dropout_seed_ptr(const uint32_t* p) { g_seed_ptr = p; }
+HqDropKey hq_drop_key(uint32_t seed, uint32_t opid) { return HqDropKey{hq_op_key(seed, opid), opid, g_seed_ptr}; }
+
 void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, const float* beta, uint16_t* y, uint16_t* z,
                float* mean, float* rstd, int T, int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s,
                uint8_t* y8, float* q8, int phase) {
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
-  const uint32_t key = hq_op_key(seed, opid);
+  const HqDropKey key = hq_drop_key(seed, opid);
   const float ks = hq_keep_scale(thr);
   const int blocks = (T + kWaves - 1) / kWaves;
   dispatch_nch(H, [&](auto nch) {
@@ -704,7 +714,7 @@ void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const
                const float* rstd, uint16_t* dz, uint16_t* da, float* part, HqOuts outs, int T, int H, float p,
                uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s) {
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
-  const uint32_t key = hq_op_key(seed, opid);
+  const HqDropKey key = hq_drop_key(seed, opid);
   const float ks = hq_keep_scale(thr);
   const int nb = hq_ln_bwd_partials(T);
   dispatch_nch(H, [&](auto nch) {
@@ -718,7 +728,7 @@ void hq_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, 
                   const uint16_t* wt, const float* gamma, const float* beta, uint16_t* y, float* mean, float* rstd, int T,
                   int H, float eps, float p, uint32_t seed, uint32_t opid, int V, int P, int NTY, hipStream_t s) {
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
-  const uint32_t key = hq_op_key(seed, opid);
+  const HqDropKey key = hq_drop_key(seed, opid);
   const float ks = hq_keep_scale(thr);
   dispatch_nch(H, [&](auto nch) {
     hipLaunchKernelGGL(embed_fwd_kernel<decltype(nch)::value>, dim3((T + kWaves - 1) / kWaves), dim3(256), 0, s, ids,
@@ -732,7 +742,7 @@ void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, c
                   int n_types, int pad_word, int pad_pos, float p, uint32_t seed, uint32_t opid, bool accumulate,
                   int V, int P, int L, hipStream_t s) {
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
-  const uint32_t key = hq_op_key(seed, opid);
+  const HqDropKey key = hq_drop_key(seed, opid);
   const float ks = hq_keep_scale(thr);
   if (L <= 0 || T % L) L = T;  // rows are b·L + l; any other layout is one "sequence" of T positions
   const int B = T / L;

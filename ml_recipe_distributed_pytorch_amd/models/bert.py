@@ -385,6 +385,22 @@ class BertForQuestionAnswering(nn.Module):
                     mod._buffers[k] = fn(b)
         return self
 
+    def use_device_seed(self, enable: bool):
+        """Dropout kernels read their per-step seed from a device word (``seed_device``) instead of a
+        launch argument — required inside a captured HIP graph, whose replays must draw new masks.  The
+        registration is process-wide (one captured model per process)."""
+        from .._native import kernels
+        if enable:
+            if getattr(self, "_seed_dev", None) is None or self._seed_dev.device != self.store.device:
+                self._seed_dev = torch.zeros(1, dtype=torch.int32, device=self.store.device)
+            kernels().set_dropout_seed(self._seed_dev)
+        else:
+            kernels().set_dropout_seed(None)
+
+    @property
+    def seed_device(self) -> Optional[torch.Tensor]:
+        return getattr(self, "_seed_dev", None)
+
     def compute_dtype_for(self, device) -> torch.dtype:
         if torch.device(device).type != "cuda":
             return torch.float32

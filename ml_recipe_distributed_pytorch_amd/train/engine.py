@@ -79,8 +79,15 @@ class StepResult:
 
 
 class TrainEngine:
+    """``graph=True`` (GPU, bf16, one micro-batch per step, no gradient reducer): after two eager warm-up
+    steps the forward + loss + backward of a micro-batch is captured once into a HIP graph and replayed for
+    every later batch of the same shape (inputs copied into the captured tensors, the dropout seed written
+    to the model's device seed word); the clip + fused optimizer step stays eager (its learning rate
+    changes every step).  At small micro-batches the step is launch-bound (the reference's 2 × 512):
+    one graph launch replaces ~300 kernel launches.  Other shapes fall back to the eager path."""
+
     def __init__(self, model, loss_fn, optimizer, *, scheduler=None, reducer=None, max_grad_norm: float = 1.0,
-                 batch_split: int = 1, no_sync_accum: bool = True, profile: bool = False):
+                 batch_split: int = 1, no_sync_accum: bool = True, profile: bool = False, graph: bool = False):
         self.model = model
         self.loss_fn = loss_fn
         self.optimizer = optimizer
@@ -92,13 +99,92 @@ class TrainEngine:
         self.profile = profile
         self.micro = 0
         self._timer = PhaseTimer(profile, model.store.device)
+        self.graph = bool(graph)
+        self._graph = None
+        self._graph_warm = 0
+        self._static = None
+        self.graph_replays = 0
 
     @property
     def device(self):
         return self.model.store.device
 
+    # ------------------------------------------------------------------ HIP graph path
+    def _graph_eligible(self) -> bool:
+        m = self.model
+        return (self.graph and self.batch_split == 1 and self.reducer is None and not self.profile
+                and m.store.device.type == "cuda" and getattr(m, "precision", "bf16") == "bf16"
+                and getattr(m, "grad_side_stream", None) is None and m.training)
+
+    @staticmethod
+    def _shape_key(inputs, labels):
+        return tuple((k, tuple(v.shape), v.dtype) for d in (inputs, labels) for k, v in sorted(d.items())
+                     if torch.is_tensor(v))
+
+    def _capture(self, inputs, labels):
+        m = self.model
+        static_in = {k: v.clone() if torch.is_tensor(v) else v for k, v in inputs.items()}
+        static_lab = {k: v.clone() if torch.is_tensor(v) else v for k, v in labels.items()}
+        m.use_device_seed(True)
+        m.store._t_dirty = True   # the Wᵀ refresh belongs in the graph: the weights change every step
+        m.zero_grad()             # "fresh" groups: the captured backward overwrites the arena gradients
+        side = torch.cuda.Stream(device=m.store.device)
+        side.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        rng = torch.get_rng_state()   # the capture's forward draws a (unused) host seed: keep the stream aligned
+        with torch.cuda.graph(g, stream=side):
+            loss = self.loss_fn(m(**static_in), static_lab)
+            loss.backward()
+        torch.set_rng_state(rng)
+        torch.cuda.current_stream().wait_stream(side)
+        self._graph, self._static = g, (static_in, static_lab, self._shape_key(inputs, labels), self.loss_fn.last)
+
+    def _graph_micro_step(self, inputs, labels) -> Optional[StepResult]:
+        if self._graph is None:
+            if self._graph_warm < 2:          # eager warm-up: kernel attributes, Wᵀ copies, allocator pools
+                self._graph_warm += 1
+                return None
+            self._capture(inputs, labels)
+        elif self._shape_key(inputs, labels) != self._static[2]:
+            return None
+        static_in, static_lab, _, record = self._static
+        for src, dst in ((inputs, static_in), (labels, static_lab)):
+            for k, v in src.items():
+                if torch.is_tensor(v):
+                    dst[k].copy_(v, non_blocking=True)
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+        self.model.seed_device.fill_(seed)
+        self._timer.reset()
+        self._timer.mark()
+        self._graph.replay()
+        self.graph_replays += 1
+        self.loss_fn.last = record
+        self._timer.mark("bwd")
+        self.micro += 1
+        return self._apply()
+
+    def release_graph(self):
+        if self._graph is not None:
+            self.model.use_device_seed(False)
+        self._graph, self._static, self._graph_warm = None, None, 0
+
     def micro_step(self, inputs, labels) -> Optional[StepResult]:
         """Forward+backward of one micro-batch; runs the optimizer on the accumulation boundary."""
+        if self._graph_eligible():
+            res = self._graph_micro_step(inputs, labels)
+            if res is not None:
+                return res
+        elif self._graph is not None:
+            self.release_graph()
+        if self._graph is not None:   # eager step beside a live graph: host seeds again
+            self.model.use_device_seed(False)
+            try:
+                return self._eager_micro_step(inputs, labels)
+            finally:
+                self.model.use_device_seed(True)
+        return self._eager_micro_step(inputs, labels)
+
+    def _eager_micro_step(self, inputs, labels) -> Optional[StepResult]:
         timer = self._timer
         if self.micro % self.batch_split == 0:
             timer.reset()

@@ -121,6 +121,7 @@ class Trainer:
     no_sync_accum: bool = True
     log_every: int = 1
     profile: bool = False
+    cuda_graph: bool = False
     eval_shard: bool = False
     precision: Optional[str] = None
     torch_profile_dir: Optional[str] = None
@@ -164,7 +165,7 @@ class Trainer:
             self.engine = TrainEngine(self.model, self.loss, self.optimizer, scheduler=self.scheduler,
                                       reducer=self.reducer, max_grad_norm=self.max_grad_norm,
                                       batch_split=self.batch_split, no_sync_accum=self.no_sync_accum,
-                                      profile=self.profile)
+                                      profile=self.profile, graph=self.cuda_graph)
         self.global_step = 0
         self.start_epoch = 1
         self.epoch_complete = True

@@ -176,6 +176,9 @@ def get_trainer_parser() -> ArgumentParser:
                              "split when a micro-batch would not fit.  The per-step gradient is the same mean over "
                              "train_batch_size samples (up to the per-micro-batch CE normalisation over valid spans).")
     parser.add_argument("--profile", action="store_true", help="Per-phase step timers + perf/* TB scalars.")
+    parser.add_argument("--cuda_graph", type=_opt_bool, default=False, nargs="?", const=True,
+                        help="GPU, one micro-batch per step, single process: capture the forward+backward into a HIP "
+                             "graph after two warm-up steps and replay it (launch-bound small micro-batches).")
     parser.add_argument("--torch_profile_dir", type=cast2(str), default=None,
                         help="Export a torch.profiler Chrome trace of optimizer steps --torch_profile_steps here.")
     parser.add_argument("--torch_profile_steps", type=str, default="3:5",

@@ -16,7 +16,9 @@ from ml_recipe_distributed_pytorch_amd import _native  # noqa: E402
 
 SHAPES = [(2304, 768, "bias"), (768, 768, "bias"), (3072, 768, "bias"), (768, 3072, "bias"), (768, 768, "none"),
           (768, 2304, "none"), (3072, 768, "none")]
-EPI = {"none": 0, "bias": 1}
+if os.environ.get("SMALL_SHAPES") == "epi":   # epilogue-heavy FFN shapes: own kernels only (no vendor twin)
+    SHAPES = [(3072, 768, "gelud"), (3072, 768, "dmul"), (3072, 768, "bias"), (768, 768, "resid")]
+EPI = {"none": 0, "bias": 1, "resid": 4, "gelud": 5, "dmul": 6}
 
 
 def timeit(fn, iters):
@@ -45,7 +47,13 @@ def main():
             b = torch.rand(N, device=dev)
             bb = b.bfloat16()
             e = EPI[name]
-            kw = {"bias": b} if e == 1 else {}
+            kw = {"bias": b} if e in (1, 5) else {}
+            if e in (5, 6):
+                kw["pre"] = torch.randn(T, N, device=dev).bfloat16()
+            if e == 6:
+                kw["part"] = None   # sized per kernel below
+            if e == 4:
+                kw["resid"] = torch.randn(T, N, device=dev).bfloat16()
             arms = {"auto": 0, "vS": 4}
             if T % 256 == 0:
                 arms["v256"] = 3
@@ -53,12 +61,16 @@ def main():
             for _ in range(a.rounds):
                 for n, v in arms.items():
                     k.gemm_set_variant(v)
+                    if e == 6:
+                        kw["part"] = torch.empty(k.gemm_nt_part_rows(T, N, K), N, device=dev)
                     res[n].append(timeit(lambda: k.gemm_nt(A, W, e, **kw), iters))
                 k.gemm_set_variant(0)
                 if e == 1:
                     res["blas"].append(timeit(lambda: torch.addmm(bb, A, W.t()), iters))
-                else:
+                elif e == 0:
                     res["blas"].append(timeit(lambda: torch.mm(A, W.t()), iters))
+                else:
+                    res["blas"].append(float("nan"))
             k.gemm_set_variant(0)
             fl = 2.0 * T * N * K
             row = {"T": T, "N": N, "K": K, "epi": name, "pick": k.gemm_nt_supported(T, N, K)}
