@@ -369,7 +369,7 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor key_bias, int64_t B, int64_t L, 
 }
 
 Tensor attn_bwd(Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, Tensor mbits, int64_t B, int64_t L,
-                int64_t nh, double p, double scale) {
+                int64_t nh, double p, double scale, bool deterministic) {
   check_attn(qkv, key_bias, B, L, nh);
   check(dctx, BF16, "dctx"); check(ctx, BF16, "ctx"); check(lse, F32, "lse");
   const int64_t H = qkv.size(1) / 3;
@@ -384,7 +384,7 @@ Tensor attn_bwd(Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias
   auto delta = at::empty({B, nh, L}, lse.options());
   hq_attn_bwd(ptr<uint16_t>(dctx), ptr<uint16_t>(qkv), ptr<uint16_t>(ctx), ptr<float>(lse), ptr<float>(key_bias),
               p > 0 ? ptr<uint16_t>(mbits) : nullptr, ptr<uint16_t>(dqkv), ptr<float>(delta), (int)B, (int)L, (int)nh, 64,
-              (float)p, (float)scale, cur_stream());
+              (float)p, (float)scale, deterministic, cur_stream());
   return dqkv;
 }
 

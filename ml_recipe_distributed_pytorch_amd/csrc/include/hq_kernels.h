@@ -49,7 +49,7 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
                  int nh, int dh, float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s);
 void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx, const float* lse, const float* key_bias,
                  const uint16_t* mbits, uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p, float scale,
-                 hipStream_t s);
+                 bool deterministic, hipStream_t s);
 
 // ---- optim.hip --------------------------------------------------------------------------------
 struct HqOptChunk {      // one work item of the fused optimizer: <= kOptChunk elements of one segment

@@ -1348,6 +1348,246 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
   }
 }
 
+// ============================================================================ backward v4: fused
+// One workgroup per (batch, head) for L <= 32·NW (NW <= 12): wave w owns keys 32w … 32w+31 for the whole
+// query sweep, so dK / dV stay in its registers (as in the v3 dK/dV kernel) AND the dQ of every 32-query
+// tile is summed over the workgroup's waves in LDS.  S, dP and the softmax / dropout work are therefore
+// computed ONCE per (query tile, key subtile) — v3 recomputes them in its separate dQ kernel (7 MFMA
+// units per tile pair instead of 5).  Per wave and query tile: S (4 + 1 aug MFMA: bias, −LSE), dP (4),
+// dVᵀ += dOᵀ·(P∘mask) (4), dKᵀ += Q'ᵀ·dS (4), dQ += dS·K (4: dS goes through a per-wave LDS image [key][q]
+// so that ds_read_b64_tr_b16 puts the keys on the MFMA K axis, K comes from the wave's LDS image the same
+// way), then 32 ds_add_f32 per lane into the tile's fp32 dQ accumulator — double-buffered and flushed as
+// bf16 by the first 256 threads during the next tile.  δ = rowsum(dO·O) is formed in the staging pass.
+// K and V of every wave live in LDS (register fragments would spill at 3 waves/SIMD); two waves share one
+// [32][64] dSᵀ image (32 query columns each).  LDS (NW = 12): 2 staging slots 20 KB + K / V images 96 KB
+// + dSᵀ images 24 KB + dQ accumulators 18 KB = 158 KB.
+constexpr int kDqStride = 72;   // fp32 row stride of the dQ accumulator: lanes q and q+4 land 32 banks apart
+
+template <bool DROP, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void attn_bwd_fused_kernel(
+    const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dctx, const uint16_t* __restrict__ ctx,
+    const float* __restrict__ lse, const float* __restrict__ key_bias, const uint16_t* __restrict__ mbits,
+    uint16_t* __restrict__ dqkv, int L, int nh, float c_scale, float scale, float kscale, int dbg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // slot: Q' [32][64] 4 KB | dO [32][64] 4 KB | A' words [32] uint4 512 B | δ [32] f32 128 B | bits [NW][64] u16
+  constexpr int SLOT = 2 * RTILE + 512 + 128 + NW * 128;
+  char* slots = reinterpret_cast<char*>(smem);
+  uint16_t* kimg = reinterpret_cast<uint16_t*>(slots + 2 * SLOT);  // [NW][32][64] K rows of each wave's keys
+  uint16_t* vimg = kimg + NW * 32 * D;                             // [NW][32][64] V rows
+  uint16_t* dsimg = vimg + NW * 32 * D;                            // [NW/2][32][64] dSᵀ: key rows, a wave pair's
+  float* dqacc = reinterpret_cast<float*>(dsimg + NW / 2 * 32 * D);  // query columns side by side; dQ fp32 [2][32][kDqStride]
+  const int Lp = (L + 31) & ~31, n32 = Lp >> 5;
+  const int nblk = gridDim.x, ob = blockIdx.x, xcd = ob & 7, qq = nblk >> 3, rr = nblk & 7;
+  const int bh = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (ob >> 3);
+  const int b = bh / nh, h = bh - b * nh;
+  const int H = nh * D, ld = 3 * H;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, hh = lane >> 5;
+  const int tid = threadIdx.x;
+  const int kj = wave * 32 + (lane & 31);
+  const bool active = wave * 32 < L;
+  const bool kok = kj < L;
+  const uint16_t* base = qkv + (size_t)b * L * ld + h * D;
+  HQ_DASSERT(L > 0 && n32 <= NW);
+
+  // ---- prologue: this wave's K and V rows into its LDS images
+  const int kr = kok ? kj : L - 1;
+  uint16_t* tK = kimg + wave * 32 * D;
+  uint16_t* tV = vimg + wave * 32 * D;
+  uint16_t* tS = dsimg + (wave >> 1) * 32 * D;
+  const int scol = 32 * (wave & 1);   // this wave's query columns in the shared dSᵀ image
+  {
+    bf16x8_t kf[4], vv[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      kf[s] = *reinterpret_cast<const bf16x8_t*>(base + (size_t)kr * ld + H + 16 * s + 8 * hh);
+      vv[s] = *reinterpret_cast<const bf16x8_t*>(base + (size_t)kr * ld + 2 * H + 16 * s + 8 * hh);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      *reinterpret_cast<bf16x8_t*>(tK + lds_off(lane & 31, 16 * s + 8 * hh)) = kf[s];
+      *reinterpret_cast<bf16x8_t*>(tV + lds_off(lane & 31, 16 * s + 8 * hh)) = vv[s];
+    }
+  }
+  typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+  bf16x8_t kaug;
+  {
+    const float bl = kok ? key_bias[(size_t)b * L + kj] * LOG2E : -1e30f;
+    const uint16_t bhi = bf16_rne(bl), blo = kok ? bf16_rne(bl - hq_bf2f(bhi)) : 0;
+    const u32x4 w = hh ? u32x4{0u, 0u, 0u, 0u}
+                       : u32x4{0x3F803F80u, 0x3F80u | ((uint32_t)bhi << 16), (uint32_t)blo, 0u};
+    kaug = __builtin_bit_cast(bf16x8_t, w);
+  }
+  for (int i = tid; i < 2 * 32 * kDqStride; i += NW * 64) dqacc[i] = 0.f;
+
+  // ---- staging of query tile t by the first 256 threads (row tid>>3, 16-B chunk tid&7 of Q, dO and O;
+  // every thread issues the loads, rows folded mod 32, so no load is exec-masked): one register set,
+  // issued a full tile ahead of its commit
+  const int srow = (tid >> 3) & 31, schunk = tid & 7;
+  struct Stage {
+    uint4 q, o, c;
+    float l;
+    uint16_t bits;
+  };
+  auto issue = [&](int t, Stage& st) {
+    int u = tid;                      // laundered: per-lane addresses rebuilt here, not hoisted and spilled
+    asm volatile("" : "+v"(u));
+    const int q = min(t * 32 + ((u >> 3) & 31), L - 1), ch = u & 7;
+    const size_t orow = ((size_t)b * L + q) * H + h * D + ch * 8;
+    st.q = *reinterpret_cast<const uint4*>(base + (size_t)q * ld + ch * 8);
+    st.o = *reinterpret_cast<const uint4*>(dctx + orow);
+    st.c = *reinterpret_cast<const uint4*>(ctx + orow);
+    const int ql = t * 32 + (u & 31);
+    st.l = lse[(size_t)bh * L + min(ql, L - 1)];
+    if (ql >= L) st.l = 1e30f;   // queries past L: P = 0 (finite: split3)
+    st.bits = 0;
+    if constexpr (DROP) st.bits = mbits[(((size_t)bh * n32 + t) * n32 + min(wave, n32 - 1)) * 64 + lane];
+  };
+  auto commit = [&](int t, const Stage& st) {
+    char* slot = slots + (t & 1) * SLOT;
+    if (tid < 256) {   // waves 0-3: whole waves, so the shuffles below see full rows
+      uint16_t* sq = reinterpret_cast<uint16_t*>(slot);
+      uint16_t* so = sq + 32 * D;
+      float f[8], g[8];
+      hq_unpack8(st.q, f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] *= c_scale;     // Q·c rounded exactly as the forward's prescale8
+      *reinterpret_cast<uint4*>(sq + lds_off(srow, schunk * 8)) = hq_pack8(f);
+      *reinterpret_cast<uint4*>(so + lds_off(srow, schunk * 8)) = st.o;
+      hq_unpack8(st.o, f);
+      hq_unpack8(st.c, g);
+      float d = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d = fmaf(f[j], g[j], d);
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      if (schunk == 0) reinterpret_cast<float*>(slot + 2 * RTILE + 512)[srow] = d;   // δ of query srow
+      if (tid < 32) {
+        uint16_t lh, lm, ll;
+        split3(-st.l * LOG2E, lh, lm, ll);
+        reinterpret_cast<uint4*>(slot + 2 * RTILE)[tid] =
+            make_uint4((uint32_t)lh | ((uint32_t)lm << 16), (uint32_t)ll | (0x3F80u << 16), 0x3F80u, 0u);
+      }
+    }
+    if constexpr (DROP) reinterpret_cast<uint16_t*>(slot + 2 * RTILE + 640)[wave * 64 + lane] = st.bits;
+  };
+  // dQ of query tile t (complete: every wave's adds precede the barrier that ended its iteration) -> bf16
+  auto flush = [&](int t) {
+    if (tid < 256) {
+      float* acc = dqacc + (t & 1) * 32 * kDqStride + srow * kDqStride + schunk * 8;
+      const float4 a = *reinterpret_cast<const float4*>(acc), c = *reinterpret_cast<const float4*>(acc + 4);
+      const float v[8] = {a.x * scale, a.y * scale, a.z * scale, a.w * scale,
+                          c.x * scale, c.y * scale, c.z * scale, c.w * scale};
+      const int q = t * 32 + srow;
+      if (q < L) *reinterpret_cast<uint4*>(dqkv + ((size_t)b * L + q) * ld + h * D + schunk * 8) = hq_pack8(v);
+      *reinterpret_cast<float4*>(acc) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(acc + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+
+  Stage st;
+  issue(0, st);
+  commit(0, st);
+  if (n32 > 1) issue(1, st);
+  __syncthreads();
+
+  const f32x16_t zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  f32x16_t dv[2] = {zero16, zero16}, dk[2] = {zero16, zero16};
+  const int krel = lane & 31;
+  const int hh_f = (krel >> 2) & 1;
+  const int r_f = (krel & 3) + 4 * (krel >> 3);
+  const float ksc = DROP ? kscale : 1.f;
+  for (int t = 0; t < n32; ++t) {
+    // fragment offsets recomputed per iteration from a laundered lane id (3 VALU each): without the
+    // launder the compiler hoists ~20 lane-constant LDS offsets out of the loop and, at 3 waves/SIMD
+    // (168-VGPR budget), spills them to scratch — each reload a vmcnt(0) wait behind the staged loads
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    auto R8 = [&](const uint16_t* tile, int s) { return lds_row8(tile, ln & 31, 16 * s + 8 * (ln >> 5)); };
+    auto T8 = [&](const uint16_t* tile, int s, int d) { return lds_tr8(tile, 0, s, d, ln); };
+    const char* slot = slots + (t & 1) * SLOT;
+    const uint16_t* tq = reinterpret_cast<const uint16_t*>(slot);
+    const uint16_t* to = tq + 32 * D;
+    if (t > 0) flush(t - 1);
+    if (active) {
+      const uint4 aw = reinterpret_cast<const uint4*>(slot + 2 * RTILE)[hh ? 0 : krel];
+      const bf16x8_t qa = hh ? bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0} : __builtin_bit_cast(bf16x8_t, u32x4{aw.x, aw.y, aw.z, aw.w});
+      f32x16_t s_acc = mfma32(R8(tq, 0), R8(tK, 0), zero16);
+#pragma unroll
+      for (int s = 1; s < 4; ++s) s_acc = mfma32(R8(tq, s), R8(tK, s), s_acc);
+      s_acc = mfma32(qa, kaug, s_acc);                   // S' = c·q·k + bias_k − lse_q (log2 domain)
+      f32x16_t p_acc = mfma32(R8(to, 0), R8(tV, 0), zero16);
+#pragma unroll
+      for (int s = 1; s < 4; ++s) p_acc = mfma32(R8(to, s), R8(tV, s), p_acc);
+      const uint16_t* wsrc = reinterpret_cast<const uint16_t*>(slot + 2 * RTILE + 640) + wave * 64 + 4 * hh + 32 * hh_f;
+      const float* sdl = reinterpret_cast<const float*>(slot + 2 * RTILE + 512);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        float pd[8], dsv[8];
+#pragma unroll
+        for (int gg = 0; gg < 2; ++gg) {
+          const int g = 2 * s + gg;
+          uint32_t lo = 0xFFFFFFFFu, hi = 0xFFFFFFFFu;
+          if constexpr (DROP) {
+            const uint64_t w = *reinterpret_cast<const uint64_t*>(wsrc + 8 * g);
+            lo = (uint32_t)w >> r_f;
+            hi = (uint32_t)(w >> 32) >> r_f;
+          }
+          const float4 d4 = *reinterpret_cast<const float4*>(sdl + 8 * g + 4 * hh);
+          const float mk[4] = {(lo & 1u) ? ksc : 0.f, ((lo >> 16) & 1u) ? ksc : 0.f, (hi & 1u) ? ksc : 0.f,
+                               ((hi >> 16) & 1u) ? ksc : 0.f};
+          const float dl[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int r = 4 * g + i;
+            const float P = __builtin_amdgcn_exp2f(s_acc[r]);
+            pd[4 * gg + i] = P * mk[i];
+            dsv[4 * gg + i] = (p_acc[r] * mk[i] - dl[i]) * P;
+          }
+          // dSᵀ image: key row krel, query columns 16s + 8gg + 4hh … +3 (one 8-byte store)
+          *reinterpret_cast<uint2*>(tS + lds_off(krel, scol + 16 * s + 8 * gg + 4 * hh)) =
+              make_uint2(hq_pack2(dsv[4 * gg], dsv[4 * gg + 1]), hq_pack2(dsv[4 * gg + 2], dsv[4 * gg + 3]));
+        }
+        const bf16x8_t pb = pack_b(pd, 0), sb = pack_b(dsv, 0);
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          dv[d] = mfma32(T8(to, s, d), pb, dv[d]);
+          dk[d] = mfma32(T8(tq, s, d), sb, dk[d]);
+        }
+      }
+      // dQ (queries on the rows, head dims on the lanes) = Σ_keys dS·K, keys on the MFMA K axis via the
+      // transposed reads of the dSᵀ and K images (same key order on both operands)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      float* accb = dqacc + (t & 1) * 32 * kDqStride;
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {   // one 32-column half at a time: 16 accumulator registers live
+        f32x16_t dq = mfma32(T8(tS, 0, wave & 1), T8(tK, 0, d), zero16);
+        dq = mfma32(T8(tS, 1, wave & 1), T8(tK, 1, d), dq);
+        if (dbg & 1) {   // timing experiment only (wrong dQ): plain stores instead of LDS atomics
+#pragma unroll
+          for (int r = 0; r < 16; ++r) accb[acc_row(r, hh) * kDqStride + d * 32 + krel] = dq[r];
+        } else if (!(dbg & 2)) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) atomicAdd(accb + acc_row(r, hh) * kDqStride + d * 32 + krel, dq[r]);
+        }
+      }
+    }
+    if (t + 1 < n32) {
+      commit(t + 1, st);   // slot (t+1)&1: last read in iteration t-1, before the barrier that ended it
+      __syncthreads();
+      if (t + 2 < n32) issue(t + 2, st);
+    } else {
+      __syncthreads();
+    }
+  }
+  flush(n32 - 1);
+  if (active && kok) {
+    uint16_t* out = dqkv + ((size_t)b * L + kj) * ld + h * D;
+    store_row64(out + 2 * H, dv, 1.f, hh);
+    store_row64(out + H, dk, LN2, hh);                   // Q' = c·Q with c = scale·log2e: dK = Σ dS·Q'/log2e
+  }
+}
+
 // waves per workgroup for a sequence of L: all 32-row subtiles of a head in one workgroup up to
 // 12 waves (L <= 384: 3 waves/SIMD), else 8 waves with the head split over grid.y.
 int waves_for(int L) {
@@ -1476,7 +1716,7 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
 
 void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx, const float* lse, const float* key_bias,
                  const uint16_t* mbits, uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p,
-                 float scale, hipStream_t s) {
+                 float scale, bool deterministic, hipStream_t s) {
   set_attn_prio();
   if (dh != D || L > 512) { fprintf(stderr, "hq_attn_bwd: head_dim %d / L %d unsupported\n", dh, L); abort(); }
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
@@ -1484,7 +1724,35 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
   const uint16_t* bits = thr ? mbits : nullptr;
   const int Lp = (L + 31) & ~31, n32 = Lp / 32;
   const char* ev = getenv("HQ_ATTN_BWD");
-  if (!ev || atoi(ev) == 3) {
+  const int variant = ev ? atoi(ev) : 3;
+  // v4 fused (opt-in, HQ_ATTN_BWD=4): one workgroup per (batch, head); its dQ sums the waves' key slices
+  // with LDS float atomics, so the summation order (last bits of dQ) varies run to run -> deterministic
+  // mode takes the two-kernel path.  Measured at B=256 L=384 (profiles/r2_attn): 4.9 ms, of which 4.3 ms
+  // are the ds_add_f32 (≈190 clk per 64-lane instruction); with the adds replaced by plain stores 595 /
+  // 655 µs (p = 0 / 0.1) vs v3 668-745 µs, so the design's ceiling is small and v3 stays the default.
+  if (variant == 4 && n32 <= 12 && !deterministic) {
+    auto run = [&](auto cw) {
+      constexpr int NW = decltype(cw)::value;
+      const size_t lds = 2 * (size_t)(2 * RTILE + 512 + 128 + NW * 128) + (2 * (size_t)NW + NW / 2) * 32 * D * 2 +
+                         2 * 32 * kDqStride * sizeof(float);
+      auto launch = [&](auto kern) {
+        static bool attr =
+            (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess);
+        (void)attr;
+        const char* ed = getenv("HQ_ATTN_FUSED_DBG");   // timing experiments (tools/attn_bench.py)
+        hipLaunchKernelGGL(kern, dim3(B * nh), dim3(NW * 64), lds, s, qkv, dctx, ctx, lse, key_bias, bits, dqkv, L, nh,
+                           scale * LOG2E, scale, ks, ed ? atoi(ed) : 0);
+      };
+      if (bits) launch(attn_bwd_fused_kernel<true, NW>);
+      else launch(attn_bwd_fused_kernel<false, NW>);
+    };
+    if (n32 <= 4) run(std::integral_constant<int, 4>{});
+    else if (n32 <= 8) run(std::integral_constant<int, 8>{});
+    else run(std::integral_constant<int, 12>{});
+    (void)delta;
+    return;
+  }
+  if (variant >= 3) {
     const int nb = (L + RQ - 1) / RQ;                 // 128-row blocks (queries for dQ, keys for dK/dV)
     constexpr int AH = 3;
     const size_t lds_dq = (size_t)(AH + 2) * 2 * RTILE + Lp * sizeof(uint4) + (bits ? (size_t)RW * n32 * 128 : 0);

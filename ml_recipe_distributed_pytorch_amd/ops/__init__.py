@@ -89,9 +89,18 @@ def attn_fwd(qkv, key_bias, B, L, nh, p, seed, opid, scale):
     return ctx, lse, None
 
 
+def deterministic() -> bool:
+    """Bitwise run-to-run reproducible kernels wanted: ``torch.use_deterministic_algorithms(True)`` or
+    ``HQ_DETERMINISTIC=1``.  Only the attention backward has a faster order-nondeterministic path (the
+    single-kernel backward sums dQ over key slices with LDS float atomics); the embedding-gradient
+    scatter stays atomic either way."""
+    return torch.are_deterministic_algorithms_enabled() or os.environ.get("HQ_DETERMINISTIC", "0") == "1"
+
+
 def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale):
     if dctx.is_cuda:
-        return _k().attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, int(B), int(L), int(nh), float(p), float(scale))
+        return _k().attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, int(B), int(L), int(nh), float(p), float(scale),
+                             deterministic())
     return ref.attn_bwd(dctx, qkv, ctx, lse, key_bias, B, L, nh, p, seed, opid, scale)
 
 

@@ -14,6 +14,7 @@ working), console + optional file output at ``dump_dir/<exp>/<date>.log``, and a
 from __future__ import annotations
 
 import logging
+import os
 import random
 import sys
 from typing import Optional
@@ -63,7 +64,11 @@ def get_logger(*, level=logging.INFO, filename=None, filemode="w", logger_name=N
 
 
 def set_seed(seed=None) -> Optional[int]:
-    """Seed python / numpy / torch (CPU and all HIP devices).  ``None`` leaves every generator alone."""
+    """Seed python / numpy / torch (CPU and all HIP devices).  ``None`` leaves every generator alone.
+
+    Like the reference (modules/utils.py:34-43, ``cudnn.deterministic = True``) a seed also selects the
+    run-to-run reproducible kernels: ``HQ_DETERMINISTIC=1`` routes the attention backward to its
+    two-kernel path instead of the single-kernel one with LDS-atomic dQ (ops.deterministic)."""
     if seed is None:
         return None
     seed = int(seed)
@@ -71,6 +76,7 @@ def set_seed(seed=None) -> Optional[int]:
         fn(seed)
     if torch.cuda.is_available():
         torch.cuda.manual_seed_all(seed)
+    os.environ["HQ_DETERMINISTIC"] = "1"
     logger.info(f"Random seed was set to {seed}. It can affect speed of training and performance of result model.")
     return seed
 

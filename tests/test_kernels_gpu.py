@@ -105,7 +105,7 @@ def test_gelu_and_bias_grad(cuda):
     _close(g2, d.float().sum(0), 1e-2, 1e-4, "bias_grad")
 
 
-def _attn_case(cuda, B, L, nh, p, masked, ramp=0.0, amp=1.0, ctx_tol=2e-2, left_pad=0):
+def _attn_case(cuda, B, L, nh, p, masked, ramp=0.0, amp=1.0, ctx_tol=2e-2, left_pad=0, det=False):
     k = _native.kernels()
     torch.manual_seed(3)
     H = nh * 64
@@ -122,15 +122,41 @@ def _attn_case(cuda, B, L, nh, p, masked, ramp=0.0, amp=1.0, ctx_tol=2e-2, left_
     _close(lse, lser, 1e-2, 1e-3, "lse")
     _close(ctx, ctxr, ctx_tol, 2e-2, "ctx")
     dctx = _bf(torch.randn(B * L, H))
-    dq = k.attn_bwd(dctx.to(cuda), qkv.to(cuda), ctx, lse, kb.to(cuda), bits, B, L, nh, p, scale)
+    dq = k.attn_bwd(dctx.to(cuda), qkv.to(cuda), ctx, lse, kb.to(cuda), bits, B, L, nh, p, scale, det)
     dqr = ref.attn_bwd(dctx, qkv, ctx.cpu(), lse.cpu(), kb, B, L, nh, p, 555, 3, scale)
     _close(dq, dqr, 3e-2, 3e-2, "dqkv")
 
 
 @pytest.mark.parametrize("L", [384, 512, 256, 128, 100, 24, 7])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_attention(cuda, L, p):
-    _attn_case(cuda, 2, L, 2, p, masked=True)
+@pytest.mark.parametrize("det", [False, True], ids=["fused", "det"])
+def test_attention(cuda, monkeypatch, L, p, det):
+    """fused: the opt-in single-kernel backward (HQ_ATTN_BWD=4, L <= 384, LDS-atomic dQ); det: the
+    deterministic flag, which keeps the default two-kernel backward (ring dQ + dK/dV kernels) either way."""
+    if not det:
+        monkeypatch.setenv("HQ_ATTN_BWD", "4")
+    _attn_case(cuda, 2, L, 2, p, masked=True, det=det)
+
+
+def test_attention_bwd_deterministic_mode_repeatable(cuda, monkeypatch):
+    """The deterministic backward is bitwise repeatable; the opt-in fused one agrees with it to fp32-sum
+    reordering."""
+    k = _native.kernels()
+    torch.manual_seed(5)
+    B, L, nh = 4, 384, 12
+    H = nh * 64
+    qkv = _bf(torch.randn(B * L, 3 * H)).to(cuda)
+    kb = torch.zeros(B, L, device=cuda)
+    kb[1, 300:] = -10000.0
+    ctx, lse, bits = k.attn_fwd(qkv, kb, B, L, nh, 0.1, 7, 1, 0.125)
+    dctx = _bf(torch.randn(B * L, H)).to(cuda)
+    d0 = k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125, True)
+    for _ in range(3):
+        assert torch.equal(k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125, True), d0)
+    monkeypatch.setenv("HQ_ATTN_BWD", "4")
+    f = k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125, False).float()
+    _close(f[:, :H], d0[:, :H].float(), 1e-2, 1e-2, "fused dQ vs deterministic")
+    _close(f[:, H:], d0[:, H:].float(), 1e-2, 1e-2, "fused dK/dV vs deterministic")
 
 
 def test_attention_bert_base_shape(cuda):
@@ -263,7 +289,7 @@ def test_attention_grid_scale_vs_fp32_oracle(cuda):
     _close(lse, lser, 1e-2, 1e-3, "lse")
     _close(ctx, ctxr, 2e-2, 2e-2, "ctx")
     dctx = _bf(torch.randn(B * L, H, device=cuda))
-    dq = k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125)
+    dq = k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125, False)
     dqr = ref.attn_bwd(dctx, qkv, ctx, lse, kb, B, L, nh, 0.1, 99, 5, 0.125)
     _close(dq, dqr, 3e-2, 3e-2, "dqkv")
 

@@ -20,6 +20,12 @@ pytestmark = pytest.mark.gpu
 _ATOMIC = ("word_embeddings", "position_embeddings")
 
 
+@pytest.fixture(autouse=True)
+def _deterministic(monkeypatch):
+    """Bitwise comparisons need the deterministic attention backward (ops.deterministic)."""
+    monkeypatch.setenv("HQ_DETERMINISTIC", "1")
+
+
 def _engine(dev, reducer_kw=None, seed=11, clip=0.0):
     from types import SimpleNamespace
     from ml_recipe_distributed_pytorch_amd.models.bert import BertForQuestionAnswering

@@ -70,8 +70,8 @@ def main():
         for rnd in range(a.rounds):
             for v in [x for x in a.bwd.split(",") if x]:
                 os.environ["HQ_ATTN_BWD"] = v
-                grads[v] = k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125)
-                tb = timeit(lambda: k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125))
+                grads[v] = k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125, False)
+                tb = timeit(lambda: k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125, False))
                 print(f"p={p} bwd v{v} round {rnd}: {tb:8.1f} us ({2.5 * fl_fwd / tb / 1e6:6.1f} TF)", flush=True)
         vs = list(grads)
         for v in vs[1:]:

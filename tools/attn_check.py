@@ -17,7 +17,7 @@ for L, p in ((128, 0.1), (100, 0.1), (128, 0.0)):
     kb = torch.zeros(B, L)
     ctx, lse, bits = k.attn_fwd(qkv.cuda(), kb.cuda(), B, L, nh, p, 555, 3, 0.125)
     dctx = torch.randn(B * L, H).bfloat16()
-    dq = k.attn_bwd(dctx.cuda(), qkv.cuda(), ctx, lse, kb.cuda(), bits, B, L, nh, p, 0.125).float().cpu()
+    dq = k.attn_bwd(dctx.cuda(), qkv.cuda(), ctx, lse, kb.cuda(), bits, B, L, nh, p, 0.125, False).float().cpu()
     dqr = ref.attn_bwd(dctx, qkv, ctx.cpu(), lse.cpu(), kb, B, L, nh, p, 555, 3, 0.125).float()
     for i, nm in enumerate("QKV"):
         a, b = dq[:, i * H:(i + 1) * H], dqr[:, i * H:(i + 1) * H]
