@@ -257,6 +257,22 @@ Tensor fp8_quant_delayed(Tensor x, Tensor state, int64_t phase) {
   return y;
 }
 
+// Quantise many bf16 segments of `x` into `y` (uint8/e4m3 buffer) in one launch, each under its own
+// delayed-scaling state row of `states` [nseg, 4].  seg: int64 [nseg, 4] = (x offset, y offset, n8,
+// first block); `blocks` = total blocks (last segment's first block + its block count).
+void fp8_quant_delayed_multi(Tensor x, Tensor y, Tensor seg, Tensor states, int64_t blocks, int64_t phase) {
+  check(x, BF16, "x"); check(states, F32, "states");
+  TORCH_CHECK(y.device() == x.device() && y.is_contiguous() && y.element_size() == 1, "fp8_quant_delayed_multi: y");
+  TORCH_CHECK(seg.device() == x.device() && seg.scalar_type() == at::kLong && seg.is_contiguous() && seg.dim() == 2 &&
+                  seg.size(1) == 4 && states.numel() == seg.size(0) * 4,
+              "fp8_quant_delayed_multi: seg int64 [n,4] / states f32 [n,4]");
+  c10::DeviceGuard g(x.device());
+  hq_fp8_quant_delayed_multi(ptr<uint16_t>(x), reinterpret_cast<uint8_t*>(y.data_ptr()), reinterpret_cast<const long long*>(seg.data_ptr<int64_t>()),
+                             (int)seg.size(0), blocks, ptr<float>(states), (int)(phase % 3), cur_stream());
+}
+
+int64_t fp8_quant_multi_blocks(int64_t n8) { return hq_fp8_quant_multi_blocks(n8); }
+
 void transpose_tiles(Tensor src, Tensor dst, Tensor tiles) {
   check(src, BF16, "src"); check(dst, BF16, "dst");
   TORCH_CHECK(tiles.device().is_cuda() && tiles.scalar_type() == at::kInt && tiles.is_contiguous() && tiles.dim() == 2 &&
@@ -581,6 +597,8 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("colsum_into", &colsum_into);
   m.def("fp8_quantize", &fp8_quantize);
   m.def("fp8_quant_delayed", &fp8_quant_delayed);
+  m.def("fp8_quant_delayed_multi", &fp8_quant_delayed_multi);
+  m.def("fp8_quant_multi_blocks", &fp8_quant_multi_blocks);
   m.def("gemm_fp8_supported", &gemm_fp8_supported);
   m.def("gemm_fp8", &gemm_fp8, py::arg("A8"), py::arg("B8"), py::arg("epi"), py::arg("bias"), py::arg("sa"), py::arg("sb"),
         py::arg("pre") = py::none(), py::arg("out8") = py::none(), py::arg("state") = py::none(), py::arg("phase") = 0);

@@ -67,6 +67,36 @@ __device__ __forceinline__ float hq_gelu_grad(float x) {
   return fmaf(x, d, c);
 }
 
+// GELU and GELU' of 8 values (the GELUD GEMM epilogues) in packed fp32 (v_pk_mul_f32 / v_pk_fma_f32, two
+// lanes' worth per instruction); only rcp / exp2 stay scalar.  Same operations in the same order as
+// hq_normal_cdf_pdf + fmaf(x, pdf, cdf) / x·cdf, so the results are bitwise those of the scalar form.
+typedef float hq_f2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ hq_f2_t hq_s2(float c) { return hq_f2_t{c, c}; }
+__device__ __forceinline__ hq_f2_t hq_fma2(hq_f2_t a, hq_f2_t b, hq_f2_t c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ void hq_gelu_grad8(float* x, float* g) {
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    const hq_f2_t v = {x[e], x[e + 1]};
+    const hq_f2_t z = hq_f2_t{fabsf(v.x), fabsf(v.y)} * hq_s2(0.70710678118654752f);
+    const hq_f2_t den = hq_fma2(hq_s2(0.3275911f), z, hq_s2(1.f));
+    const hq_f2_t t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+    hq_f2_t p = hq_fma2(hq_s2(1.061405429f), t, hq_s2(-1.453152027f));
+    p = hq_fma2(p, t, hq_s2(1.421413741f));
+    p = hq_fma2(p, t, hq_s2(-0.284496736f));
+    p = hq_fma2(p, t, hq_s2(0.254829592f)) * t;
+    const hq_f2_t ea = (v * v) * hq_s2(-0.72134752044448170f);
+    const hq_f2_t ex = {__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
+    const hq_f2_t q = (hq_s2(0.5f) * p) * ex;                       // Φ(-|x|)
+    const hq_f2_t omq = hq_s2(1.f) - q;
+    const hq_f2_t cdf = {v.x >= 0.f ? omq.x : q.x, v.y >= 0.f ? omq.y : q.y};
+    const hq_f2_t pdf = hq_s2(0.3989422804014327f) * ex;
+    const hq_f2_t gr = hq_fma2(v, pdf, cdf);
+    const hq_f2_t y = v * cdf;
+    g[e] = gr.x; g[e + 1] = gr.y;
+    x[e] = y.x; x[e + 1] = y.y;
+  }
+}
+
 // ------------------------------------------------------------------------------ reductions
 __device__ __forceinline__ float hq_wave_sum(float v) {
 #pragma unroll

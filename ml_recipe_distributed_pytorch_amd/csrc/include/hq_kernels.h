@@ -107,6 +107,9 @@ void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* b
                  const float* sb, uint8_t* C8, float* q8, int phase, int M, int N, int K, int epi, hipStream_t s);
 // delayed-scaling e4m3 quantiser (one pass): y = x / s(prev amax), amax tracked in q8 (see gemm_fp8.hip)
 void hq_fp8_quant_delayed(const uint16_t* x, uint8_t* y, size_t n, float* q8, int phase, hipStream_t s);
+long long hq_fp8_quant_multi_blocks(long long n8);   // blocks of one segment of n8 8-element groups
+void hq_fp8_quant_delayed_multi(const uint16_t* x, uint8_t* y, const long long* seg, int nseg, long long blocks,
+                                float* states, int phase, hipStream_t s);
 
 // tiles: int32 [ntiles][6] = (src_off, dst_off, rows, cols, r0, c0); src [rows][cols] -> dst [cols][rows]
 void hq_transpose_tiles(const uint16_t* src, uint16_t* dst, const int* tiles, int ntiles, hipStream_t s);

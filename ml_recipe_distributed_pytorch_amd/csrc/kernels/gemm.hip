@@ -222,13 +222,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
     } else if constexpr (EPI == HQ_EPI_GELUD) {
       float x[8], g[8];
       hq_unpack8(piece, x);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float c, d;
-        hq_normal_cdf_pdf(x[e], c, d);
-        g[e] = fmaf(x[e], d, c);   // gelu'(x)
-        x[e] *= c;                 // gelu(x)
-      }
+      hq_gelu_grad8(x, g);   // g = gelu'(x), x = gelu(x)
       *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
       piece = hq_pack8(x);
     } else if constexpr (EPI == HQ_EPI_DMUL) {
@@ -405,13 +399,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nts_kernel(const uint16_t* __rest
     } else if constexpr (EPI == HQ_EPI_GELUD) {
       float x[8], g[8];
       hq_unpack8(piece, x);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float c, d;
-        hq_normal_cdf_pdf(x[e], c, d);
-        g[e] = fmaf(x[e], d, c);
-        x[e] *= c;
-      }
+      hq_gelu_grad8(x, g);   // g = gelu'(x), x = gelu(x)
       *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
       piece = hq_pack8(x);
     } else if constexpr (EPI == HQ_EPI_DMUL) {
@@ -699,13 +687,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
     } else if constexpr (EPI == HQ_EPI_GELUD) {
       float x[8], g[8];
       hq_unpack8(piece, x);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float c, d;
-        hq_normal_cdf_pdf(x[e], c, d);
-        g[e] = fmaf(x[e], d, c);   // gelu'(x)
-        x[e] *= c;                 // gelu(x)
-      }
+      hq_gelu_grad8(x, g);   // g = gelu'(x), x = gelu(x)
       *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
       piece = hq_pack8(x);
     } else if constexpr (EPI == HQ_EPI_DMUL) {
@@ -1022,13 +1004,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
           } else {
             float x[8], g[8];
             hq_unpack8(piece, x);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              float c, d;
-              hq_normal_cdf_pdf(x[e], c, d);
-              g[e] = fmaf(x[e], d, c);
-              x[e] *= c;
-            }
+            hq_gelu_grad8(x, g);   // g = gelu'(x), x = gelu(x)
             const uint4 gp = hq_pack8(g);
             if (!(epi_flags & kDbgNoStore)) store16(P + goff, gp, epi_flags & kNtP);
             else asm volatile("" :: "v"(gp.x), "v"(gp.y), "v"(gp.z), "v"(gp.w));

@@ -210,13 +210,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
     if constexpr (EPI == HQ_EPI_GELUD) {
       float x[8], g[8];
       hq_unpack8(piece, x);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        float c, d;
-        hq_normal_cdf_pdf(x[e], c, d);
-        g[e] = fmaf(x[e], d, c);
-        x[e] *= c;
-      }
+      hq_gelu_grad8(x, g);   // g = gelu'(x), x = gelu(x)
       *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
       piece = hq_pack8(x);
       if constexpr (Q8) {
@@ -248,7 +242,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
       float m = red[0];
 #pragma unroll
       for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w]);
-      atomicMax(st + phase, __float_as_uint(m));
+      if (__float_as_uint(m) > __hip_atomic_load(st + phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(st + phase, __float_as_uint(m));   // monotonic slot: a stale read only costs a redundant atomic
     }
     if (blockIdx.x == 0 && tid == 0) {
       st[(phase + 1) % 3] = 0u;   // cleared for the step after next's accumulation
@@ -311,7 +306,64 @@ __global__ __launch_bounds__(256) void quant_delayed_kernel(const uint16_t* __re
   }
 }
 
+// Every weight of the model in ONE launch (ParamStore.view_fp8 after each optimizer step): segment g is
+// x[xo, xo + 8·n8) -> y[yo, …) under its own state states[g]; a block handles kQmBlk8 8-element groups
+// of one segment (segment g owns blocks blk[g] … blk[g+1]-1).  Same math as quant_delayed_kernel; the
+// per-block amax only reaches the atomic when it beats the slot's current value (monotonic, so a stale
+// read costs at most a redundant atomic) — 48 launches of ~13 µs each become one bandwidth-bound pass.
+constexpr int kQmBlk8 = 256 * 8;
+__global__ __launch_bounds__(256) void quant_delayed_multi_kernel(const uint16_t* __restrict__ x, uint8_t* __restrict__ y,
+                                                                  const long long* __restrict__ seg, int nseg,
+                                                                  float* __restrict__ states, int phase) {
+  int g = 0;
+  while (g + 1 < nseg && (long long)blockIdx.x >= seg[4 * (g + 1) + 3]) ++g;   // uniform scan, nseg <= ~100
+  const long long xo = seg[4 * g], yo = seg[4 * g + 1], n8 = seg[4 * g + 2], b0 = seg[4 * g + 3];
+  float* q8 = states + 4 * g;
+  const float s = delayed_scale(q8, phase);
+  const float inv = 1.f / s;
+  const uint4* xs = reinterpret_cast<const uint4*>(x + xo);
+  uint2* ys = reinterpret_cast<uint2*>(y + yo);
+  const long long i0 = ((long long)blockIdx.x - b0) * kQmBlk8;
+  const long long i1 = i0 + kQmBlk8 < n8 ? i0 + kQmBlk8 : n8;
+  float m = 0.f;
+  for (long long i = i0 + threadIdx.x; i < i1; i += 256) {
+    float f[8];
+    hq_unpack8(xs[i], f);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      m = fmaxf(m, fabsf(f[k]));
+      f[k] = fminf(fmaxf(f[k] * inv, -kFp8Max), kFp8Max);
+    }
+    uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+    lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+    uint32_t hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+    hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+    ys[i] = make_uint2(lo, hi);
+  }
+  m = hq_wave_max(m);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  unsigned* st = reinterpret_cast<unsigned*>(q8);
+  if (threadIdx.x == 0) {
+    const unsigned mb = __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+    if (mb > __hip_atomic_load(st + phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(st + phase, mb);
+    if (blockIdx.x == b0) {
+      st[(phase + 1) % 3] = 0u;
+      q8[3] = s;
+    }
+  }
+}
+
 }  // namespace
+
+long long hq_fp8_quant_multi_blocks(long long n8) { return (n8 + kQmBlk8 - 1) / kQmBlk8; }
+
+void hq_fp8_quant_delayed_multi(const uint16_t* x, uint8_t* y, const long long* seg, int nseg, long long blocks,
+                                float* states, int phase, hipStream_t s) {
+  if (blocks <= 0 || nseg <= 0) return;
+  hipLaunchKernelGGL(quant_delayed_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, y, seg, nseg, states, phase);
+}
 
 int hq_gemm_fp8_supported(int M, int N, int K) {
   return (M % BM == 0 && N % BN == 0 && K % BK == 0 && K >= 2 * BK && (size_t)BM * K < (1ull << 31) &&

@@ -21,8 +21,10 @@ constexpr int kRowsPerWave = 8;   // rows a wave walks in the backward kernels
 constexpr int kWaves = 4;         // 256-thread blocks
 
 // Q8 (--precision fp8): y is also written as e4m3 under the delayed scale of the consuming GEMM's input
-// state q8 (the next QKV / FFN1 projection reads it instead of a separate quantisation pass over y);
-// grid-stride rows so the amax needs one atomic per block (<= 2048 per call).
+// state q8 (the next QKV / FFN1 projection reads it instead of a separate quantisation pass over y).
+// One block per 4 rows as in the bf16 kernel (a 2048-block grid-stride variant serialised each wave's
+// rows: 157 vs 102 µs at T = 98304); a wave's amax reaches the atomic only when it beats the slot's
+// current value, so nearly all of the T waves skip it.
 template <int NCH, bool Q8>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict__ a, const uint16_t* __restrict__ resid,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -37,7 +39,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict_
     s8 = hq_fp8_delayed_scale(q8, phase);
     inv8 = 1.f / s8;
   }
-  const int stride = Q8 ? gridDim.x * kWaves : T;
+  const int stride = gridDim.x * kWaves;
   for (int row = blockIdx.x * kWaves + wave; row < T; row += stride) {
   const size_t base = (size_t)row * H;
   float v[NCH][4];
@@ -101,7 +103,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict_
     __syncthreads();
     if (threadIdx.x == 0) {
       const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-      atomicMax(reinterpret_cast<unsigned*>(q8) + phase, __float_as_uint(m));
+      unsigned* slot = reinterpret_cast<unsigned*>(q8) + phase;
+      if (__float_as_uint(m) > __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(slot, __float_as_uint(m));
       if (blockIdx.x == 0) {
         reinterpret_cast<unsigned*>(q8)[(phase + 1) % 3] = 0u;   // cleared for the step after next
         q8[3] = s8;                                              // dequant scale of this step's y8
@@ -694,9 +698,13 @@ void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, con
   const HqDropKey key = hq_drop_key(seed, opid);
   const float ks = hq_keep_scale(thr);
   const int blocks = (T + kWaves - 1) / kWaves;
+  static const int q8_rows = [] {   // rows per wave of the e4m3 variant (HQ_LNQ8_ROWS: A/B sweeps)
+    const char* e = getenv("HQ_LNQ8_ROWS");
+    return e ? std::max(1, atoi(e)) : 4;
+  }();
   dispatch_nch(H, [&](auto nch) {
     if (y8)
-      hipLaunchKernelGGL((ln_fwd_kernel<decltype(nch)::value, true>), dim3(std::min(blocks, 2048)), dim3(256), 0, s, a,
+      hipLaunchKernelGGL((ln_fwd_kernel<decltype(nch)::value, true>), dim3((T + q8_rows * kWaves - 1) / (q8_rows * kWaves)), dim3(256), 0, s, a,
                          resid, gamma, beta, y, z, mean, rstd, T, H, eps, key, thr, ks, y8, q8, phase);
     else
       hipLaunchKernelGGL((ln_fwd_kernel<decltype(nch)::value, false>), dim3(blocks), dim3(256), 0, s, a, resid, gamma,

@@ -72,6 +72,7 @@ class ParamStore:
         self._t_dirty = True
         self._fp8: Dict[str, Tuple[torch.Tensor, torch.Tensor]] = {}
         self._fp8_state: Dict[str, object] = {}
+        self._fp8_states_buf: Optional[torch.Tensor] = None
         self._fp8_dirty = True
 
     # ------------------------------------------------------------------ allocation
@@ -119,7 +120,6 @@ class ParamStore:
         self._dirty = False
         self._t_dirty = True
         self._fp8_dirty = True
-        self._fp8_dirty = True
         self.compute_t = None
         self._t_tiles = None
 
@@ -162,15 +162,43 @@ class ParamStore:
         if key not in self._t_off or not self._transposable():
             return None
         if self._fp8_dirty:
-            # one delayed-scaling pass per weight (the amax of the previous update sets the scale; the
-            # first call seeds it by current scaling) instead of memset + amax + quantise launches
-            from .. import ops
-            if not self._fp8_state or next(iter(self._fp8_state.values())).buf.device != self.compute.device:
-                self._fp8_state = {kk: ops.Fp8DelayedState(self.compute.device) for kk in self._t_keys}
-            self._fp8 = {kk: (self._fp8_state[kk].quantize(self.view(kk)), self._fp8_state[kk].scale)
-                         for kk in self._t_keys}
-            self._fp8_dirty = False
+            self._requantize_fp8()
         return self._fp8[key]
+
+    def _requantize_fp8(self):
+        """Every registered weight -> e4m3 in ONE launch (gemm_fp8.hip quant_delayed_multi_kernel), each
+        under its own delayed-scaling state (the amax of the previous update sets the scale); the first
+        call seeds every state by current scaling.  Replaces one launch per weight (48 × ~13 µs)."""
+        from .. import ops
+        from .._native import kernels
+        dev = self.compute.device
+        if not self._fp8_state or self._fp8_states_buf.device != dev:
+            n = len(self._t_keys)
+            self._fp8_states_buf = torch.zeros(n, 4, dtype=torch.float32, device=dev)
+            self._fp8_state = {kk: ops.Fp8DelayedState(dev, buf=self._fp8_states_buf[i])
+                               for i, kk in enumerate(self._t_keys)}
+            rows, yo, blk = [], 0, 0
+            for kk in self._t_keys:
+                e = self.by_key[kk]
+                assert e.numel % 8 == 0 and e.offset % 8 == 0, f"{kk}: fp8 quantisation needs 8-aligned segments"
+                rows.append([e.offset, yo, e.numel // 8, blk])
+                blk += kernels().fp8_quant_multi_blocks(e.numel // 8)
+                yo += (e.numel + 255) // 256 * 256
+            self._fp8_seg = torch.tensor(rows, dtype=torch.int64).to(dev)
+            self._fp8_blocks = blk
+            self._fp8_y = torch.empty(yo, dtype=torch.uint8, device=dev)
+            self._fp8_views = {kk: self._fp8_y[r[1]:r[1] + self.by_key[kk].numel].view(torch.float8_e4m3fn)
+                               .view(self.by_key[kk].shape) for kk, r in zip(self._t_keys, rows)}
+            self._fp8_step = 0
+            for i, kk in enumerate(self._t_keys):   # seed: slot (0 + 2) % 3 = amax of the weight itself
+                _, sc = kernels().fp8_quantize(self.view(kk))
+                self._fp8_states_buf[i, 2] = sc.reshape(()) * 448.0
+        phase = self._fp8_step % 3
+        self._fp8_step += 1
+        kernels().fp8_quant_delayed_multi(self.compute, self._fp8_y, self._fp8_seg, self._fp8_states_buf,
+                                          self._fp8_blocks, phase)
+        self._fp8 = {kk: (self._fp8_views[kk], self._fp8_state[kk].scale) for kk in self._t_keys}
+        self._fp8_dirty = False
 
     def view_t(self, key: str) -> Optional[torch.Tensor]:
         """Wᵀ of a registered weight, or None when unavailable (CPU / fp32 / not registered)."""

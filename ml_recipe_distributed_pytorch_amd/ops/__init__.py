@@ -174,8 +174,8 @@ class Fp8DelayedState:
     + the scale in use, see gemm_fp8.hip) and a host step counter selecting the slots — so neither the
     quantiser nor the GEMM ever synchronises with the host."""
 
-    def __init__(self, device):
-        self.buf = torch.zeros(4, dtype=torch.float32, device=device)
+    def __init__(self, device, buf: Optional[torch.Tensor] = None):
+        self.buf = torch.zeros(4, dtype=torch.float32, device=device) if buf is None else buf
         self.step = 0
 
     def next_phase(self) -> int:

@@ -98,3 +98,18 @@ def test_predictor_parser_validate_cfg():
     path = os.path.join(ROOT, "config", "validate.cfg")
     _, (p, m) = flags.get_params((flags.get_predictor_parser, flags.get_model_parser), ["-c", path])
     assert p.limit == 100 and p.split_by_sentence and p.truncate and p.max_seq_len == 512
+
+
+def test_set_seed_selects_deterministic_kernels(monkeypatch):
+    """Like the reference's set_seed (cudnn.deterministic = True), a seed selects the run-to-run
+    reproducible kernels (ops.deterministic); no seed leaves the choice alone."""
+    import random
+
+    from ml_recipe_distributed_pytorch_amd import ops
+    from ml_recipe_distributed_pytorch_amd.utils.logging import set_seed
+    monkeypatch.setenv("HQ_DETERMINISTIC", "0")   # restored (unset) at teardown
+    assert set_seed(None) is None and not ops.deterministic()
+    assert set_seed("7") == 7 and ops.deterministic()
+    a = random.random()
+    set_seed(7)
+    assert random.random() == a

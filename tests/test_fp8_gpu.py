@@ -141,3 +141,35 @@ def test_fp8_model_step_runs_on_own_kernels(cuda):
     sum(v.float().mean() for v in out.values()).backward()
     torch.cuda.synchronize()
     assert torch.isfinite(m.store.grad).all()
+
+
+@pytest.mark.gpu
+def test_fp8_quant_delayed_multi_matches_per_tensor(cuda):
+    """All weights in one launch (ParamStore.view_fp8): each segment under its own state row, bitwise
+    equal to the per-tensor quantiser with the same state, over three phases (amax slots rotate)."""
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(9)
+    sizes = [768 * 2304, 768 * 768, 64, 3072 * 768 + 8]
+    offs, o = [], 0
+    for n in sizes:
+        offs.append(o)
+        o += (n + 63) // 64 * 64
+    x = (torch.randn(o, device=cuda, generator=g) * 0.05).bfloat16()
+    for i, n in enumerate(sizes):   # different magnitudes per segment
+        x[offs[i]:offs[i] + n] *= 10.0 ** (i - 1)
+    states = torch.zeros(len(sizes), 4, device=cuda)
+    states[:, 2] = torch.tensor([0.3, 5.0, 0.0, 40.0], device=cuda)   # seeded "previous amax"
+    ref_states = [states[i].clone() for i in range(len(sizes))]
+    rows, yo, blk = [], 0, 0
+    for off, n in zip(offs, sizes):
+        rows.append([off, yo, n // 8, blk])
+        blk += k.fp8_quant_multi_blocks(n // 8)
+        yo += (n + 255) // 256 * 256
+    seg = torch.tensor(rows, dtype=torch.int64, device=cuda)
+    y = torch.zeros(yo, dtype=torch.uint8, device=cuda)
+    for phase in range(3):
+        k.fp8_quant_delayed_multi(x, y, seg, states, blk, phase)
+        for i, (off, n) in enumerate(zip(offs, sizes)):
+            exp = k.fp8_quant_delayed(x[off:off + n], ref_states[i], phase)
+            assert torch.equal(y[rows[i][1]:rows[i][1] + n], exp.view(torch.uint8)), (phase, i)
+            assert torch.equal(states[i], ref_states[i]), (phase, i)

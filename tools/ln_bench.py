@@ -40,8 +40,10 @@ def main():
     dy = torch.randn(T, H, device=dev).bfloat16()
     gg, gb, gbias = torch.zeros(H, device=dev), torch.zeros(H, device=dev), torch.zeros(H, device=dev)
     mb = T * H * 2 / 1e6
+    st8 = torch.zeros(4, device=dev)
     for name, fn, nbytes in (
             ("ln_fwd", lambda: k.ln_fwd(x, r, g, b, 1e-12, 0.1, 1, 0), 4 * mb),
+            ("ln_fwd + e4m3 (fp8)", lambda: k.ln_fwd(x, r, g, b, 1e-12, 0.1, 1, 0, q8=st8, phase=0), 4.5 * mb),
             ("ln_bwd (dy)", lambda: k.ln_bwd(dy, None, z, g, mean, rstd, 0.1, 1, 0, gg, gb, gbias, False), 4 * mb),
             ("ln_bwd (dy + dy2)", lambda: k.ln_bwd(dy, r, z, g, mean, rstd, 0.1, 1, 0, gg, gb, gbias, False), 5 * mb)):
         us = sorted(timeit(fn) for _ in range(5))[2]
