@@ -370,17 +370,25 @@ void check_attn(const Tensor& qkv, const Tensor& kb, int64_t B, int64_t L, int64
 }
 
 std::vector<Tensor> attn_fwd(Tensor qkv, Tensor key_bias, int64_t B, int64_t L, int64_t nh, double p, int64_t seed,
-                             int64_t opid, double scale) {
+                             int64_t opid, double scale, c10::optional<Tensor> q8, int64_t phase) {
   check_attn(qkv, key_bias, B, L, nh);
   const int64_t H = qkv.size(1) / 3;
+  const bool want8 = q8.has_value() && q8->defined();
+  if (want8) {
+    check(*q8, F32, "q8");
+    TORCH_CHECK(q8->numel() == 4, "q8 must be the f32[4] delayed-scaling state");
+  }
   c10::DeviceGuard g(qkv.device());
   auto ctx = at::empty({B * L, H}, qkv.options());
   auto lse = at::empty({B, nh, L}, key_bias.options());
   const int64_t mbytes = p > 0 ? (int64_t)hq_attn_mask_bytes((int)B, (int)L, (int)nh) : 0;
   auto mbits = at::empty({mbytes / 2}, qkv.options().dtype(at::kShort));
+  Tensor ctx8 = want8 ? at::empty({B * L, H}, qkv.options().dtype(at::kFloat8_e4m3fn)) : Tensor();
   hq_attn_fwd(ptr<uint16_t>(qkv), ptr<float>(key_bias), ptr<uint16_t>(ctx), ptr<float>(lse),
               mbytes ? ptr<uint16_t>(mbits) : nullptr, (int)B, (int)L, (int)nh, 64, (float)p, u32(seed), u32(opid),
-              (float)scale, cur_stream());
+              (float)scale, cur_stream(), want8 ? reinterpret_cast<uint8_t*>(ctx8.data_ptr()) : nullptr,
+              want8 ? ptr<float>(*q8) : nullptr, (int)(phase % 3));
+  if (want8) return {ctx, lse, mbits, ctx8};
   return {ctx, lse, mbits};
 }
 
@@ -617,7 +625,9 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("qa_heads_bwd", &qa_heads_bwd);
   m.def("gelu_bwd", &gelu_bwd);
   m.def("bias_grad", &bias_grad);
-  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("key_bias"), py::arg("B"), py::arg("L"), py::arg("nh"),
+        py::arg("p"), py::arg("seed"), py::arg("opid"), py::arg("scale"), py::arg("q8") = py::none(),
+        py::arg("phase") = 0);
   m.def("attn_bwd", &attn_bwd);
   m.def("grad_norm", &grad_norm);
   m.def("sq_norm_partials", [](Tensor x, int64_t nparts) {

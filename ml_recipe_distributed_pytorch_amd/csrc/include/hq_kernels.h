@@ -45,8 +45,10 @@ void hq_bias_grad(const uint16_t* dy, float* part, HqOuts outs, int T, int N, bo
 
 // ---- attention.hip ----------------------------------------------------------------------------
 size_t hq_attn_mask_bytes(int B, int L, int nh);   // dropout keep-bits written by fwd, read by bwd
+// ctx8 / q8 / phase (optional, --precision fp8): ctx also written as e4m3 under the delayed-scaling state q8
 void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, float* lse, uint16_t* mbits, int B, int L,
-                 int nh, int dh, float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s);
+                 int nh, int dh, float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s,
+                 uint8_t* ctx8 = nullptr, float* q8 = nullptr, int phase = 0);
 void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx, const float* lse, const float* key_bias,
                  const uint16_t* mbits, uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p, float scale,
                  bool deterministic, hipStream_t s);
@@ -108,6 +110,10 @@ void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* b
 // delayed-scaling e4m3 quantiser (one pass): y = x / s(prev amax), amax tracked in q8 (see gemm_fp8.hip)
 void hq_fp8_quant_delayed(const uint16_t* x, uint8_t* y, size_t n, float* q8, int phase, hipStream_t s);
 long long hq_fp8_quant_multi_blocks(long long n8);   // blocks of one segment of n8 8-element groups
+// fp8 producers write per-wave amax partials into this device scratch (>= n floats, current device) and
+// hq_fp8_amax_fold folds them into the delayed-scaling state q8 (slot `phase`, clears (phase+1)%3, q8[3])
+float* hq_fp8_amax_parts(size_t n);
+void hq_fp8_amax_fold(const float* part, int n, float* q8, int phase, hipStream_t s);
 void hq_fp8_quant_delayed_multi(const uint16_t* x, uint8_t* y, const long long* seg, int nseg, long long blocks,
                                 float* states, int phase, hipStream_t s);
 

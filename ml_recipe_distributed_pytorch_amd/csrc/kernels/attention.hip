@@ -145,6 +145,32 @@ __device__ __forceinline__ void store_row64(uint16_t* out, const f32x16_t (&a)[2
     }
 }
 
+// store_row64 plus the same 8 bf16-rounded values per lane as e4m3 (x·inv8) at out8 (same element
+// offsets, one byte each); returns this lane's |max| for the delayed-scaling amax.
+__device__ __forceinline__ float store_row64_q8(uint16_t* out, uint8_t* out8, const f32x16_t (&a)[2], float mul,
+                                                float inv8, int hh) {
+  float amax = 0.f;
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; g += 2) {
+      const float va[4] = {a[d][4 * g] * mul, a[d][4 * g + 1] * mul, a[d][4 * g + 2] * mul, a[d][4 * g + 3] * mul};
+      const float vb[4] = {a[d][4 * g + 4] * mul, a[d][4 * g + 5] * mul, a[d][4 * g + 6] * mul, a[d][4 * g + 7] * mul};
+      const uint2 A = hq_pack4(va), B = hq_pack4(vb);
+      const auto r0 = __builtin_amdgcn_permlane32_swap(A.x, B.x, false, false);
+      const auto r1 = __builtin_amdgcn_permlane32_swap(A.y, B.y, false, false);
+      const uint4 w = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+      const int col = d * 32 + 8 * g + 8 * hh;
+      *reinterpret_cast<uint4*>(out + col) = w;
+      float f[8];
+      hq_unpack8(w, f);   // quantise the bf16-rounded ctx, exactly what the bf16 copy holds
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(f[e]));
+      *reinterpret_cast<uint2*>(out8 + col) = make_uint2(hq_pack_fp8x4(f, inv8), hq_pack_fp8x4(f + 4, inv8));
+    }
+  return amax;
+}
+
 // Static issue priority of a workgroup's waves for the whole main loop (MI355X_MICROARCH "Two waves per
 // SIMD", item 4): VALU issue on a SIMD goes to the higher-priority, then the older wave.  g_attn_prio
 // (host: HQ_ATTN_PRIO) 0 = off, 1 = second half of the waves at prio 1, 2 = three levels (3 waves/SIMD).
@@ -461,7 +487,10 @@ __global__ __launch_bounds__(RW * 64, DROP ? 3 : 4) void attn_fwd_ring_kernel(co
                                                                    uint16_t* __restrict__ ctx, float* __restrict__ lse,
                                                                    uint16_t* __restrict__ mbits, int L, int nh,
                                                                    int n_qb, float c_scale, HqDropKey kd_,
-                                                                   uint32_t thr, float kscale, int force_slow) {
+                                                                   uint32_t thr, float kscale, int force_slow,
+                                                                   uint8_t* __restrict__ ctx8,
+                                                                   const float* __restrict__ q8,
+                                                                   float* __restrict__ part8, int phase) {
   const uint32_t key = kd_.get();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
@@ -558,6 +587,7 @@ __global__ __launch_bounds__(RW * 64, DROP ? 3 : 4) void attn_fwd_ring_kernel(co
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     (void)__syncthreads_or(0);                         // the workgroup's slow-path vote (below)
+    if (ctx8 != nullptr && lane == 0) part8[blockIdx.x * RW + wave] = 0.f;   // its (empty) amax partial
     return;
   }
   // Branch-free tile loop: a per-tile rescale branch makes hipcc copy the 32 O registers across the join
@@ -705,6 +735,18 @@ __global__ __launch_bounds__(RW * 64, DROP ? 3 : 4) void attn_fwd_ring_kernel(co
     l_tot = xor32_sum(l2.x + l2.y);
   }
   const float inv = (DROP ? kscale : 1.f) / l_tot;
+  if (ctx8 != nullptr) {   // --precision fp8: ctx also in e4m3 for the out-projection (delayed scaling)
+    const float s8 = hq_fp8_delayed_scale(q8, phase);
+    float amax = 0.f;
+    if (qi < L) {
+      const size_t row = ((size_t)b * L + qi) * H + h * D;
+      amax = store_row64_q8(ctx + row, ctx8 + row, o, inv, 1.f / s8, hh);
+      if (hh == 0) lse[(size_t)bh * L + qi] = (m_b + __builtin_amdgcn_logf(l_tot)) * LN2;
+    }
+    amax = hq_wave_max(amax);   // -> this wave's partial slot, folded by hq_fp8_amax_fold (no atomics)
+    if (lane == 0) part8[blockIdx.x * RW + wave] = amax;
+    return;
+  }
   if (qi < L) {  // lanes q and q+32 share qi: the permlane partners are active together
     store_row64(ctx + ((size_t)b * L + qi) * H + h * D, o, inv, hh);
     if (hh == 0) lse[(size_t)bh * L + qi] = (m_b + __builtin_amdgcn_logf(l_tot)) * LN2;  // v_log_f32 = log2
@@ -1649,9 +1691,11 @@ static int attn_force_slow() {  // tests: HQ_ATTN_FORCE_SLOW=1 sends every workg
 }
 
 void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, float* lse, uint16_t* mbits, int B, int L,
-                 int nh, int dh, float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s) {
+                 int nh, int dh, float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s, uint8_t* ctx8,
+                 float* q8, int phase) {
   set_attn_prio();
   if (dh != D || L > 512) { fprintf(stderr, "hq_attn_fwd: head_dim %d / L %d unsupported\n", dh, L); abort(); }
+  if (ctx8 && attn_fwd_variant() != 3) { fprintf(stderr, "hq_attn_fwd: e4m3 ctx needs the ring forward (v3)\n"); abort(); }
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const HqDropKey key = hq_drop_key(seed, opid);
   const int Lp = (L + 31) & ~31, n32 = Lp / 32;
@@ -1661,6 +1705,8 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
     const char* ea = getenv("HQ_ATTN_AHEAD");
     const int ahead = ea ? atoi(ea) : 2;
     const size_t lds = (size_t)(ahead == 2 ? 4 : 6) * 2 * RTILE + Lp * sizeof(uint2);
+    const int nparts = B * nh * n_qb * RW;
+    float* part8 = ctx8 ? hq_fp8_amax_parts((size_t)nparts) : nullptr;
     auto run = [&](auto cn) {
       constexpr int NT = decltype(cn)::value;
       auto launch1 = [&](auto kern) {
@@ -1668,7 +1714,8 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
             (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess);
         (void)attr;
         hipLaunchKernelGGL(kern, dim3(B * nh * n_qb), dim3(RW * 64), lds, s, qkv, key_bias, ctx, lse,
-                           thr ? mbits : nullptr, L, nh, n_qb, scale * LOG2E, key, thr, hq_keep_scale(thr), force_slow);
+                           thr ? mbits : nullptr, L, nh, n_qb, scale * LOG2E, key, thr, hq_keep_scale(thr), force_slow,
+                           ctx8, q8, part8, phase);
       };
       auto launch = [&](auto k2, auto k4) { if (ahead == 2) launch1(k2); else launch1(k4); };
       // EVEN (L % 32 == 0) also selects the unclamped DMA addressing: never pass it for a ragged L
@@ -1688,6 +1735,7 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
     else if (L == 256) run(std::integral_constant<int, 8>{});
     else if (L == 128) run(std::integral_constant<int, 4>{});
     else run(std::integral_constant<int, 0>{});
+    if (ctx8) hq_fp8_amax_fold(part8, nparts, q8, phase, s);
     return;
   }
   const int nw = waves_for(L);

@@ -19,6 +19,8 @@
 // into slot `phase`, slot (phase+1)%3 is cleared for the step after, and the scale used is stored in
 // state[3] for the consumer GEMM's dequantisation.  No host synchronisation anywhere.
 #include <algorithm>
+#include <cstdio>
+#include <vector>
 
 #include "hq_common.h"
 #include "hq_kernels.h"
@@ -64,8 +66,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
                                                                uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                                uint16_t* __restrict__ P, const float* __restrict__ sa,
                                                                const float* __restrict__ sb, uint8_t* __restrict__ C8,
-                                                               float* __restrict__ q8, int phase, int M, int N, int K,
-                                                               int lda, int ldb, int ldc) {
+                                                               const float* __restrict__ q8, float* __restrict__ part8,
+                                                               int phase, int M, int N, int K, int lda, int ldb, int ldc) {
   constexpr int PANEL = 256 * 128, STAGE = 2 * PANEL;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -230,25 +232,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
     }
     *reinterpret_cast<uint4*>(C + goff) = piece;
   }
-  if constexpr (Q8) {
-    // one atomic per BLOCK: per-wave atomics on the single amax word serialised in L2 (~+300 µs/call)
+  if constexpr (Q8) {   // this wave's amax -> its own partial slot (hq_fp8_amax_fold reduces them)
     amax = hq_wave_max(amax);
-    __syncthreads();                                  // every wave is done with its staging region
-    float* red = reinterpret_cast<float*>(smem);
-    if (lane == 0) red[wave] = amax;
-    __syncthreads();
-    unsigned* st = reinterpret_cast<unsigned*>(q8);
-    if (tid == 0) {
-      float m = red[0];
-#pragma unroll
-      for (int w = 1; w < 8; ++w) m = fmaxf(m, red[w]);
-      if (__float_as_uint(m) > __hip_atomic_load(st + phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMax(st + phase, __float_as_uint(m));   // monotonic slot: a stale read only costs a redundant atomic
-    }
-    if (blockIdx.x == 0 && tid == 0) {
-      st[(phase + 1) % 3] = 0u;   // cleared for the step after next's accumulation
-      q8[3] = s8;                 // dequant scale of this step's C8
-    }
+    if (lane == 0) part8[blockIdx.x * (kThreads / 64) + wave] = amax;
   }
 }
 
@@ -267,8 +253,11 @@ void launch(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, 
     return true;
   }();
   (void)init;
-  hipLaunchKernelGGL((gemm_fp8_kernel<EPI, Q8>), dim3((M / BM) * (N / BN)), dim3(kThreads), lds, s, A, B, C, bias, P, sa, sb,
-                     C8, q8, phase, M, N, K, K, K, N);
+  const int grid = (M / BM) * (N / BN);
+  float* part8 = Q8 ? hq_fp8_amax_parts((size_t)grid * (kThreads / 64)) : nullptr;
+  hipLaunchKernelGGL((gemm_fp8_kernel<EPI, Q8>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, sa, sb,
+                     C8, q8, part8, phase, M, N, K, K, K, N);
+  if (Q8) hq_fp8_amax_fold(part8, grid * (kThreads / 64), q8, phase, s);
 }
 
 // ------------------------------------------------------------------ delayed-scaling quantiser
@@ -276,7 +265,8 @@ void launch(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, 
 // into slot `phase`, slot (phase+1)%3 cleared, s stored in state[3].  One read of x instead of the
 // current-scaling path's two.
 __global__ __launch_bounds__(256) void quant_delayed_kernel(const uint16_t* __restrict__ x, uint2* __restrict__ y, size_t n8,
-                                                            float* __restrict__ q8, int phase) {
+                                                            const float* __restrict__ q8, float* __restrict__ part,
+                                                            int phase) {
   const float s = delayed_scale(q8, phase);
   const float inv = 1.f / s;
   float m = 0.f;
@@ -295,15 +285,7 @@ __global__ __launch_bounds__(256) void quant_delayed_kernel(const uint16_t* __re
     y[i] = make_uint2(lo, hi);
   }
   m = hq_wave_max(m);
-  __shared__ float red[4];
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  unsigned* st = reinterpret_cast<unsigned*>(q8);
-  if (threadIdx.x == 0) atomicMax(st + phase, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st[(phase + 1) % 3] = 0u;
-    q8[3] = s;
-  }
+  if ((threadIdx.x & 63) == 0) part[blockIdx.x * 4 + (threadIdx.x >> 6)] = m;
 }
 
 // Every weight of the model in ONE launch (ParamStore.view_fp8 after each optimizer step): segment g is
@@ -314,11 +296,12 @@ __global__ __launch_bounds__(256) void quant_delayed_kernel(const uint16_t* __re
 constexpr int kQmBlk8 = 256 * 8;
 __global__ __launch_bounds__(256) void quant_delayed_multi_kernel(const uint16_t* __restrict__ x, uint8_t* __restrict__ y,
                                                                   const long long* __restrict__ seg, int nseg,
-                                                                  float* __restrict__ states, int phase) {
+                                                                  const float* __restrict__ states,
+                                                                  float* __restrict__ part, int phase) {
   int g = 0;
   while (g + 1 < nseg && (long long)blockIdx.x >= seg[4 * (g + 1) + 3]) ++g;   // uniform scan, nseg <= ~100
   const long long xo = seg[4 * g], yo = seg[4 * g + 1], n8 = seg[4 * g + 2], b0 = seg[4 * g + 3];
-  float* q8 = states + 4 * g;
+  const float* q8 = states + 4 * g;
   const float s = delayed_scale(q8, phase);
   const float inv = 1.f / s;
   const uint4* xs = reinterpret_cast<const uint4*>(x + xo);
@@ -341,17 +324,55 @@ __global__ __launch_bounds__(256) void quant_delayed_multi_kernel(const uint16_t
     ys[i] = make_uint2(lo, hi);
   }
   m = hq_wave_max(m);
-  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) part[blockIdx.x * 4 + (threadIdx.x >> 6)] = m;
+}
+
+// ------------------------------------------------------------------ amax fold
+// The fp8 producers (LN forward, attention ctx store, FFN1 epilogue, the quantisers) write one amax per
+// wave into a scratch array instead of atomics on the state word: tens of thousands of same-address
+// atomics serialise in one L2 channel (measured: 36.9 K per-wave atomics turned a 236 µs attention
+// forward into 967 µs).  This single-block kernel then folds the partials into slot `phase`, clears slot
+// (phase+1)%3 and stores the scale the producer used in state[3] — segment g of a multi-segment call
+// (blockIdx.x = g) folds partials [4·blk[g], 4·blk[g+1]).
+__global__ __launch_bounds__(1024) void amax_fold_kernel(const float* __restrict__ part, const long long* __restrict__ seg,
+                                                         int nseg, long long nblk, int n, float* __restrict__ states,
+                                                         int phase) {
+  const int g = blockIdx.x;
+  long long i0 = 0, i1 = n;
+  if (seg != nullptr) {
+    i0 = 4 * seg[4 * g + 3];
+    i1 = 4 * (g + 1 < nseg ? seg[4 * (g + 1) + 3] : nblk);
+  }
+  float* q8 = states + 4 * g;
+  // partial counts are multiples of 4 (4 or 8 waves per producer block): float4 loads, 4 in flight
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  const long long j0 = i0 >> 2, j1 = i1 >> 2;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), c = a;
+  long long j = j0 + threadIdx.x;
+  for (; j + 3 * 1024 < j1; j += 4 * 1024) {
+    const float4 v0 = p4[j], v1 = p4[j + 1024], v2 = p4[j + 2048], v3 = p4[j + 3072];
+    a.x = fmaxf(fmaxf(a.x, v0.x), v1.x); a.y = fmaxf(fmaxf(a.y, v0.y), v1.y);
+    a.z = fmaxf(fmaxf(a.z, v0.z), v1.z); a.w = fmaxf(fmaxf(a.w, v0.w), v1.w);
+    c.x = fmaxf(fmaxf(c.x, v2.x), v3.x); c.y = fmaxf(fmaxf(c.y, v2.y), v3.y);
+    c.z = fmaxf(fmaxf(c.z, v2.z), v3.z); c.w = fmaxf(fmaxf(c.w, v2.w), v3.w);
+  }
+  for (; j < j1; j += 1024) {
+    const float4 v = p4[j];
+    a.x = fmaxf(a.x, v.x); a.y = fmaxf(a.y, v.y); a.z = fmaxf(a.z, v.z); a.w = fmaxf(a.w, v.w);
+  }
+  float m = fmaxf(fmaxf(fmaxf(a.x, a.y), fmaxf(a.z, a.w)), fmaxf(fmaxf(c.x, c.y), fmaxf(c.z, c.w)));
+  m = hq_wave_max(m);
+  __shared__ float red[16];
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  unsigned* st = reinterpret_cast<unsigned*>(q8);
   if (threadIdx.x == 0) {
-    const unsigned mb = __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
-    if (mb > __hip_atomic_load(st + phase, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(st + phase, mb);
-    if (blockIdx.x == b0) {
-      st[(phase + 1) % 3] = 0u;
-      q8[3] = s;
-    }
+#pragma unroll
+    for (int w = 1; w < 16; ++w) m = fmaxf(m, red[w]);   // m = red[0] here (thread 0's wave)
+    unsigned* st = reinterpret_cast<unsigned*>(q8);
+    const float s = delayed_scale(q8, phase);
+    st[phase] = __float_as_uint(fmaxf(__uint_as_float(st[phase]), m));
+    st[(phase + 1) % 3] = 0u;   // cleared for the step after next's accumulation
+    q8[3] = s;                  // dequant scale of this step's e4m3 output
   }
 }
 
@@ -362,7 +383,32 @@ long long hq_fp8_quant_multi_blocks(long long n8) { return (n8 + kQmBlk8 - 1) / 
 void hq_fp8_quant_delayed_multi(const uint16_t* x, uint8_t* y, const long long* seg, int nseg, long long blocks,
                                 float* states, int phase, hipStream_t s) {
   if (blocks <= 0 || nseg <= 0) return;
-  hipLaunchKernelGGL(quant_delayed_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, y, seg, nseg, states, phase);
+  float* part = hq_fp8_amax_parts((size_t)blocks * 4);
+  hipLaunchKernelGGL(quant_delayed_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, y, seg, nseg, states, part,
+                     phase);
+  hipLaunchKernelGGL(amax_fold_kernel, dim3(nseg), dim3(1024), 0, s, part, seg, nseg, blocks, 0, states, phase);
+}
+
+float* hq_fp8_amax_parts(size_t n) {
+  // per-device scratch, grown on demand and never freed while kernels may still read it (the old block is
+  // kept: a grow happens a handful of times per process).  Producers and their fold share one stream.
+  static std::vector<std::pair<float*, size_t>> bufs;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if ((int)bufs.size() <= dev) bufs.resize(dev + 1, {nullptr, 0});
+  auto& b = bufs[dev];
+  if (b.second < n) {
+    const size_t cap = std::max<size_t>(n, 1 << 18);
+    float* p = nullptr;
+    if (hipMalloc(&p, cap * sizeof(float)) != hipSuccess) { fprintf(stderr, "hq_fp8_amax_parts: hipMalloc failed\n"); abort(); }
+    b = {p, cap};
+  }
+  return b.first;
+}
+
+void hq_fp8_amax_fold(const float* part, int n, float* q8, int phase, hipStream_t s) {
+  if (n % 4 != 0) { fprintf(stderr, "hq_fp8_amax_fold: %d partials (must be a multiple of 4)\n", n); abort(); }
+  hipLaunchKernelGGL(amax_fold_kernel, dim3(1), dim3(1024), 0, s, part, nullptr, 1, 0LL, n, q8, phase);
 }
 
 int hq_gemm_fp8_supported(int M, int N, int K) {
@@ -382,7 +428,9 @@ void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* b
 
 void hq_fp8_quant_delayed(const uint16_t* x, uint8_t* y, size_t n, float* q8, int phase, hipStream_t s) {
   const size_t n8 = n / 8;
-  const int grid = (int)std::min<size_t>((n8 + 255) / 256, 256 * 4);   // ≤ 1024 block-level atomics
-  hipLaunchKernelGGL(quant_delayed_kernel, dim3(grid ? grid : 1), dim3(256), 0, s, x, reinterpret_cast<uint2*>(y), n8, q8,
+  const int grid = std::max(1, (int)std::min<size_t>((n8 + 255) / 256, 256 * 8));
+  float* part = hq_fp8_amax_parts((size_t)grid * 4);
+  hipLaunchKernelGGL(quant_delayed_kernel, dim3(grid), dim3(256), 0, s, x, reinterpret_cast<uint2*>(y), n8, q8, part,
                      phase);
+  hq_fp8_amax_fold(part, grid * 4, q8, phase, s);
 }

@@ -22,16 +22,17 @@ constexpr int kWaves = 4;         // 256-thread blocks
 
 // Q8 (--precision fp8): y is also written as e4m3 under the delayed scale of the consuming GEMM's input
 // state q8 (the next QKV / FFN1 projection reads it instead of a separate quantisation pass over y).
-// One block per 4 rows as in the bf16 kernel (a 2048-block grid-stride variant serialised each wave's
-// rows: 157 vs 102 µs at T = 98304); a wave's amax reaches the atomic only when it beats the slot's
-// current value, so nearly all of the T waves skip it.
+// Each wave walks q8_rows rows; its amax goes to a partial slot that hq_fp8_amax_fold reduces (no
+// same-address atomics: those serialise in one L2 channel — a per-block filtered atomic still cost
+// +27 µs at T = 98304, a per-wave one +97 µs).
 template <int NCH, bool Q8>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict__ a, const uint16_t* __restrict__ resid,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      uint16_t* __restrict__ y, uint16_t* __restrict__ z,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out, int T,
                                                      int H, float eps, HqDropKey kd_, uint32_t thr, float kscale,
-                                                     uint8_t* __restrict__ y8, float* __restrict__ q8, int phase) {
+                                                     uint8_t* __restrict__ y8, const float* __restrict__ q8,
+                                                     float* __restrict__ part8, int phase) {
   const uint32_t key = kd_.get();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float amax = 0.f, inv8 = 1.f, s8 = 1.f;
@@ -96,21 +97,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict_
   }
   if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
   }
-  if constexpr (Q8) {
-    __shared__ float red[kWaves];
+  if constexpr (Q8) {   // this wave's amax -> its own partial slot (hq_fp8_amax_fold reduces them)
     amax = hq_wave_max(amax);
-    if (lane == 0) red[wave] = amax;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-      unsigned* slot = reinterpret_cast<unsigned*>(q8) + phase;
-      if (__float_as_uint(m) > __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMax(slot, __float_as_uint(m));
-      if (blockIdx.x == 0) {
-        reinterpret_cast<unsigned*>(q8)[(phase + 1) % 3] = 0u;   // cleared for the step after next
-        q8[3] = s8;                                              // dequant scale of this step's y8
-      }
-    }
+    if (lane == 0) part8[blockIdx.x * kWaves + wave] = amax;
   }
 }
 
@@ -703,12 +692,16 @@ void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, con
     return e ? std::max(1, atoi(e)) : 4;
   }();
   dispatch_nch(H, [&](auto nch) {
-    if (y8)
-      hipLaunchKernelGGL((ln_fwd_kernel<decltype(nch)::value, true>), dim3((T + q8_rows * kWaves - 1) / (q8_rows * kWaves)), dim3(256), 0, s, a,
-                         resid, gamma, beta, y, z, mean, rstd, T, H, eps, key, thr, ks, y8, q8, phase);
-    else
+    if (y8) {
+      const int g8 = (T + q8_rows * kWaves - 1) / (q8_rows * kWaves);
+      float* part8 = hq_fp8_amax_parts((size_t)g8 * kWaves);
+      hipLaunchKernelGGL((ln_fwd_kernel<decltype(nch)::value, true>), dim3(g8), dim3(256), 0, s, a, resid, gamma, beta,
+                         y, z, mean, rstd, T, H, eps, key, thr, ks, y8, q8, part8, phase);
+      hq_fp8_amax_fold(part8, g8 * kWaves, q8, phase, s);
+    } else {
       hipLaunchKernelGGL((ln_fwd_kernel<decltype(nch)::value, false>), dim3(blocks), dim3(256), 0, s, a, resid, gamma,
-                         beta, y, z, mean, rstd, T, H, eps, key, thr, ks, nullptr, nullptr, 0);
+                         beta, y, z, mean, rstd, T, H, eps, key, thr, ks, nullptr, nullptr, nullptr, 0);
+    }
   });
 }
 

@@ -177,12 +177,12 @@ class _LayerFn(torch.autograd.Function):
         def proj(inp, name):  # bf16 forward projection
             return ops.linear_fwd(inp, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), kinds[name])
 
-        # --precision fp8 (BASELINE config #5): QKV, FFN1 and FFN2 run on the own block-scaled fp8 MFMA
-        # kernel (gemm_fp8.hip) with e4m3 inputs written by their PRODUCERS under delayed scaling — QKV's by
-        # the previous layer's second LayerNorm (layer 0: one quantisation pass over the embeddings), FFN1's
-        # by this layer's first LayerNorm, FFN2's by FFN1's epilogue — so no standalone quantiser runs per
-        # layer.  The out-projection stays bf16 (its input, the attention context, would need its own pass:
-        # about what the fp8 GEMM saves).  Backward GEMMs are bf16 throughout.
+        # --precision fp8 (BASELINE config #5): every forward projection — QKV, out-projection, FFN1, FFN2
+        # — runs on the own block-scaled fp8 MFMA kernel (gemm_fp8.hip) with e4m3 inputs written by their
+        # PRODUCERS under delayed scaling: QKV's by the previous layer's second LayerNorm (layer 0: one
+        # quantisation pass over the embeddings), the out-projection's by the attention forward's ctx store,
+        # FFN1's by this layer's first LayerNorm, FFN2's by FFN1's epilogue — so no standalone quantiser
+        # runs per layer.  Backward GEMMs are bf16 throughout.
         fp8 = fp8 and ops.fp8_gemm_ok(x.shape[0], 3 * cfg.hidden_size, cfg.hidden_size)
         s8 = m.fp8_states(idx) if fp8 else None
         if fp8:
@@ -192,8 +192,13 @@ class _LayerFn(torch.autograd.Function):
             qkv = ops.linear_fwd_fp8_own(x8, s8["qkv"], W8("qkv"), Bm("qkv.bias"))
         else:
             qkv = proj(x, "qkv")
-        ctxv, lse, bits = ops.attn_fwd(qkv, key_bias, B, L, nh, pa, info.seed, op0, scale)
-        a1 = proj(ctxv, "attention.output.dense")
+        if fp8:
+            ctxv, lse, bits, ctx8 = ops.attn_fwd_q8(qkv, key_bias, B, L, nh, pa, info.seed, op0, scale, s8["out"])
+            a1 = ops.linear_fwd_fp8_own(ctx8, s8["out"], W8("attention.output.dense"),
+                                        Bm("attention.output.dense.bias"))
+        else:
+            ctxv, lse, bits = ops.attn_fwd(qkv, key_bias, B, L, nh, pa, info.seed, op0, scale)
+            a1 = proj(ctxv, "attention.output.dense")
         ln1 = (st.view(p + "attention.output.LayerNorm.weight", "master"),
                st.view(p + "attention.output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph, info.seed, op0 + 1)
         h1_8 = None
@@ -412,7 +417,7 @@ class BertForQuestionAnswering(nn.Module):
             self._fp8_states = {}
         st = self._fp8_states.get(idx)
         if st is None or st["qkv"].buf.device != self.store.device:
-            st = {k: ops.Fp8DelayedState(self.store.device) for k in ("qkv", "ffn1", "ffn2")}
+            st = {k: ops.Fp8DelayedState(self.store.device) for k in ("qkv", "out", "ffn1", "ffn2")}
             self._fp8_states[idx] = st
         return st
 

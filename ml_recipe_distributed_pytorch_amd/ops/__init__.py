@@ -97,6 +97,14 @@ def deterministic() -> bool:
     return torch.are_deterministic_algorithms_enabled() or os.environ.get("HQ_DETERMINISTIC", "0") == "1"
 
 
+def attn_fwd_q8(qkv, key_bias, B, L, nh, p, seed, opid, scale, state: "Fp8DelayedState"):
+    """``attn_fwd`` that also writes ctx in e4m3 under ``state`` — the delayed-scaling state of the
+    out-projection that consumes it (producer-side quantisation): (ctx, lse, keep-bits, ctx8)."""
+    ctx, lse, bits, ctx8 = _k().attn_fwd(qkv, key_bias, int(B), int(L), int(nh), float(p), int(seed), int(opid),
+                                         float(scale), q8=state.buf, phase=state.next_phase())
+    return ctx, lse, bits, ctx8
+
+
 def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale):
     if dctx.is_cuda:
         return _k().attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, int(B), int(L), int(nh), float(p), float(scale),

@@ -122,8 +122,8 @@ def test_ln_fwd_fp8_output(cuda, T, H):
 
 @pytest.mark.gpu
 def test_fp8_model_step_runs_on_own_kernels(cuda):
-    """--precision fp8 at a tile-aligned shape: every forward projection except the out-projection on
-    gemm_fp8 with producer-quantised inputs; a training step stays finite and close to bf16."""
+    """--precision fp8 at a tile-aligned shape: every forward projection (QKV, out-projection, FFN1, FFN2)
+    on gemm_fp8 with producer-quantised inputs; a training step stays finite and close to bf16."""
     from ml_recipe_distributed_pytorch_amd.models.bert import BertForQuestionAnswering
     from ml_recipe_distributed_pytorch_amd.models.config import get_config
     cfg = get_config("bert-base-uncased", num_hidden_layers=2, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
@@ -173,3 +173,32 @@ def test_fp8_quant_delayed_multi_matches_per_tensor(cuda):
             exp = k.fp8_quant_delayed(x[off:off + n], ref_states[i], phase)
             assert torch.equal(y[rows[i][1]:rows[i][1] + n], exp.view(torch.uint8)), (phase, i)
             assert torch.equal(states[i], ref_states[i]), (phase, i)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attn_fwd_fp8_ctx_output(cuda, p):
+    """Attention forward with the e4m3 copy of ctx for the fp8 out-projection: ctx / lse / keep-bits equal
+    the plain call bitwise, ctx8 = e4m3(bf16(ctx) / s) under the delayed scale, amax lands in the state."""
+    k = _native.kernels()
+    B, L, nh = 4, 384, 12
+    g = torch.Generator(device=cuda).manual_seed(11)
+    qkv = torch.randn(B * L, 3 * nh * 64, device=cuda, generator=g).bfloat16()
+    kb = torch.zeros(B, L, device=cuda)
+    kb[2, 300:] = -10000.0
+    ref = k.attn_fwd(qkv, kb, B, L, nh, p, 5, 9, 0.125)
+    state = torch.zeros(4, device=cuda)
+    out = k.attn_fwd(qkv, kb, B, L, nh, p, 5, 9, 0.125, q8=state, phase=0)
+    for x, y in zip(out[:3], ref):
+        assert torch.equal(x, y)
+    ctx, ctx8 = out[0].float(), out[3]
+    assert ctx8.dtype == torch.float8_e4m3fn and state[3].item() == 1.0
+    assert torch.equal(ctx8.view(torch.uint8), ctx.clamp(-448, 448).to(torch.float8_e4m3fn).view(torch.uint8))
+    amax = state[:3].view(torch.int32)[0].view(torch.float32).item()
+    assert amax == ctx.abs().max().item()
+    out2 = k.attn_fwd(qkv, kb, B, L, nh, p, 5, 9, 0.125, q8=state, phase=1)
+    s = state[3].item()
+    assert s == pytest.approx(2 * amax / 448, rel=1e-6)
+    exp = (ctx / s).clamp(-448, 448).to(torch.float8_e4m3fn)
+    diff = (out2[3].view(torch.uint8).int() - exp.view(torch.uint8).int()).abs()
+    assert diff.max().item() <= 1 and (diff > 0).float().mean().item() < 1e-4   # x·(1/s) vs x/s rounding
