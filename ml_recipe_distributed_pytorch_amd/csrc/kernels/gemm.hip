@@ -27,6 +27,8 @@
 //   a float4 of bias per lane, and the column (bias-grad) sums reduce over lanes.
 // * XCD-aware bijective block remap: each XCD walks a contiguous range of tiles in M-major order,
 //   so the tiles that share an A row-panel share that XCD's L2.
+#include <vector>
+
 #include "hq_common.h"
 #include "hq_kernels.h"
 
@@ -275,12 +277,16 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
 // workgroups share a CU.  The M tail costs nothing extra: the A descriptor's num_records ends at row M,
 // the out-of-range rows stage as zeros, and the epilogue stores only rows < M.  Same epilogues as v1;
 // DGELU / DMUL column partials are per 128-row block (part has ceil(M/128) rows).
+// Split-K (ksplit > 1, EPI none / bias / resid only): for grids far below one workgroup per CU with a long
+// K (the reference micro-batch of 2 × 512 tokens: 48 tiles of N = 768 at K = 3072 / 2304), workgroup
+// id / tiles sums K-tiles [split·nt/ksplit, (split+1)·nt/ksplit) into fp32 slab ws[split] and
+// splitk_epi_kernel folds the slabs in order (deterministic) and applies the epilogue.
 template <int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_nts_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                           uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                           uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
                                                           float* __restrict__ part, int M, int N, int K, int lda, int ldb,
-                                                          int ldc) {
+                                                          int ldc, int ksplit, float* __restrict__ ws) {
   constexpr int SB = 128;                  // tile rows = tile cols
   constexpr int PANEL = SB * 128;          // one operand panel: 128 rows × 64 bf16
   constexpr int STAGE = 2 * PANEL;
@@ -292,13 +298,16 @@ __global__ __launch_bounds__(256, 2) void gemm_nts_kernel(const uint16_t* __rest
 
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tiles = nwg / ksplit;
+  const int split = id / tiles, tile = id - split * tiles;
   const int tiles_n = N / SB;
   const int tm = tile / tiles_n, tn = tile % tiles_n;
   const int m0 = tm * SB, n0 = tn * SB;
   const int rows_a = min(SB, M - m0);
-  const int nt = K / BK;
-  HQ_DASSERT(rows_a > 0 && n0 + SB <= N && K % BK == 0);
+  const int nk = K / BK, kt0 = split * nk / ksplit, nt = (split + 1) * nk / ksplit - kt0;
+  HQ_DASSERT(rows_a > 0 && n0 + SB <= N && K % BK == 0 && nt > 0 && (ksplit == 1 || EPI == HQ_EPI_NONE ||
+             EPI == HQ_EPI_BIAS || EPI == HQ_EPI_RESID));
 
   const __amdgpu_buffer_rsrc_t ra =
       __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), (short)0, rows_a * lda * 2, 0x00020000);
@@ -314,12 +323,13 @@ __global__ __launch_bounds__(256, 2) void gemm_nts_kernel(const uint16_t* __rest
   }
   auto stage = [&](int t, int buf) {
     char* base = smem + buf * STAGE + wave_u * 32 * 128;
+    const int ko = (kt0 + t) * BK * 2;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(base + i * 8 * 128), 16, voA[i], t * BK * 2, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_void*)(base + i * 8 * 128), 16, voA[i], ko, 0, 0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(base + PANEL + i * 8 * 128), 16, voB[i], t * BK * 2, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(base + PANEL + i * 8 * 128), 16, voB[i], ko, 0, 0);
   };
   auto bar = []() {
     asm volatile("" ::: "memory");
@@ -360,6 +370,22 @@ __global__ __launch_bounds__(256, 2) void gemm_nts_kernel(const uint16_t* __rest
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();                                               // WAR: stage t+2 reuses this buffer
+  }
+
+  if (ksplit > 1) {   // fp32 slab of this split: lane holds C[m][n … n+3] (swapped-operand accumulator)
+    float* slab = ws + (size_t)split * M * N;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4_t& a = acc[i][j];
+        *reinterpret_cast<float4*>(slab + (size_t)m * N + n0 + wn * 64 + j * 16 + fq * 4) =
+            make_float4(a[0], a[1], a[2], a[3]);
+      }
+    }
+    return;
   }
 
   // ---- epilogue: acc (+bias) -> bf16 in this wave's LDS region [64][64], then row-coalesced 16-B pieces
@@ -437,6 +463,38 @@ __global__ __launch_bounds__(256, 2) void gemm_nts_kernel(const uint16_t* __rest
     }
     __syncthreads();
     if (tid < SB) part[(size_t)tm * N + n0 + tid] = red[tid] + red[SB + tid];
+  }
+}
+
+// C[m, n] = epi(Σ_s ws[s][m][n]) for the split-K vS path: slabs summed in split order (deterministic).
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_epi_kernel(const float* __restrict__ ws, int ksplit, uint16_t* __restrict__ C,
+                                                         const float* __restrict__ bias, const uint16_t* __restrict__ R,
+                                                         int M, int N, int ldc) {
+  const size_t n8 = (size_t)M * N / 8;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+    const size_t e = i * 8;
+    const int m = (int)(e / N), n = (int)(e - (size_t)m * N);
+    float v[8];
+    const float4* w0 = reinterpret_cast<const float4*>(ws + e);
+    float4 a = w0[0], b = w0[1];
+    for (int s = 1; s < ksplit; ++s) {
+      const float4* ws_s = reinterpret_cast<const float4*>(ws + (size_t)s * M * N + e);
+      const float4 c = ws_s[0], d = ws_s[1];
+      a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
+      b.x += d.x; b.y += d.y; b.z += d.z; b.w += d.w;
+    }
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    if constexpr (EPI == HQ_EPI_BIAS) {
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + n), b1 = *reinterpret_cast<const float4*>(bias + n + 4);
+      v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+    } else if constexpr (EPI == HQ_EPI_RESID) {
+      float rr[8];
+      hq_unpack8(*reinterpret_cast<const uint4*>(R + (size_t)m * ldc + n), rr);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] += rr[k];
+    }
+    *reinterpret_cast<uint4*>(C + (size_t)m * ldc + n) = hq_pack8(v);
   }
 }
 
@@ -1074,6 +1132,44 @@ int g_gemm_stagger = [] {
   return (e ? atoi(e) & 0xFF : 0) | ((f ? atoi(f) & 0xFF : 0) << 8);
 }();
 
+int nts_num_cus() {
+  static int ncu = [] {
+    int dev = 0, n = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  return ncu;
+}
+
+// vS split-K factor: only epilogues without column partials / GELU, grids below half a workgroup per CU,
+// and at least 8 K-tiles per split; HQ_GEMM_SPLITK=0 disables (A/B), N > 1 forces up to N.
+int g_nts_splitk = [] {
+  const char* e = getenv("HQ_GEMM_SPLITK");
+  return e ? atoi(e) : -1;
+}();
+template <int EPI>
+int nts_ksplit(int tiles, int nk) {
+  if (!(EPI == HQ_EPI_NONE || EPI == HQ_EPI_BIAS || EPI == HQ_EPI_RESID) || g_nts_splitk == 0) return 1;
+  int ks = g_nts_splitk > 1 ? g_nts_splitk : (2 * tiles <= nts_num_cus() ? 2 * nts_num_cus() / tiles : 1);
+  ks = std::min(ks, std::min(4, nk / 8));
+  return ks > 1 ? ks : 1;
+}
+
+float* hq_splitk_ws(size_t n) {   // per-device fp32 scratch for split-K slabs (same stream as its consumer)
+  static std::vector<std::pair<float*, size_t>> bufs;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if ((int)bufs.size() <= dev) bufs.resize(dev + 1, {nullptr, 0});
+  auto& b = bufs[dev];
+  if (b.second < n) {
+    float* p = nullptr;
+    if (hipMalloc(&p, n * sizeof(float)) != hipSuccess) { fprintf(stderr, "hq_splitk_ws: hipMalloc failed\n"); abort(); }
+    b = {p, n};   // the old block is kept (kernels may still read it): grows happen a few times per process
+  }
+  return b.first;
+}
+
 constexpr size_t epi_lds(int bn) {
   const size_t stage = 2 * (size_t)(BM * 128 + bn * 128);
   const size_t epi = 8 * 128 * (size_t)(bn / 4 * 2 + 16);
@@ -1091,8 +1187,17 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
     }();
     (void)init;
     const int grid_s = ((M + 127) / 128) * (N / 128);
-    hipLaunchKernelGGL((gemm_nts_kernel<EPI>), dim3(grid_s), dim3(256), lds, s, A, B, C, bias, P, R, part, M, N, K, lda,
-                       ldb, ldc);
+    const int ks = nts_ksplit<EPI>(grid_s, K / BK);
+    float* ws = ks > 1 ? hq_splitk_ws((size_t)ks * M * N) : nullptr;
+    hipLaunchKernelGGL((gemm_nts_kernel<EPI>), dim3(grid_s * ks), dim3(256), lds, s, A, B, C, bias, P, R, part, M, N, K,
+                       lda, ldb, ldc, ks, ws);
+    if (ks > 1) {
+      const size_t n8 = (size_t)M * N / 8;
+      const int g = (int)std::min<size_t>((n8 + 255) / 256, 2048);
+      hipLaunchKernelGGL((splitk_epi_kernel<EPI == HQ_EPI_BIAS ? HQ_EPI_BIAS : EPI == HQ_EPI_RESID ? HQ_EPI_RESID
+                                                                                                   : HQ_EPI_NONE>),
+                         dim3(g), dim3(256), 0, s, ws, ks, C, bias, R, M, N, ldc);
+    }
     return;
   }
   const int grid = (M / BM) * (N / bn);

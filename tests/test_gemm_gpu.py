@@ -231,3 +231,30 @@ def test_gemm_nt_gelu_derivative_epilogues(cuda, M, N, K):
     exp = _ref(A, B).bfloat16().float() * gd.float()
     _close(d, exp)
     torch.testing.assert_close(part.sum(0), exp.sum(0), atol=5e-2 * (1 + exp.abs().sum(0).max().item() / M), rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 3072), (1000, 768, 2304), (2048, 768, 1024)])
+def test_gemm_nt_split_k_low_fill(cuda, M, N, K, variant):
+    """Split-K on the 128²-tile kernel for low-fill grids with a long K (the reference micro-batch's
+    FFN2 forward / FFN1 and QKV dgrads: 48 tiles at K = 3072 / 2304): none / bias / resid epilogues
+    against the fp32 oracle, rows past M untouched, bitwise repeatable (slabs folded in split order)."""
+    if variant not in (0, 4):
+        pytest.skip("split-K lives in the 128²-tile kernel")
+    k = _native.kernels()
+    assert k.gemm_nt_supported(M, N, K) == 1
+    g = torch.Generator(device=cuda).manual_seed(M + K)
+    A = (torch.randn(M, K, device=cuda, generator=g) * 0.5).bfloat16()
+    B = (torch.randn(N, K, device=cuda, generator=g) * 0.1).bfloat16()
+    bias = torch.randn(N, device=cuda, generator=g) * 0.1
+    ref = _ref(A, B)
+    big = torch.full((M + 64, N), 7.0, device=cuda, dtype=torch.bfloat16)
+    k.gemm_nt(A, B, EPI_BIAS, bias=bias, out=big[:M])
+    _close(big[:M], ref + bias)
+    assert torch.equal(big[M:].float(), torch.full((64, N), 7.0, device=cuda)), "rows past M were written"
+    c0 = k.gemm_nt(A, B, EPI_NONE)
+    _close(c0, ref)
+    for _ in range(3):
+        assert torch.equal(k.gemm_nt(A, B, EPI_NONE), c0)
+    resid = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+    _close(k.gemm_nt(A, B, EPI_RESID, resid=resid), ref + resid.float())
