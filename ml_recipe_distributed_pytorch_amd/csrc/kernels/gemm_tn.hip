@@ -21,6 +21,7 @@
 // fragment (12.5 % more MFMAs in a third of the waves of a third of the blocks) and write fp32 partials
 // [S][N] that the same reduce kernel folds in — replacing a separate 450 MB column-sum pass.
 #include <algorithm>
+#include <cstdlib>
 
 #include "hq_common.h"
 #include "hq_kernels.h"
@@ -273,7 +274,13 @@ int hq_gemm_tn_splits(int T, int N, int K) {
   int S = 256 / tiles;                     // one full round of the 256 CUs
   if (S < 1) S = 1;
   const int nkt = (T + BT - 1) / BT;
-  while (S > 1 && nkt / S < 8) --S;        // keep >= 8 K-tiles per block (prologue amortised)
+  // K-tiles per block kept (prologue amortised): 4 (micro-batch 2 x 512: 388 -> 400 samples/s vs 8, batch
+  // 64 neutral; batch 256 never splits that far); HQ_TN_MIN_KT: A/B
+  static const int min_kt = [] {
+    const char* e = getenv("HQ_TN_MIN_KT");
+    return e ? std::max(1, atoi(e)) : 4;
+  }();
+  while (S > 1 && nkt / S < min_kt) --S;
   if (nkt < 2) return 0;
   return S;
 }
