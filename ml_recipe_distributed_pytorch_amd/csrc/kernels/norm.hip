@@ -140,7 +140,9 @@ __device__ __forceinline__ void ln_bwd_load(const uint16_t* __restrict__ dy, con
   }
 }
 
-template <int NCH>
+// RPW rows per wave: 8 at large T (partials amortised), 2 for small token counts (T = 1024: 32 blocks of
+// 8-row waves left most CUs idle and each wave latency-bound — see ln_rows_per_wave)
+template <int NCH, int RPW = kRowsPerWave>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dy2,
                                                      const uint16_t* __restrict__ z, const float* __restrict__ gamma,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
     float4 g = col < H ? *reinterpret_cast<const float4*>(gamma + col) : make_float4(0.f, 0.f, 0.f, 0.f);
     gam[c][0] = g.x; gam[c][1] = g.y; gam[c][2] = g.z; gam[c][3] = g.w;
   }
-  const int row0 = blockIdx.x * kWaves * kRowsPerWave + wave;
+  const int row0 = blockIdx.x * kWaves * RPW + wave;
   // loads run TWO rows ahead (c = this row, n = next, f = the one after): with one row in flight per
   // wave the kernel left ~15 % of the HBM bandwidth unused at its 4 waves/SIMD occupancy
   uint2 cdy[NCH], cdy2[NCH], cz[NCH], ndy[NCH], ndy2[NCH], nz[NCH];
@@ -174,20 +176,20 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
     cmu = mean[row0];
     crs = rstd[row0];
   }
-  if (kRowsPerWave > 1 && row0 + kWaves < T) {
+  if (RPW > 1 && row0 + kWaves < T) {
     ln_bwd_load<NCH>(dy, dy2, z, (size_t)(row0 + kWaves) * H, lane, H, ndy, ndy2, nz);
     nmu = mean[row0 + kWaves];
     nrs = rstd[row0 + kWaves];
   }
 #pragma unroll
-  for (int r = 0; r < kRowsPerWave; ++r) {
+  for (int r = 0; r < RPW; ++r) {
     const int row = row0 + r * kWaves;
     if (row < T) {
       const size_t base = (size_t)row * H;
       uint2 fdy[NCH], fdy2[NCH], fz[NCH];
       float fmu = 0.f, frs = 0.f;
       const int frow = row + 2 * kWaves;
-      if (r + 2 < kRowsPerWave && frow < T) {
+      if (r + 2 < RPW && frow < T) {
         ln_bwd_load<NCH>(dy, dy2, z, (size_t)frow * H, lane, H, fdy, fdy2, fz);
         fmu = mean[frow];
         frs = rstd[frow];
@@ -278,7 +280,7 @@ __global__ __launch_bounds__(256) void span_fwd_kernel(const uint16_t* __restric
 template <int NCH>
 __global__ __launch_bounds__(256) void span_bwd_kernel(const uint16_t* __restrict__ seq, const float* __restrict__ w,
                                                        const float* __restrict__ g, uint16_t* __restrict__ dseq,
-                                                       float* __restrict__ part, int T, int H) {
+                                                       float* __restrict__ part, int T, int H, int rpw) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float acc[2][NCH][4];
@@ -293,8 +295,8 @@ __global__ __launch_bounds__(256) void span_bwd_kernel(const uint16_t* __restric
 #pragma unroll
     for (int i = 0; i < 4; ++i) { acc[0][c][i] = 0.f; acc[1][c][i] = 0.f; }
   }
-  const int row0 = blockIdx.x * kWaves * kRowsPerWave;
-  for (int r = 0; r < kRowsPerWave; ++r) {
+  const int row0 = blockIdx.x * kWaves * rpw;
+  for (int r = 0; r < rpw; ++r) {
     const int row = row0 + r * kWaves + wave;
     if (row >= T) break;
     const float2 gg = *reinterpret_cast<const float2*>(g + 2 * (size_t)row);
@@ -705,7 +707,11 @@ void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, con
   });
 }
 
-int hq_ln_bwd_partials(int T) { return (T + kWaves * kRowsPerWave - 1) / (kWaves * kRowsPerWave); }
+static int ln_rows_per_wave(int T) { return T >= 16384 ? kRowsPerWave : 2; }
+int hq_ln_bwd_partials(int T) {
+  const int rpw = ln_rows_per_wave(T);
+  return (T + kWaves * rpw - 1) / (kWaves * rpw);
+}
 int hq_embed_bwd_partials(int T, int L) {
   if (L <= 0 || T % L) L = T;
   return ((L + kWaves - 1) / kWaves) * ((T / L + kEmbNB - 1) / kEmbNB);
@@ -719,8 +725,12 @@ void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const
   const float ks = hq_keep_scale(thr);
   const int nb = hq_ln_bwd_partials(T);
   dispatch_nch(H, [&](auto nch) {
-    hipLaunchKernelGGL(ln_bwd_kernel<decltype(nch)::value>, dim3(nb), dim3(256), 4 * H * sizeof(float), s, dy, dy2, z,
-                       gamma, mean, rstd, dz, da, part, T, H, key, thr, ks);
+    if (ln_rows_per_wave(T) == kRowsPerWave)
+      hipLaunchKernelGGL((ln_bwd_kernel<decltype(nch)::value, kRowsPerWave>), dim3(nb), dim3(256), 4 * H * sizeof(float), s,
+                         dy, dy2, z, gamma, mean, rstd, dz, da, part, T, H, key, thr, ks);
+    else
+      hipLaunchKernelGGL((ln_bwd_kernel<decltype(nch)::value, 2>), dim3(nb), dim3(256), 4 * H * sizeof(float), s, dy, dy2,
+                         z, gamma, mean, rstd, dz, da, part, T, H, key, thr, ks);
   });
   colsum(part, nb, 3 * H, outs, H, accumulate, s);
 }
@@ -799,7 +809,7 @@ void hq_span_bwd(const uint16_t* seq, const float* w, const float* g, uint16_t* 
   const int nb = hq_ln_bwd_partials(T);
   dispatch_nch(H, [&](auto nch) {
     hipLaunchKernelGGL(span_bwd_kernel<decltype(nch)::value>, dim3(nb), dim3(256), 4 * H * sizeof(float), s, seq, w, g,
-                       dseq, part, T, H);
+                       dseq, part, T, H, ln_rows_per_wave(T));
   });
   colsum(part, nb, 2 * H, HqOuts{{dw, dw + H, nullptr, nullptr}}, H, accumulate, s);
 }
