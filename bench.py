@@ -54,6 +54,9 @@ def parse():
 
 def main():
     args = parse()
+    if os.environ.get("HQ_HANG_DUMP_S"):   # hang diagnosis: every rank dumps its Python stacks and exits
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["HQ_HANG_DUMP_S"]), exit=True)
     import torch
     import torch.distributed as dist
 

@@ -113,3 +113,25 @@ def test_set_seed_selects_deterministic_kernels(monkeypatch):
     a = random.random()
     set_seed(7)
     assert random.random() == a
+
+
+def test_hw_queue_reservation_skipped_when_ranks_share_a_gpu(monkeypatch):
+    """8 HIP hardware queues per process only when each rank has its own GPU: ranks sharing one (the
+    gloo rehearsal, more local ranks than visible GPUs) keep HIP's default."""
+    import ml_recipe_distributed_pytorch_amd as pkg
+    monkeypatch.delenv("HQ_BENCH_BACKEND", raising=False)
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,1")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    assert not pkg._ranks_share_a_gpu()
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    assert pkg._ranks_share_a_gpu()
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    monkeypatch.setenv("HQ_BENCH_BACKEND", "gloo")
+    assert pkg._ranks_share_a_gpu()
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    pkg._reserve_hw_queues()
+    import os
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "4"
+    monkeypatch.setenv("HQ_BENCH_BACKEND", "nccl")
+    pkg._reserve_hw_queues()
+    assert os.environ["GPU_MAX_HW_QUEUES"] == "8"
