@@ -828,7 +828,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
                                                                uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                                uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
                                                                float* __restrict__ part, int M, int N, int K, int lda,
-                                                               int ldb, int ldc, int stagger) {
+                                                               int ldb, int ldc, int stagger, unsigned* __restrict__ sched) {
   constexpr int BN = 256;
   constexpr int PANEL = 256 * 128;
   constexpr int STAGE = 2 * PANEL;
@@ -837,7 +837,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   constexpr int REGION = 64 * RS;            // one wave's 64-row staging round (9216 B)
   constexpr int SPARE = 2 * STAGE;           // past both stage buffers: wave 7's region, then csum scratch
   constexpr int E = NT3Epi<EPI>::E;
-  static_assert(7 * REGION <= STAGE && SPARE + REGION + 2 * BN * 4 <= 160 * 1024, "LDS plan");
+  constexpr int TICKET = SPARE + REGION + 2 * BN * 4;   // LDS word: the tile after `next` (dynamic schedule)
+  static_assert(7 * REGION <= STAGE && TICKET + 16 <= 160 * 1024, "LDS plan");
   const int epi_flags = stagger >> 8;   // HQ_GEMM_EPIFLAGS (A/B knobs; 0 in production)
   stagger &= 0xFF;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
@@ -919,8 +920,24 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     asm volatile("" ::: "memory");
   };
 
+  // Tile schedule.  Static: tile id, id + nwg, id + 2·nwg, …  — the blocks of one XCD (x = bid & 7, the
+  // cnt_x workgroups with ids base_x … base_x + cnt_x - 1) walk, round after round, the same contiguous
+  // run of cnt_x tiles, so their A row panels stay in that XCD's L2.  Dynamic (sched != null) keeps that
+  // per-XCD sequence, tile(s) = (s / cnt_x)·nwg + base_x + s % cnt_x, but hands out its entries s ≥ 2·cnt_x
+  // by tickets from the XCD's own counter (sched[32·x]); the first two (s = j, cnt_x + j) stay static, as the
+  // pipeline stages the next tile's K-tile 0 during this tile's last K-tiles, so `next` must be known when
+  // this tile starts.  A workgroup dispatched late — its CU held by another stream's kernel, e.g. the RCCL
+  // all-reduce overlapped with the backward — then delays only its first two tiles instead of its whole
+  // 1/nwg share (tools/gemm_contention_bench.py).  The ticket is drawn by thread 0 at the top of the tile
+  // (a per-lane address keeps hipcc's atomic optimizer — whose readfirstlane would wait for the return on
+  // the spot — out of it) and published through LDS after the K-loop, where hipcc drains vmcnt anyway.
+  // Every workgroup bumps sched[256] on exit; the last one zeroes the counters for the next launch on this
+  // stream (stream order: the next launch starts after this one has drained, graph replays included).
   int tile = id;
-  if (tile >= ntiles) return;   // whole workgroup
+  if (tile >= ntiles) return;   // whole workgroup (never: grid <= tiles)
+  int next = tile + nwg;
+  const int cnt_x = q + (xcd < r ? 1 : 0), base_x = id - (bid >> 3);
+  unsigned* tix = sched ? sched + 32 * xcd : nullptr;
   // Phase offset for half of each XCD's workgroups (stagger × 8128 cycles): the tile seams of all CUs
   // otherwise coincide, and every epilogue's stores / aux loads hit HBM in one chip-wide burst that the
   // next K-tile's counted wait (vmcnt counts stores too) then stalls on.
@@ -936,8 +953,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   bool first = true;
 
   for (;;) {
-    const int next = tile + nwg;
     const bool last = next >= ntiles;
+    unsigned ticket = 0;
+    if (sched && !last && tid == 0) {
+      unsigned zero;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(zero));   // opaque per-lane offset (see above)
+      ticket = __hip_atomic_fetch_add(tix + zero, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     const __amdgpu_buffer_rsrc_t na = rsrc_a(last ? tile : next), nb = rsrc_b(last ? tile : next);
     const int tm = tile / tiles_n, tn = tile % tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
@@ -1006,6 +1028,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       for (int t = 0; t < nt; ++t) ktile(t);
     }
     // every wave has passed its last MFMA phase: the buffer of the last K-tile is free
+    if (sched && !last && tid == 0)
+      *reinterpret_cast<unsigned*>(smem + TICKET) = 2u * (unsigned)cnt_x + ticket;   // sequence index s
     const int bl = (p0 + nt - 1) & 1;
     char* wreg = wave < 7 ? smem + bl * STAGE + wave * REGION : smem + SPARE;
 
@@ -1111,12 +1135,34 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
     stA(na, 0, 1, bl); stB(nb, 0, 1, bl);
+    int after = next + nwg;
+    if (sched) {
+      const unsigned sx = *reinterpret_cast<const unsigned*>(smem + TICKET);
+      const long t = (long)(sx / (unsigned)cnt_x) * nwg + base_x + (long)(sx % (unsigned)cnt_x);
+      after = t < ntiles ? (int)t : ntiles;
+    }
     tile = next;
+    next = __builtin_amdgcn_readfirstlane(after);
     ca = na;
     cb = nb;
     p0 = (p0 + nt) & 1;
     first = false;
   }
+  if (sched && tid == 0) {
+    if (__hip_atomic_fetch_add(sched + 256, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)nwg - 1) {
+      for (int x = 0; x < 8; ++x) __hip_atomic_store(sched + 32 * x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(sched + 256, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Spin kernel for the contention diagnostic (hq_cu_hog): 96 KiB of LDS keeps it alone on its CU, as a
+// GEMM workgroup would need that CU's whole LDS; s_memrealtime is the 100 MHz constant clock.
+__global__ __launch_bounds__(256) void cu_hog_kernel(long ticks) {
+  extern __shared__ char hog_lds[];
+  const long t0 = (long)__builtin_amdgcn_s_memrealtime();
+  while ((long)__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  if (threadIdx.x == 1023) hog_lds[0] = 0;   // never true: keeps the LDS allocation
 }
 
 // 0 = auto (v3 for K <= 2304, else v2), 1 = force v1, 2 = force v2, 3 = force v3; HQ_GEMM_VARIANT sets it
@@ -1131,6 +1177,40 @@ int g_gemm_stagger = [] {
   const char* f = getenv("HQ_GEMM_EPIFLAGS");
   return (e ? atoi(e) & 0xFF : 0) | ((f ? atoi(f) & 0xFF : 0) << 8);
 }();
+
+int g_gemm_sched = [] {
+  const char* e = getenv("HQ_GEMM_SCHED");
+  return e ? atoi(e) : 1;
+}();
+
+// Per (device, stream) slot of the v3 ticket schedule: 8 per-XCD ticket counters and the exit counter,
+// each on its own 128-B line (words 32·x, 256), carved from one 64-slot block per device that is
+// allocated and zeroed on the first use (an eager call: no allocation inside a graph capture once the
+// step has run once).  Stream order serialises the launches that share a slot.
+constexpr size_t kSchedWords = 9 * 32;
+unsigned* nt3_sched_slot(hipStream_t s) {
+  struct Pool { unsigned* base = nullptr; std::vector<hipStream_t> streams; };
+  static std::vector<Pool> pools;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if ((int)pools.size() <= dev) pools.resize(dev + 1);
+  Pool& p = pools[dev];
+  if (!p.base) {
+    void* q = nullptr;
+    if (hipMalloc(&q, 64 * kSchedWords * sizeof(unsigned)) != hipSuccess ||
+        hipMemset(q, 0, 64 * kSchedWords * sizeof(unsigned)) != hipSuccess) {
+      fprintf(stderr, "nt3_sched_slot: allocation failed, static tile schedule\n");
+      g_gemm_sched = 0;
+      return nullptr;
+    }
+    p.base = static_cast<unsigned*>(q);
+  }
+  for (size_t i = 0; i < p.streams.size(); ++i)
+    if (p.streams[i] == s) return p.base + kSchedWords * i;
+  if (p.streams.size() >= 64) return nullptr;   // more streams than slots: static schedule on the rest
+  p.streams.push_back(s);
+  return p.base + kSchedWords * (p.streams.size() - 1);
+}
 
 int nts_num_cus() {
   static int ncu = [] {
@@ -1206,7 +1286,7 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
   // K = 768 / 2304 on the b256 shapes, -1-3 % at K = 3072: tools/gemm_nt3_check.py, profiles/s3_gemm_v3)
   const bool v3_auto = g_gemm_variant == 0 && K <= 2304;
   if (bn == 256 && (g_gemm_variant == 3 || v3_auto) && K >= 2 * BK && srd_ok) {
-    constexpr size_t lds = 2 * 2 * 256 * 128 + 64 * 144 + 2 * 256 * 4;
+    constexpr size_t lds = 2 * 2 * 256 * 128 + 64 * 144 + 2 * 256 * 4 + 16;
     static int ncu = [] {
       int dev = 0, n = 0;
       (void)hipGetDevice(&dev);
@@ -1214,8 +1294,10 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
       (void)hipFuncSetAttribute((const void*)gemm_nt3_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       return n > 0 ? n : 256;
     }();
-    hipLaunchKernelGGL((gemm_nt3_kernel<EPI>), dim3(std::min(grid, ncu)), dim3(kThreads), lds, s, A, B, C, bias, P, R, part,
-                       M, N, K, lda, ldb, ldc, g_gemm_stagger);
+    const int nwg = std::min(grid, ncu);
+    unsigned* sched = (g_gemm_sched && grid > 2 * nwg) ? nt3_sched_slot(s) : nullptr;
+    hipLaunchKernelGGL((gemm_nt3_kernel<EPI>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, R, part,
+                       M, N, K, lda, ldb, ldc, g_gemm_stagger, sched);
   } else if (bn == 256 && (g_gemm_variant == 0 || g_gemm_variant == 2 || g_gemm_variant == 3) && K >= 2 * BK && srd_ok) {
     // production v2: buffer_load…lds staging (+8-12 % over global_load_lds on the BERT shapes,
     // tools/gemm_lab); grouped 8-row-panel tile order only for wide N (+15 % at 8192², neutral at
@@ -1258,6 +1340,16 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
 
 void hq_gemm_set_variant(int v) { g_gemm_variant = v; }
 void hq_gemm_set_stagger(int v) { g_gemm_stagger = v; }
+void hq_gemm_set_sched(int v) { g_gemm_sched = v; }
+void hq_cu_hog(int blocks, int usec, hipStream_t s) {
+  constexpr int lds = 96 * 1024;
+  static bool init = [] {
+    (void)hipFuncSetAttribute((const void*)cu_hog_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    return true;
+  }();
+  (void)init;
+  hipLaunchKernelGGL(cu_hog_kernel, dim3(blocks), dim3(256), lds, s, (long)usec * 100);
+}
 
 // Kernel family for a shape: 256 / 128 = the 256-row kernels with that block width, 1 = vS (128² tiles),
 // 0 = unsupported.  Variants 1-3 force the 256-row kernels where they apply, 4 forces vS; auto takes the
