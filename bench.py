@@ -176,6 +176,7 @@ def main():
            "graph_replays": engine.graph_replays,
            "reducer": reducer.kind if reducer is not None else "none",
            "reducer_buckets": reducer.n_buckets if reducer is not None else 0,
+           "gemm_sched": reducer.gemm_sched if reducer is not None else "static",
            "comm_wait_ms": round(comm["comm_wait_ms"], 3) if "comm_wait_ms" in comm else None,
            "comm_span_ms": round(comm["comm_span_ms"], 3) if "comm_span_ms" in comm else None,
            "mfu_bf16_dense": round(value * flops_per_sample / (world * 2.5e15), 4),

@@ -87,9 +87,10 @@ int hq_gemm_nt_part_rows(int M, int N, int K);
 // v2 above), 1 = v1, 2 = v2, 3 = v3 (the 256-row kernels wherever M % 256 == 0), 4 = 128² tiles always
 void hq_gemm_set_variant(int v);
 void hq_gemm_set_stagger(int v);   // v3 start offset of half the workgroups (units of s_sleep(127))
-// v3 tile scheduling: 1 = dynamic (a workgroup's third and later tiles come from a per-stream atomic ticket
-// counter, so CUs held by another stream's kernels — RCCL all-reduce under the backward — cost the GEMM
-// only their share), 0 = static round-robin (tile = id + k·grid); HQ_GEMM_SCHED sets it, default 1
+// v3 tile scheduling: 1 = dynamic (a workgroup's third and later tiles come from per-XCD atomic ticket
+// counters, so CUs held by another stream's kernels — RCCL all-reduce under the backward — cost the GEMM
+// only their share), 0 = static round-robin (tile = id + k·grid); HQ_GEMM_SCHED sets it, default 0 (the
+// DP reducer selects 1 when world > 1)
 void hq_gemm_set_sched(int v);
 // Diagnostic: `blocks` workgroups (one per CU: 96 KiB LDS each) that spin for `usec` µs on stream s —
 // stands in for a collective kernel holding CUs while a GEMM runs (tools/gemm_contention_bench.py)

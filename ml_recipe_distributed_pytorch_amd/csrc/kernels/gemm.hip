@@ -928,7 +928,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   // pipeline stages the next tile's K-tile 0 during this tile's last K-tiles, so `next` must be known when
   // this tile starts.  A workgroup dispatched late — its CU held by another stream's kernel, e.g. the RCCL
   // all-reduce overlapped with the backward — then delays only its first two tiles instead of its whole
-  // 1/nwg share (tools/gemm_contention_bench.py).  The ticket is drawn by thread 0 at the top of the tile
+  // 1/nwg share (tools/gemm_contention_bench.py).  The ticket is drawn by thread 0 early in the tile
   // (a per-lane address keeps hipcc's atomic optimizer — whose readfirstlane would wait for the return on
   // the spot — out of it) and published through LDS after the K-loop, where hipcc drains vmcnt anyway.
   // Every workgroup bumps sched[256] on exit; the last one zeroes the counters for the next launch on this
@@ -955,11 +955,17 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   for (;;) {
     const bool last = next >= ntiles;
     unsigned ticket = 0;
-    if (sched && !last && tid == 0) {
-      unsigned zero;
-      asm volatile("v_mov_b32 %0, 0" : "=v"(zero));   // opaque per-lane offset (see above)
-      ticket = __hip_atomic_fetch_add(tix + zero, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    const bool draw = sched && !last;
+    // drawn in phase P1 of K-tile 0, after that phase's stage: the counted vmcnt(6) of K-tile 1's P1 (6 newer
+    // loads by then) retires it about a K-tile later, so its round trip never stalls a wait (issued at the
+    // tile top it was the OLDEST op under K-tile 0's first wait and cost ~1-3 % per GEMM)
+    auto draw_ticket = [&]() {
+      if (tid == 0) {
+        unsigned zero;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(zero));   // opaque per-lane offset (see above)
+        ticket = __hip_atomic_fetch_add(tix + zero, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    };
     const __amdgpu_buffer_rsrc_t na = rsrc_a(last ? tile : next), nb = rsrc_b(last ? tile : next);
     const int tm = tile / tiles_n, tn = tile % tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
@@ -1002,6 +1008,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       }
       readB(b0, 1, bf1);
       if (more1) stA(a1, 1, k1, b1);
+      if (t == 0 && draw) draw_ticket();
       bar();
       mma(0, 1, bf1);
       bar();
@@ -1028,7 +1035,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       for (int t = 0; t < nt; ++t) ktile(t);
     }
     // every wave has passed its last MFMA phase: the buffer of the last K-tile is free
-    if (sched && !last && tid == 0)
+    if (draw && tid == 0)
       *reinterpret_cast<unsigned*>(smem + TICKET) = 2u * (unsigned)cnt_x + ticket;   // sequence index s
     const int bl = (p0 + nt - 1) & 1;
     char* wreg = wave < 7 ? smem + bl * STAGE + wave * REGION : smem + SPARE;
@@ -1178,9 +1185,11 @@ int g_gemm_stagger = [] {
   return (e ? atoi(e) & 0xFF : 0) | ((f ? atoi(f) & 0xFF : 0) << 8);
 }();
 
+// default static: uncontended the dynamic schedule costs ~0.9 % of the step (profiles/r2_sched); GradReducer
+// switches it on when an all-reduce overlaps the backward (world > 1); HQ_GEMM_SCHED overrides either way
 int g_gemm_sched = [] {
   const char* e = getenv("HQ_GEMM_SCHED");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 0;
 }();
 
 // Per (device, stream) slot of the v3 ticket schedule: 8 per-XCD ticket counters and the exit counter,

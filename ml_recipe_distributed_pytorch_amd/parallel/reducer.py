@@ -102,10 +102,24 @@ class GradReducer:
         self._first_ev = None
         self._build_buckets()
         model.set_grad_listener(self._on_group_ready)
+        self.gemm_sched = self._pick_gemm_sched(on_gpu)
         if self.world > 1 and broadcast_params:
             self.broadcast_parameters()
 
     # ------------------------------------------------------------------ setup
+    def _pick_gemm_sched(self, on_gpu: bool) -> str:
+        """Persistent-GEMM tile schedule while gradients are all-reduced under the backward: the collective's
+        blocks hold CUs, and with the static schedule the GEMM workgroups that wait for those CUs run their
+        whole share late (+160-180 µs per GEMM per 200 µs held, tools/gemm_contention_bench.py); the dynamic
+        per-XCD ticket schedule costs ~0.9 % of the uncontended step, so it is switched on only here, when a
+        collective actually overlaps the backward.  HQ_GEMM_SCHED (0/1) overrides."""
+        if not on_gpu:
+            return "n/a"
+        env = os.environ.get("HQ_GEMM_SCHED")
+        dynamic = (env == "1") if env in ("0", "1") else self.world > 1
+        kernels().gemm_set_sched(1 if dynamic else 0)
+        return "dynamic" if dynamic else "static"
+
     def _make_native(self):
         if self.world == 1:  # forced single-rank communicator: no rendezvous needed
             uid = kernels().rccl_unique_id()

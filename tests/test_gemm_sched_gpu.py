@@ -46,7 +46,7 @@ def sched_reset():
     k = _native.kernels()
     k.gemm_set_variant(3)
     yield k
-    k.gemm_set_sched(1)
+    k.gemm_set_sched(0)
     k.gemm_set_variant(0)
 
 

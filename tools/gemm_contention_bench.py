@@ -84,7 +84,7 @@ def main():
                     e1.record(main_s)
                     torch.cuda.synchronize()
                     res.setdefault((sched, h), []).append(e0.elapsed_time(e1) * 1e3)
-        k.gemm_set_sched(1)
+        k.gemm_set_sched(0)
         fl = 2.0 * M * N * K
         for h in hogs:
             s0 = statistics.median(res[(0, h)])
