@@ -27,6 +27,7 @@
 //   a float4 of bias per lane, and the column (bias-grad) sums reduce over lanes.
 // * XCD-aware bijective block remap: each XCD walks a contiguous range of tiles in M-major order,
 //   so the tiles that share an A row-panel share that XCD's L2.
+#include <mutex>
 #include <vector>
 
 #include "hq_common.h"
@@ -934,7 +935,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   // Every workgroup bumps sched[256] on exit; the last one zeroes the counters for the next launch on this
   // stream (stream order: the next launch starts after this one has drained, graph replays included).
   int tile = id;
-  if (tile >= ntiles) return;   // whole workgroup (never: grid <= tiles)
+  HQ_DASSERT(tile < ntiles);     // the host launches min(tiles, CUs) workgroups, so every one has a tile
+  if (tile >= ntiles) return;   // (unreachable; an early exit would skip the exit count that re-zeroes sched)
   int next = tile + nwg;
   const int cnt_x = q + (xcd < r ? 1 : 0), base_x = id - (bid >> 3);
   unsigned* tix = sched ? sched + 32 * xcd : nullptr;
@@ -1200,6 +1202,8 @@ constexpr size_t kSchedWords = 9 * 32;
 unsigned* nt3_sched_slot(hipStream_t s) {
   struct Pool { unsigned* base = nullptr; std::vector<hipStream_t> streams; };
   static std::vector<Pool> pools;
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
   int dev = 0;
   (void)hipGetDevice(&dev);
   if ((int)pools.size() <= dev) pools.resize(dev + 1);
