@@ -1199,30 +1199,38 @@ int g_gemm_sched = [] {
 // allocated and zeroed on the first use (an eager call: no allocation inside a graph capture once the
 // step has run once).  Stream order serialises the launches that share a slot.
 constexpr size_t kSchedWords = 9 * 32;
-unsigned* nt3_sched_slot(hipStream_t s) {
-  struct Pool { unsigned* base = nullptr; std::vector<hipStream_t> streams; };
-  static std::vector<Pool> pools;
-  static std::mutex mu;
-  std::lock_guard<std::mutex> lock(mu);
+struct SchedPool { unsigned* base = nullptr; std::vector<hipStream_t> streams; };
+std::mutex g_sched_mu;
+
+// the current device's pool, allocated and zeroed on first use (caller holds g_sched_mu)
+SchedPool* sched_pool_locked() {
+  static std::vector<SchedPool> pools;
   int dev = 0;
   (void)hipGetDevice(&dev);
   if ((int)pools.size() <= dev) pools.resize(dev + 1);
-  Pool& p = pools[dev];
+  SchedPool& p = pools[dev];
   if (!p.base) {
     void* q = nullptr;
     if (hipMalloc(&q, 64 * kSchedWords * sizeof(unsigned)) != hipSuccess ||
         hipMemset(q, 0, 64 * kSchedWords * sizeof(unsigned)) != hipSuccess) {
-      fprintf(stderr, "nt3_sched_slot: allocation failed, static tile schedule\n");
+      fprintf(stderr, "nt3 tile schedule: slot allocation failed, static schedule\n");
       g_gemm_sched = 0;
       return nullptr;
     }
     p.base = static_cast<unsigned*>(q);
   }
-  for (size_t i = 0; i < p.streams.size(); ++i)
-    if (p.streams[i] == s) return p.base + kSchedWords * i;
-  if (p.streams.size() >= 64) return nullptr;   // more streams than slots: static schedule on the rest
-  p.streams.push_back(s);
-  return p.base + kSchedWords * (p.streams.size() - 1);
+  return &p;
+}
+
+unsigned* nt3_sched_slot(hipStream_t s) {
+  std::lock_guard<std::mutex> lock(g_sched_mu);
+  SchedPool* p = sched_pool_locked();
+  if (!p) return nullptr;
+  for (size_t i = 0; i < p->streams.size(); ++i)
+    if (p->streams[i] == s) return p->base + kSchedWords * i;
+  if (p->streams.size() >= 64) return nullptr;   // more streams than slots: static schedule on the rest
+  p->streams.push_back(s);
+  return p->base + kSchedWords * (p->streams.size() - 1);
 }
 
 int nts_num_cus() {
@@ -1353,7 +1361,13 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
 
 void hq_gemm_set_variant(int v) { g_gemm_variant = v; }
 void hq_gemm_set_stagger(int v) { g_gemm_stagger = v; }
-void hq_gemm_set_sched(int v) { g_gemm_sched = v; }
+void hq_gemm_set_sched(int v) {
+  g_gemm_sched = v;
+  if (v) {   // allocate the slots now, eagerly: a first GEMM inside a graph capture must not hipMalloc
+    std::lock_guard<std::mutex> lock(g_sched_mu);
+    (void)sched_pool_locked();
+  }
+}
 void hq_cu_hog(int blocks, int usec, hipStream_t s) {
   constexpr int lds = 96 * 1024;
   static bool init = [] {
