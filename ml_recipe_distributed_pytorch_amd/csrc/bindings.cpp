@@ -91,23 +91,29 @@ void embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tenso
 
 // ------------------------------------------------------------------ residual + dropout + LayerNorm
 // With q8 (f32[4] delayed-scaling state of the consuming fp8 GEMM's input): also returns y as e4m3.
-std::vector<Tensor> ln_fwd(Tensor a, Tensor resid, Tensor gamma, Tensor beta, double eps, double p, int64_t seed, int64_t opid,
-                           c10::optional<Tensor> q8, int64_t phase) {
-  check(a, BF16, "a"); check(resid, BF16, "resid"); check(gamma, F32, "gamma"); check(beta, F32, "beta");
-  TORCH_CHECK(a.dim() == 2 && a.sizes() == resid.sizes(), "a/resid shape");
+// resid = None: `a` already is z (EPI_BDR GEMM epilogue) -> returns {y, a, mean, rstd} without touching z
+std::vector<Tensor> ln_fwd(Tensor a, c10::optional<Tensor> resid_opt, Tensor gamma, Tensor beta, double eps, double p,
+                           int64_t seed, int64_t opid, c10::optional<Tensor> q8, int64_t phase) {
+  const bool zin = !(resid_opt.has_value() && resid_opt->defined());
+  check(a, BF16, "a"); check(gamma, F32, "gamma"); check(beta, F32, "beta");
+  if (!zin) check(*resid_opt, BF16, "resid");
+  TORCH_CHECK(a.dim() == 2 && (zin || a.sizes() == resid_opt->sizes()), "a/resid shape");
   const int64_t T = a.size(0), H = a.size(1);
   TORCH_CHECK(gamma.numel() == H && beta.numel() == H && H % 4 == 0 && H <= 2048, "hidden size");
   TORCH_CHECK(T * H < (int64_t)std::numeric_limits<uint32_t>::max(), "T*H exceeds 32-bit dropout index");
   const bool want8 = q8.has_value() && q8->defined();
+  TORCH_CHECK(!(zin && want8), "ln_fwd: the z-in form has no e4m3 output");
   if (want8) {
     check(*q8, F32, "q8");
     TORCH_CHECK(q8->numel() == 4, "q8 must be the f32[4] delayed-scaling state");
   }
   c10::DeviceGuard g(a.device());
-  auto y = at::empty_like(a), z = at::empty_like(a);
+  auto y = at::empty_like(a);
+  auto z = zin ? a : at::empty_like(a);
   auto mean = at::empty({T}, gamma.options()), rstd = at::empty({T}, gamma.options());
   Tensor y8 = want8 ? at::empty({T, H}, a.options().dtype(at::kFloat8_e4m3fn)) : Tensor();
-  hq_ln_fwd(ptr<uint16_t>(a), ptr<uint16_t>(resid), ptr<float>(gamma), ptr<float>(beta), ptr<uint16_t>(y), ptr<uint16_t>(z),
+  hq_ln_fwd(ptr<uint16_t>(a), zin ? nullptr : ptr<uint16_t>(*resid_opt), ptr<float>(gamma), ptr<float>(beta),
+            ptr<uint16_t>(y), zin ? nullptr : ptr<uint16_t>(z),
             ptr<float>(mean), ptr<float>(rstd), (int)T, (int)H, (float)eps, (float)p, u32(seed), u32(opid), cur_stream(),
             want8 ? reinterpret_cast<uint8_t*>(y8.data_ptr()) : nullptr, want8 ? ptr<float>(*q8) : nullptr,
             (int)(phase % 3));
@@ -143,14 +149,19 @@ std::vector<Tensor> ln_bwd(Tensor dy, c10::optional<Tensor> dy2, Tensor z, Tenso
 int64_t gemm_nt_supported(int64_t M, int64_t N, int64_t K) { return hq_gemm_nt_supported((int)M, (int)N, (int)K); }
 
 Tensor gemm_nt(Tensor A, Tensor B, int64_t epi, c10::optional<Tensor> bias, c10::optional<Tensor> pre,
-               c10::optional<Tensor> resid, c10::optional<Tensor> part, c10::optional<Tensor> out) {
+               c10::optional<Tensor> resid, c10::optional<Tensor> part, c10::optional<Tensor> out, double p, int64_t seed,
+               int64_t opid) {
   check(A, BF16, "A"); check(B, BF16, "B");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "gemm_nt: A[M,K], B[N,K] expected");
   const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
   TORCH_CHECK(M < (1ll << 31) / 4 && N * K < (1ll << 31) && M * N < (1ll << 40), "gemm_nt: shape too large");
   const int bn = hq_gemm_nt_supported((int)M, (int)N, (int)K);
   TORCH_CHECK(bn > 0, "gemm_nt: unsupported shape M=", M, " N=", N, " K=", K, " (need N%128, K%64 == 0)");
-  TORCH_CHECK(epi >= HQ_EPI_NONE && epi <= HQ_EPI_DMUL, "gemm_nt: bad epilogue");
+  TORCH_CHECK(epi >= HQ_EPI_NONE && epi <= HQ_EPI_BDR, "gemm_nt: bad epilogue");
+  if (epi == HQ_EPI_BDR) {
+    TORCH_CHECK(bias.has_value() && bias->defined(), "gemm_nt: EPI_BDR needs the fp32 bias");
+    TORCH_CHECK(M * N < (int64_t)std::numeric_limits<uint32_t>::max(), "gemm_nt: M*N exceeds 32-bit dropout index");
+  }
   c10::DeviceGuard g(A.device());
   Tensor C = (out.has_value() && out->defined()) ? *out : at::empty({M, N}, A.options());
   check(C, BF16, "out");
@@ -165,7 +176,7 @@ Tensor gemm_nt(Tensor A, Tensor B, int64_t epi, c10::optional<Tensor> bias, c10:
     check(*pre, BF16, "pre");
     TORCH_CHECK(pre->size(0) == M && pre->size(1) == N, "gemm_nt: pre shape");
   }
-  if (epi == HQ_EPI_RESID) {
+  if (epi == HQ_EPI_RESID || epi == HQ_EPI_BDR) {
     TORCH_CHECK(resid.has_value() && resid->defined(), "gemm_nt: resid required");
     check(*resid, BF16, "resid");
     TORCH_CHECK(resid->size(0) == M && resid->size(1) == N, "gemm_nt: resid shape");
@@ -178,7 +189,7 @@ Tensor gemm_nt(Tensor A, Tensor B, int64_t epi, c10::optional<Tensor> bias, c10:
   }
   hq_gemm_nt(ptr<uint16_t>(A), ptr<uint16_t>(B), ptr<uint16_t>(C), optr<float>(bias), optr<uint16_t>(pre),
              optr<uint16_t>(resid), optr<float>(part), (int)M, (int)N, (int)K, (int)K, (int)K, (int)N, (int)epi, bn,
-             cur_stream());
+             cur_stream(), (float)p, u32(seed), u32(opid));
   return C;
 }
 
@@ -591,7 +602,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("epi"), py::arg("bias") = py::none(),
         py::arg("pre") = py::none(), py::arg("resid") = py::none(), py::arg("part") = py::none(),
-        py::arg("out") = py::none());
+        py::arg("out") = py::none(), py::arg("p") = 0.0, py::arg("seed") = 0, py::arg("opid") = 0);
   m.def("gemm_nt_supported", &gemm_nt_supported);
   m.def("gemm_nt_part_rows", [](int64_t M, int64_t N, int64_t K) {
     return (int64_t)hq_gemm_nt_part_rows((int)M, (int)N, (int)K);

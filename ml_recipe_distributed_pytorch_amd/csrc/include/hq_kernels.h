@@ -21,7 +21,8 @@ HqDropKey hq_drop_key(uint32_t seed, uint32_t opid);
 // ---- norm.hip --------------------------------------------------------------------------------
 int hq_ln_bwd_partials(int T);
 int hq_rowblock_partials(int T);
-// y8 != null (fp8 path): y also as e4m3 under the delayed-scaling state q8 [4] at `phase` (see hq_common.h)
+// y8 != null (fp8 path): y also as e4m3 under the delayed-scaling state q8 [4] at `phase` (see hq_common.h);
+// resid == null (bf16 only): `a` already is z (an EPI_BDR GEMM wrote it) — only y, mean, rstd are written
 void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, const float* beta, uint16_t* y, uint16_t* z,
                float* mean, float* rstd, int T, int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s,
                uint8_t* y8 = nullptr, float* q8 = nullptr, int phase = 0);
@@ -77,7 +78,8 @@ void hq_cast_f32_bf16(const float* src, uint16_t* dst, int64_t n, float scale, h
 void hq_cast_bf16_f32(const uint16_t* src, float* dst, int64_t n, float scale, hipStream_t s);
 
 // ------------------------------------------------------------------ MFMA GEMM (gemm.hip)
-enum { HQ_EPI_NONE = 0, HQ_EPI_BIAS = 1, HQ_EPI_GELU = 2, HQ_EPI_DGELU = 3, HQ_EPI_RESID = 4, HQ_EPI_GELUD = 5, HQ_EPI_DMUL = 6 };
+enum { HQ_EPI_NONE = 0, HQ_EPI_BIAS = 1, HQ_EPI_GELU = 2, HQ_EPI_DGELU = 3, HQ_EPI_RESID = 4, HQ_EPI_GELUD = 5, HQ_EPI_DMUL = 6,
+       HQ_EPI_BDR = 7 };
 // kernel family for this shape: 256 / 128 = the 256-row kernels with that block width, 1 = the 128²-tile
 // kernel (M tails, low-fill grids), 0 = unsupported (need N % 128 == 0, K % 64 == 0)
 int hq_gemm_nt_supported(int M, int N, int K);
@@ -97,9 +99,12 @@ void hq_gemm_set_sched(int v);
 void hq_cu_hog(int blocks, int usec, hipStream_t s);
 // C[M,N] = A[M,K]·B[N,K]^T (+epilogue); P = GELU pre-activation (out for EPI_GELU, in for EPI_DGELU)
 // or its derivative gelu'(pre) (out for EPI_GELUD, in for EPI_DMUL);
-// R = residual (EPI_RESID); part = [M/256][N] column partial sums (EPI_DGELU)
+// R = residual (EPI_RESID, EPI_BDR); part = [M/256][N] column partial sums (EPI_DGELU)
+// EPI_BDR: C = z = dropout_p(bf16(acc + bias)) + R with the counter-hash stream (seed, opid) at element
+// index m·ldc + n — exactly what ln_fwd computes as z, so the following LayerNorm reads z alone
 void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,
-                float* part, int M, int N, int K, int lda, int ldb, int ldc, int epi, int bn, hipStream_t s);
+                float* part, int M, int N, int K, int lda, int ldb, int ldc, int epi, int bn, hipStream_t s,
+                float drop_p = 0.f, uint32_t drop_seed = 0, uint32_t drop_opid = 0);
 
 // Weight-gradient GEMM (gemm_tn.hip): out[N,K] (+)= Aᵀ·B, A = dy [T,N] bf16, B = x [T,K] bf16 (token-major),
 // split-K over T into S fp32 slabs part[S][N][K] (caller-provided) reduced into out; with bout != null

@@ -49,6 +49,24 @@ __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, 
 __device__ __forceinline__ float gelu_erf(float x) { return hq_gelu(x); }
 __device__ __forceinline__ float gelu_grad(float x) { return hq_gelu_grad(x); }
 
+// EPI_BDR dropout stream (unused by the other epilogues): key source, 16-bit keep threshold, keep scale
+struct HqDropArg {
+  HqDropKey kd;
+  uint32_t thr;
+  float ks;
+};
+// z = x·keep + r for 8 consecutive elements from flat index idx (even): ln_fwd's z, bit for bit
+__device__ __forceinline__ uint4 epi_bdr8(const uint4& piece, const uint4& r4, uint32_t idx, const HqDropArg& dr,
+                                          uint32_t key) {
+  float d[8], rr[8], m[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+  hq_unpack8(piece, d);
+  hq_unpack8(r4, rr);
+  if (dr.thr) hq_keep8(idx, key, dr.thr, dr.ks, m);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) d[e] = d[e] * m[e] + rr[e];
+  return hq_pack8(d);
+}
+
 // Issue the LDS-DMA of one [ROWS × 64] bf16 panel (rows of 128 B) into lds (+ byte offset).
 // Each wave-instruction moves 8 rows (64 lanes × 16 B); this wave handles `n_instr` of them
 // starting at panel row `row0`.
@@ -78,7 +96,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
                                                               uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                               uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
                                                               float* __restrict__ part, int M, int N, int K, int lda,
-                                                              int ldb, int ldc) {
+                                                              int ldb, int ldc, HqDropArg dr) {
+  const uint32_t key = EPI == HQ_EPI_BDR ? dr.kd.get() : 0u;   // EPI_BDR dropout key (device seed word under graphs)
   constexpr int WN = BN / 4;            // columns per wave
   constexpr int NJ = WN / 16;           // 16-wide n subtiles per wave
   constexpr int MI = 8;                 // 16-high m subtiles per wave (128 rows)
@@ -193,7 +212,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
   for (int j = 0; j < NJ; ++j) {
     const int nl = j * 16 + fq * 4;
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD) bv = *reinterpret_cast<const float4*>(bias + n0 + wn * WN + nl);
+    if constexpr (EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD || EPI == HQ_EPI_BDR) bv = *reinterpret_cast<const float4*>(bias + n0 + wn * WN + nl);
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       float v[4] = {acc[i][j][0] + bv.x, acc[i][j][1] + bv.y, acc[i][j][2] + bv.z, acc[i][j][3] + bv.w};
@@ -249,6 +268,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
 #pragma unroll
       for (int e = 0; e < 8; ++e) d[e] += rr[e];
       piece = hq_pack8(d);
+    } else if constexpr (EPI == HQ_EPI_BDR) {
+      piece = epi_bdr8(piece, *reinterpret_cast<const uint4*>(R + goff), (uint32_t)goff, dr, key);
     }
     *reinterpret_cast<uint4*>(C + goff) = piece;
   }
@@ -287,7 +308,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nts_kernel(const uint16_t* __rest
                                                           uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                           uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
                                                           float* __restrict__ part, int M, int N, int K, int lda, int ldb,
-                                                          int ldc, int ksplit, float* __restrict__ ws) {
+                                                          int ldc, int ksplit, float* __restrict__ ws, HqDropArg dr) {
+  const uint32_t key = EPI == HQ_EPI_BDR ? dr.kd.get() : 0u;   // EPI_BDR dropout key (device seed word under graphs)
   constexpr int SB = 128;                  // tile rows = tile cols
   constexpr int PANEL = SB * 128;          // one operand panel: 128 rows × 64 bf16
   constexpr int STAGE = 2 * PANEL;
@@ -391,7 +413,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nts_kernel(const uint16_t* __rest
 
   // ---- epilogue: acc (+bias) -> bf16 in this wave's LDS region [64][64], then row-coalesced 16-B pieces
   char* wreg = smem + wave * 64 * RS;
-  constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD;
+  constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD || EPI == HQ_EPI_BDR;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int nl = j * 16 + fq * 4;
@@ -450,6 +472,8 @@ __global__ __launch_bounds__(256, 2) void gemm_nts_kernel(const uint16_t* __rest
 #pragma unroll
       for (int e = 0; e < 8; ++e) d[e] += rr[e];
       piece = hq_pack8(d);
+    } else if constexpr (EPI == HQ_EPI_BDR) {
+      piece = epi_bdr8(piece, *reinterpret_cast<const uint4*>(R + goff), (uint32_t)goff, dr, key);
     }
     *reinterpret_cast<uint4*>(C + goff) = piece;
   }
@@ -528,7 +552,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
                                                                uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                                uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
                                                                float* __restrict__ part, int M, int N, int K, int lda,
-                                                               int ldb, int ldc) {
+                                                               int ldb, int ldc, HqDropArg dr) {
+  const uint32_t key = EPI == HQ_EPI_BDR ? dr.kd.get() : 0u;   // EPI_BDR dropout key (device seed word under graphs)
   constexpr int BN = 256;
   constexpr int PANEL = 256 * 128;      // one A or B panel (256 rows × 64 bf16)
   constexpr int HALF = 128 * 128;       // 128 rows of a panel
@@ -694,7 +719,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
   constexpr int SEGS = WN / 8;                  // 8 pieces of 16 B per local row
   constexpr int ROWS_PER_IT = 64 / SEGS;        // 8
   constexpr int NIT = 128 / ROWS_PER_IT;        // 16 row-coalesced pieces per lane
-  constexpr bool kReadsAux = EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID;
+  constexpr bool kReadsAux = EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR;
   const int seg = lane % SEGS, rsub = lane / SEGS;
   const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;   // 4 pieces per 32-col chunk
   auto grow_of = [&](int it) {
@@ -702,7 +727,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
     return m0 + (lr >> 6) * 128 + wm * 64 + (lr & 63);
   };
   char* wreg = smem + wave * (128 * RS);
-  constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD;
+  constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD || EPI == HQ_EPI_BDR;
 #pragma unroll
   for (int J = 0; J < 4; ++J) {
     const int nh = J >> 1, j = J & 1;
@@ -722,7 +747,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
   // drains vmcnt(0) before the first LDS write (the main loop's LDS-DMA shares the counter).
   uint4 aux[kReadsAux ? NIT : 1];
   if constexpr (kReadsAux) {
-    const uint16_t* src = EPI == HQ_EPI_RESID ? R : P;
+    const uint16_t* src = (EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR) ? R : P;
 #pragma unroll
     for (int it = 0; it < NIT; ++it) aux[it] = *reinterpret_cast<const uint4*>(src + (size_t)grow_of(it) * ldc + gcol);
   }
@@ -770,6 +795,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
 #pragma unroll
       for (int e = 0; e < 8; ++e) d[e] += rr[e];
       piece = hq_pack8(d);
+    } else if constexpr (EPI == HQ_EPI_BDR) {
+      piece = epi_bdr8(piece, aux[it], (uint32_t)goff, dr, key);
     }
     *reinterpret_cast<uint4*>(C + goff) = piece;
   }
@@ -820,7 +847,7 @@ __device__ __forceinline__ void store16(uint16_t* dst, const uint4& v, int nt) {
 template <int EPI>
 struct NT3Epi {
   static constexpr int kStores = 16 * (1 + (EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD ? 1 : 0));
-  static constexpr int kLoads = (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID) ? 16 : 0;
+  static constexpr int kLoads = (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR) ? 16 : 0;
   static constexpr int E = kStores + kLoads;   // vm ops per lane (the part store of waves 0-3 is not counted: a
 };                                             // smaller count only waits longer)
 
@@ -829,7 +856,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
                                                                uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                                uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
                                                                float* __restrict__ part, int M, int N, int K, int lda,
-                                                               int ldb, int ldc, int stagger, unsigned* __restrict__ sched) {
+                                                               int ldb, int ldc, int stagger, unsigned* __restrict__ sched,
+                                                               HqDropArg dr) {
+  const uint32_t key = EPI == HQ_EPI_BDR ? dr.kd.get() : 0u;   // EPI_BDR dropout key (device seed word under graphs)
   constexpr int BN = 256;
   constexpr int PANEL = 256 * 128;
   constexpr int STAGE = 2 * PANEL;
@@ -1044,8 +1073,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
 
     // ---- epilogue (v2's math), 64 local rows per round
     constexpr int SEGS = WN / 8, ROWS_PER_IT = 64 / SEGS;
-    constexpr bool kReadsAux = EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID;
-    constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD;
+    constexpr bool kReadsAux = EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR;
+    constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD || EPI == HQ_EPI_BDR;
     const int seg = lane % SEGS, rsub = lane / SEGS;
     const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;
     float csum[8];
@@ -1073,7 +1102,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
         return (size_t)(m0 + rnd * 128 + wm * 64 + lr) * ldc + gcol;
       };
       if constexpr (kReadsAux) {
-        const uint16_t* src = EPI == HQ_EPI_RESID ? R : P;
+        const uint16_t* src = (EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR) ? R : P;
 #pragma unroll
         for (int it = 0; it < 8; ++it) aux[it] = *reinterpret_cast<const uint4*>(src + goff_of(it));
       }
@@ -1122,6 +1151,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
 #pragma unroll
           for (int e = 0; e < 8; ++e) d[e] += rr[e];
           piece = hq_pack8(d);
+        } else if constexpr (EPI == HQ_EPI_BDR) {
+          piece = epi_bdr8(piece, aux[it], (uint32_t)goff, dr, key);
         }
         if (!(epi_flags & kDbgNoStore)) store16(C + goff, piece, epi_flags & kNtC);
         else asm volatile("" :: "v"(piece.x), "v"(piece.y), "v"(piece.z), "v"(piece.w));
@@ -1279,7 +1310,7 @@ constexpr size_t epi_lds(int bn) {
 
 template <int EPI>
 void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,
-                float* part, int M, int N, int K, int lda, int ldb, int ldc, int bn, hipStream_t s) {
+                float* part, int M, int N, int K, int lda, int ldb, int ldc, int bn, hipStream_t s, const HqDropArg& dr) {
   if (bn == 1) {   // vS: 128×128 tiles, M tail
     constexpr size_t lds = 2 * 2 * 128 * 128;
     static bool init = [] {
@@ -1291,7 +1322,7 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
     const int ks = nts_ksplit<EPI>(grid_s, K / BK);
     float* ws = ks > 1 ? hq_splitk_ws((size_t)ks * M * N) : nullptr;
     hipLaunchKernelGGL((gemm_nts_kernel<EPI>), dim3(grid_s * ks), dim3(256), lds, s, A, B, C, bias, P, R, part, M, N, K,
-                       lda, ldb, ldc, ks, ws);
+                       lda, ldb, ldc, ks, ws, dr);
     if (ks > 1) {
       const size_t n8 = (size_t)M * N / 8;
       const int g = (int)std::min<size_t>((n8 + 255) / 256, 2048);
@@ -1318,7 +1349,7 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
     const int nwg = std::min(grid, ncu);
     unsigned* sched = (g_gemm_sched && grid > 2 * nwg) ? nt3_sched_slot(s) : nullptr;
     hipLaunchKernelGGL((gemm_nt3_kernel<EPI>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, R, part,
-                       M, N, K, lda, ldb, ldc, g_gemm_stagger, sched);
+                       M, N, K, lda, ldb, ldc, g_gemm_stagger, sched, dr);
   } else if (bn == 256 && (g_gemm_variant == 0 || g_gemm_variant == 2 || g_gemm_variant == 3) && K >= 2 * BK && srd_ok) {
     // production v2: buffer_load…lds staging (+8-12 % over global_load_lds on the BERT shapes,
     // tools/gemm_lab); grouped 8-row-panel tile order only for wide N (+15 % at 8192², neutral at
@@ -1332,10 +1363,10 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
     (void)init;
     if (N / 256 >= 16)
       hipLaunchKernelGGL((gemm_nt2_kernel<EPI, 24>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, R, part, M, N, K,
-                         lda, ldb, ldc);
+                         lda, ldb, ldc, dr);
     else
       hipLaunchKernelGGL((gemm_nt2_kernel<EPI, 8>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, R, part, M, N, K,
-                         lda, ldb, ldc);
+                         lda, ldb, ldc, dr);
   } else if (bn == 256) {
     constexpr size_t lds = epi_lds(256);
     static bool init = [] {
@@ -1344,7 +1375,7 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
     }();
     (void)init;
     hipLaunchKernelGGL((gemm_nt_kernel<EPI, 256>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, R, part, M, N, K,
-                       lda, ldb, ldc);
+                       lda, ldb, ldc, dr);
   } else {
     constexpr size_t lds = epi_lds(128);
     static bool init = [] {
@@ -1353,7 +1384,7 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
     }();
     (void)init;
     hipLaunchKernelGGL((gemm_nt_kernel<EPI, 128>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, R, part, M, N, K,
-                       lda, ldb, ldc);
+                       lda, ldb, ldc, dr);
   }
 }
 
@@ -1403,14 +1434,21 @@ int hq_gemm_nt_part_rows(int M, int N, int K) {
 }
 
 void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,
-                float* part, int M, int N, int K, int lda, int ldb, int ldc, int epi, int bn, hipStream_t s) {
+                float* part, int M, int N, int K, int lda, int ldb, int ldc, int epi, int bn, hipStream_t s, float drop_p,
+                uint32_t drop_seed, uint32_t drop_opid) {
+  HqDropArg dr{hq_drop_key(drop_seed, drop_opid), 0u, 1.f};
+  if (epi == HQ_EPI_BDR && drop_p > 0.f) {
+    dr.thr = hq_threshold(drop_p);
+    dr.ks = hq_keep_scale(dr.thr);
+  }
   switch (epi) {
-    case HQ_EPI_NONE: launch_epi<HQ_EPI_NONE>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
-    case HQ_EPI_BIAS: launch_epi<HQ_EPI_BIAS>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
-    case HQ_EPI_GELU: launch_epi<HQ_EPI_GELU>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
-    case HQ_EPI_DGELU: launch_epi<HQ_EPI_DGELU>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
-    case HQ_EPI_RESID: launch_epi<HQ_EPI_RESID>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
-    case HQ_EPI_GELUD: launch_epi<HQ_EPI_GELUD>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
-    case HQ_EPI_DMUL: launch_epi<HQ_EPI_DMUL>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s); break;
+    case HQ_EPI_NONE: launch_epi<HQ_EPI_NONE>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
+    case HQ_EPI_BIAS: launch_epi<HQ_EPI_BIAS>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
+    case HQ_EPI_GELU: launch_epi<HQ_EPI_GELU>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
+    case HQ_EPI_DGELU: launch_epi<HQ_EPI_DGELU>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
+    case HQ_EPI_RESID: launch_epi<HQ_EPI_RESID>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
+    case HQ_EPI_GELUD: launch_epi<HQ_EPI_GELUD>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
+    case HQ_EPI_DMUL: launch_epi<HQ_EPI_DMUL>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
+    case HQ_EPI_BDR: launch_epi<HQ_EPI_BDR>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
   }
 }

@@ -103,6 +103,72 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict_
   }
 }
 
+// y = LN(z) where z = dropout(a) + resid was already written by the producing GEMM's EPI_BDR epilogue
+// (out-projection / FFN2): one read stream and one write stream instead of ln_fwd_kernel's two + two.  With
+// half the bytes per row a wave keeps RPW rows' loads in flight together (one row per wave left it
+// latency-bound: 75 µs at T = 98304 vs ~50 µs of HBM time).  Same statistics and rounding as ln_fwd_kernel.
+template <int NCH, int RPW>
+__global__ __launch_bounds__(256) void ln_fwd_z_kernel(const uint16_t* __restrict__ zin, const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, uint16_t* __restrict__ y,
+                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out, int T,
+                                                       int H, float eps) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row0 = (blockIdx.x * kWaves + wave) * RPW;
+  float v[RPW][NCH][4];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 256 + lane * 4;
+      if (row0 + r < T && col < H) hq_unpack4(*reinterpret_cast<const uint2*>(zin + (size_t)(row0 + r) * H + col), v[r][c]);
+      else v[r][c][0] = v[r][c][1] = v[r][c][2] = v[r][c][3] = 0.f;
+    }
+  float mean[RPW], rstd[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    float sum = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sum += v[r][c][i];
+    mean[r] = hq_wave_sum(sum) / H;
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    float sq = 0.f;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 256 + lane * 4;
+      if (col < H) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { const float d = v[r][c][i] - mean[r]; sq += d * d; }
+      }
+    }
+    rstd[r] = rsqrtf(hq_wave_sum(sq) / H + eps);
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    if (col < H) {
+      const float4 g = *reinterpret_cast<const float4*>(gamma + col);
+      const float4 b = *reinterpret_cast<const float4*>(beta + col);
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        if (row0 + r < T) {
+          float o[4] = {(v[r][c][0] - mean[r]) * rstd[r] * g.x + b.x, (v[r][c][1] - mean[r]) * rstd[r] * g.y + b.y,
+                        (v[r][c][2] - mean[r]) * rstd[r] * g.z + b.z, (v[r][c][3] - mean[r]) * rstd[r] * g.w + b.w};
+          *reinterpret_cast<uint2*>(y + (size_t)(row0 + r) * H + col) = hq_pack4(o);
+        }
+      }
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+      if (row0 + r < T) { mean_out[row0 + r] = mean[r]; rstd_out[row0 + r] = rstd[r]; }
+  }
+}
+
 // Reduce NQ per-lane column accumulators over the 4 waves of the block into part[block][q][H].
 template <int NCH, int NQ>
 __device__ __forceinline__ void block_partials(float (&acc)[NQ][NCH][4], float* lds, float* part, int H) {
@@ -700,6 +766,10 @@ void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, con
       hipLaunchKernelGGL((ln_fwd_kernel<decltype(nch)::value, true>), dim3(g8), dim3(256), 0, s, a, resid, gamma, beta,
                          y, z, mean, rstd, T, H, eps, key, thr, ks, y8, q8, part8, phase);
       hq_fp8_amax_fold(part8, g8 * kWaves, q8, phase, s);
+    } else if (!resid) {   // z-in: a = z from an EPI_BDR GEMM epilogue
+      constexpr int RPW = 2;
+      hipLaunchKernelGGL((ln_fwd_z_kernel<decltype(nch)::value, RPW>), dim3((T + kWaves * RPW - 1) / (kWaves * RPW)),
+                         dim3(256), 0, s, a, gamma, beta, y, mean, rstd, T, H, eps);
     } else {
       hipLaunchKernelGGL((ln_fwd_kernel<decltype(nch)::value, false>), dim3(blocks), dim3(256), 0, s, a, resid, gamma,
                          beta, y, z, mean, rstd, T, H, eps, key, thr, ks, nullptr, nullptr, nullptr, 0);

@@ -198,14 +198,15 @@ class _LayerFn(torch.autograd.Function):
                                         Bm("attention.output.dense.bias"))
         else:
             ctxv, lse, bits = ops.attn_fwd(qkv, key_bias, B, L, nh, pa, info.seed, op0, scale)
-            a1 = proj(ctxv, "attention.output.dense")
         ln1 = (st.view(p + "attention.output.LayerNorm.weight", "master"),
                st.view(p + "attention.output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph, info.seed, op0 + 1)
         h1_8 = None
         if fp8:
             h1, z1, m1, r1, h1_8 = ops.ln_fwd_q8(a1, x, *ln1, s8["ffn1"])
-        else:
-            h1, z1, m1, r1 = ops.ln_fwd(a1, x, *ln1)
+        else:   # out-projection + dropout + residual + LayerNorm (fused epilogue on the GPU)
+            name = "attention.output.dense"
+            h1, z1, m1, r1 = ops.linear_bdr_ln_fwd(ctxv, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), x,
+                                                   kinds[name], *ln1)
         act8 = None
         r8 = (ops.linear_gelu_fwd_fp8(h1, W8("intermediate.dense"), Bm("intermediate.dense.bias"), s8["ffn1"],
                                       s8["ffn2"], x8=h1_8) if fp8 else None)
@@ -215,16 +216,18 @@ class _LayerFn(torch.autograd.Function):
         else:  # `pre` holds gelu'(pre) when the fused MFMA epilogue ran (ctx.gelu_deriv)
             pre, act, ctx.gelu_deriv = ops.linear_gelu_fwd_d(h1, st.view(p + "intermediate.dense.weight"),
                                                              Bb("intermediate.dense"), Bm("intermediate.dense.bias"))
-        if act8 is not None:
-            a2 = ops.linear_fwd_fp8_own(act8, s8["ffn2"], W8("output.dense"), Bm("output.dense.bias"))
-        else:
-            a2 = proj(act, "output.dense")
         ln2 = (st.view(p + "output.LayerNorm.weight", "master"), st.view(p + "output.LayerNorm.bias", "master"),
                cfg.layer_norm_eps, ph, info.seed, op0 + 2)
-        if fp8 and idx + 1 < cfg.num_hidden_layers:  # the next layer's QKV input, in e4m3
-            h2, z2, m2, r2, info.x8[idx + 1] = ops.ln_fwd_q8(a2, h1, *ln2, m.fp8_states(idx + 1)["qkv"])
-        else:
-            h2, z2, m2, r2 = ops.ln_fwd(a2, h1, *ln2)
+        if act8 is not None:
+            a2 = ops.linear_fwd_fp8_own(act8, s8["ffn2"], W8("output.dense"), Bm("output.dense.bias"))
+            if idx + 1 < cfg.num_hidden_layers:  # the next layer's QKV input, in e4m3
+                h2, z2, m2, r2, info.x8[idx + 1] = ops.ln_fwd_q8(a2, h1, *ln2, m.fp8_states(idx + 1)["qkv"])
+            else:
+                h2, z2, m2, r2 = ops.ln_fwd(a2, h1, *ln2)
+        else:   # FFN2 + dropout + residual + LayerNorm (fused epilogue on the GPU)
+            name = "output.dense"
+            h2, z2, m2, r2 = ops.linear_bdr_ln_fwd(act, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), h1,
+                                                   kinds[name], *ln2)
         ctx.save_for_backward(x, key_bias, qkv, ctxv, lse, z1, m1, r1, h1, pre, act, z2, m2, r2)
         ctx.bits = bits
         ctx.info, ctx.idx, ctx.ph, ctx.pa, ctx.scale = info, idx, ph, pa, scale

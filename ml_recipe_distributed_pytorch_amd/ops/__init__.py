@@ -121,7 +121,7 @@ def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale
 #     128² tiles by M alignment and CU fill).  Weight gradients take the split-K TN kernel (gemm_tn.hip).
 #     Plain forward projections follow FWD_MFMA below (all three on the MFMA kernel by default);
 #   HQ_GEMM=mfma: every supported shape;  HQ_GEMM=blas: none.
-_EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID, _EPI_GELUD, _EPI_DMUL = range(7)
+_EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID, _EPI_GELUD, _EPI_DMUL, _EPI_BDR = range(8)
 _GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
 # Plain forward projections (bias epilogue) that take the MFMA kernel in auto mode, by name: qkv | out | ffn2.
 # In the full b256 step hipBLASLt's QKV pick runs 381 µs vs 316 µs standalone while the MFMA kernel holds
@@ -130,6 +130,9 @@ _GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
 # GEMMs stay in torch).
 FWD_MFMA = {k for k in os.environ.get("HQ_FWD_MFMA", "qkv,out,ffn2").split(",") if k}
 GELU_DERIV = os.environ.get("HQ_GELU_DERIV", "1") == "1"   # FFN1 stores gelu'(pre) (linear_gelu_fwd_d)
+# The out-projection / FFN2 GEMM writes z = dropout(x·Wᵀ + b) + resid itself (EPI_BDR) and the LayerNorm
+# that follows reads z alone: one HBM pass over [T, H] less per LayerNorm (linear_bdr_ln_fwd)
+LN_FUSE = os.environ.get("HQ_LN_FUSE", "1") == "1"
 
 
 def set_gemm_mode(mode: str) -> str:
@@ -165,6 +168,18 @@ def linear_fwd(x, w, b, b32=None, kind: str = "plain"):
             return _k().gemm_nt(x, w, _EPI_BIAS, bias=b32)
         return torch.addmm(b, x, w.t()) if b is not None else torch.mm(x, w.t())
     return ref.linear_fwd(x, w, b)
+
+
+def linear_bdr_ln_fwd(x, w, b, b32, resid, kind, gamma, beta, eps, p, seed, opid):
+    """LayerNorm(dropout_p(x·Wᵀ + b) + resid) -> (y, z, mean, rstd), bitwise what ``linear_fwd`` followed by
+    ``ln_fwd`` computes.  On the GPU with the own MFMA kernel the GEMM's EPI_BDR epilogue adds the dropped-out
+    projection to the residual and stores z, and the LayerNorm reads z alone (``ln_fwd`` with resid=None);
+    otherwise the two ops run as before."""
+    if (x.is_cuda and LN_FUSE and b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1], kind)
+            and x.shape[0] * w.shape[0] < 2 ** 32):
+        z = _k().gemm_nt(x, w, _EPI_BDR, bias=b32, resid=resid, p=float(p), seed=int(seed), opid=int(opid))
+        return tuple(_k().ln_fwd(z, None, gamma, beta, float(eps), 0.0, 0, 0))
+    return ln_fwd(linear_fwd(x, w, b, b32, kind), resid, gamma, beta, eps, p, seed, opid)
 
 
 def linear_fwd_fp8(x, w8s, b):

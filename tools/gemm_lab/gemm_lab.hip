@@ -21,8 +21,10 @@ __global__ void fill_rand(uint16_t* p, size_t n, uint32_t seed) {
   }
 }
 
+HqDropKey hq_drop_key(uint32_t seed, uint32_t opid) { return HqDropKey{hq_op_key(seed, opid), opid, nullptr}; }
+
 typedef void (*Kern)(const uint16_t*, const uint16_t*, uint16_t*, const float*, uint16_t*, const uint16_t*, float*, int,
-                     int, int, int, int, int);
+                     int, int, int, int, int, HqDropArg);
 
 struct Variant { const char* name; Kern k; };
 
@@ -57,10 +59,10 @@ int main(int argc, char** argv) {
     const int iters = 10;
     for (int round = 0; round < 5; ++round)
       for (int v = 0; v < NV; ++v) {
-        hipLaunchKernelGGL(vs[v].k, dim3(grid), dim3(512), lds, 0, A, B, C, nullptr, nullptr, nullptr, nullptr, M, N, K, K, K, N);
+        hipLaunchKernelGGL(vs[v].k, dim3(grid), dim3(512), lds, 0, A, B, C, nullptr, nullptr, nullptr, nullptr, M, N, K, K, K, N, HqDropArg{});
         CK(hipEventRecord(e0));
         for (int i = 0; i < iters; ++i)
-          hipLaunchKernelGGL(vs[v].k, dim3(grid), dim3(512), lds, 0, A, B, C, nullptr, nullptr, nullptr, nullptr, M, N, K, K, K, N);
+          hipLaunchKernelGGL(vs[v].k, dim3(grid), dim3(512), lds, 0, A, B, C, nullptr, nullptr, nullptr, nullptr, M, N, K, K, K, N, HqDropArg{});
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         float ms;
