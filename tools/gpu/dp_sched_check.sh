@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$(dirname "$0")/../.."
 export TMPDIR=/tmp
-O=gpurun_out/${1:-sched_policy}
+O=gpurun_out/${1:-dp_sched}
 mkdir -p "$O"
 timeout -k 10 300 python -u -m pytest tests/test_gemm_sched_gpu.py tests/test_reducer_gpu.py tests/test_gemm_gpu.py -x -q --timeout 120 --timeout-method thread -m gpu > "$O/pytest.log" 2>&1 || { tail -40 "$O/pytest.log"; exit 1; }
 tail -1 "$O/pytest.log"
