@@ -1,6 +1,7 @@
 #!/usr/bin/env python
-"""In-process interleaved A/B of a persistent-GEMM (v3) flag word (gemm_set_stagger: bits 0-7 stagger, 8-15
-HQ_GEMM_EPIFLAGS) on the BERT-base b256 shapes that run on v3.  Usage: tools/gemm_knob_ab.py 0 4096 [...]"""
+"""In-process interleaved A/B of persistent-GEMM (v3) flag words (gemm_set_stagger: bits 0-7 stagger in
+units of s_sleep(127), bits 8-15 HQ_GEMM_EPIFLAGS diagnostics) on the BERT-base b256 shapes that run on v3.
+Usage: tools/gemm_knob_ab.py 0 0x2 [...]  (default: 0 vs stagger 2)"""
 import json
 import os
 import statistics
@@ -16,7 +17,7 @@ SHAPES = (("qkv_fwd_bias", 2304, 768, 1), ("out_fwd_bdr", 768, 768, 7), ("ffn1_f
 
 
 def main():
-    words = [int(w, 0) for w in sys.argv[1:]] or [0, 16 << 8]
+    words = [int(w, 0) for w in sys.argv[1:]] or [0, 2]
     k = _native.kernels()
     dev = torch.device("cuda", 0)
     M = 98304
