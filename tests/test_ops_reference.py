@@ -149,3 +149,21 @@ def test_wgrad_split_heuristic():
     for T, N, K in ((24576, 768, 768), (24576, 2304, 768), (24576, 3072, 768), (32768, 768, 3072)):
         s = _wgrad_splits(T, N, K)
         assert T % s == 0
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_linear_bdr_ln_fwd_cpu_path(p):
+    """The fused projection + dropout + residual + LayerNorm op (GPU: EPI_BDR epilogue + z-in LayerNorm)
+    falls back on the CPU to linear_fwd → ln_fwd; its z is dropout(x·Wᵀ + b) + resid and y = LN(z)."""
+    from ml_recipe_distributed_pytorch_amd import ops
+    torch.manual_seed(0)
+    T, K, N = 64, 48, 32
+    x, w, b = torch.randn(T, K), torch.randn(N, K) * 0.2, torch.randn(N)
+    resid = torch.randn(T, N)
+    gamma, beta = torch.randn(N) * 0.1 + 1, torch.randn(N) * 0.1
+    y, z, mean, rstd = ops.linear_bdr_ln_fwd(x, w, b, None, resid, "out", gamma, beta, 1e-12, p, 1234, 7)
+    y2, z2, m2, r2 = R.ln_fwd(R.linear_fwd(x, w, b), resid, gamma, beta, 1e-12, p, 1234, 7)
+    assert torch.equal(z, z2) and torch.equal(y, y2) and torch.equal(mean, m2) and torch.equal(rstd, r2)
+    if p == 0.0:
+        ref = F.layer_norm(x @ w.t() + b + resid, (N,), gamma, beta, 1e-12)
+        assert (y - ref).abs().max().item() < 1e-4
