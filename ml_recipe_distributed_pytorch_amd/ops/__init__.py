@@ -130,9 +130,11 @@ _GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
 # GEMMs stay in torch).
 FWD_MFMA = {k for k in os.environ.get("HQ_FWD_MFMA", "qkv,out,ffn2").split(",") if k}
 GELU_DERIV = os.environ.get("HQ_GELU_DERIV", "1") == "1"   # FFN1 stores gelu'(pre) (linear_gelu_fwd_d)
-# The out-projection / FFN2 GEMM writes z = dropout(x·Wᵀ + b) + resid itself (EPI_BDR) and the LayerNorm
-# that follows reads z alone: one HBM pass over [T, H] less per LayerNorm (linear_bdr_ln_fwd)
-LN_FUSE = os.environ.get("HQ_LN_FUSE", "1") == "1"
+# HQ_LN_FUSE=1: the out-projection / FFN2 GEMM writes z = dropout(x·Wᵀ + b) + resid itself (EPI_BDR) and the
+# LayerNorm that follows reads z alone — one HBM pass over [T, H] less per LayerNorm, bitwise the same
+# result.  Off by default: the epilogue's residual read and dropout hash are serial with the persistent GEMM's
+# MFMA work and cost what the LayerNorm saves (same-box step A/B 3847 vs 3839 samples/s, profiles/r2_ln_fuse)
+LN_FUSE = os.environ.get("HQ_LN_FUSE", "0") == "1"
 
 
 def set_gemm_mode(mode: str) -> str:
