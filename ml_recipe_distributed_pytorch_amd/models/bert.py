@@ -203,7 +203,7 @@ class _LayerFn(torch.autograd.Function):
         h1_8 = None
         if fp8:
             h1, z1, m1, r1, h1_8 = ops.ln_fwd_q8(a1, x, *ln1, s8["ffn1"])
-        else:   # out-projection + dropout + residual + LayerNorm (fused epilogue on the GPU)
+        else:   # out-projection + dropout + residual + LayerNorm (one GEMM epilogue + z-in LN under HQ_LN_FUSE=1)
             name = "attention.output.dense"
             h1, z1, m1, r1 = ops.linear_bdr_ln_fwd(ctxv, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), x,
                                                    kinds[name], *ln1)
@@ -224,7 +224,7 @@ class _LayerFn(torch.autograd.Function):
                 h2, z2, m2, r2, info.x8[idx + 1] = ops.ln_fwd_q8(a2, h1, *ln2, m.fp8_states(idx + 1)["qkv"])
             else:
                 h2, z2, m2, r2 = ops.ln_fwd(a2, h1, *ln2)
-        else:   # FFN2 + dropout + residual + LayerNorm (fused epilogue on the GPU)
+        else:   # FFN2 + dropout + residual + LayerNorm (one GEMM epilogue + z-in LN under HQ_LN_FUSE=1)
             name = "output.dense"
             h2, z2, m2, r2 = ops.linear_bdr_ln_fwd(act, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), h1,
                                                    kinds[name], *ln2)
