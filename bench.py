@@ -18,7 +18,15 @@ import sys
 import time
 from types import SimpleNamespace
 
-METRIC = "samples/sec (whole node) BERT-base QA fine-tune seq=384 at 1/2/4/8 MI355X"
+METRIC = "samples/sec (whole node) BERT-base QA fine-tune seq=384 at 1/2/4/8 MI355X"   # BASELINE.json
+
+
+def metric_name(model: str, seq: int, batch: int, precision: str) -> str:
+    """BASELINE.json's metric string for the headline config (BERT-base, seq 384, 256 samples per GPU, bf16);
+    any other --model / --seq / --batch / --precision gets a label that names what was measured."""
+    if model == "bert-base-uncased" and seq == 384 and batch == 256 and precision == "bf16":
+        return METRIC
+    return f"samples/sec (whole node) {model} QA fine-tune seq={seq} batch={batch}/GPU {precision} (not the headline config)"
 # The reference publishes no numbers; BASELINE.md's "baseline to beat" is the reference recipe re-run
 # on the same MI355X (HF BertModel + its QA heads/loss, autocast bf16 for apex O1, AdamW, clip):
 # tools/ref_recipe_bench.py --batch 256 --attn sdpa (the faster of its two attention paths) = 1611.65.
@@ -75,14 +83,20 @@ def main():
         os.environ.setdefault("NCCL_MIN_NCHANNELS", str(args.rccl_channels))
         os.environ.setdefault("NCCL_MAX_NCHANNELS", str(args.rccl_channels))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1:
+    # Launched by torchrun / torch.distributed.run (RANK in the env): the process group is initialised at ANY
+    # world size, so `torchrun --nproc-per-node 1 bench.py --force_reducer` runs every line an 8-GPU run does
+    # (RCCL init with device_id, the reducer's TCPStore uid exchange and native broadcast, the dynamic GEMM
+    # schedule, barrier, all_reduce(MAX), destroy).  Plain `python bench.py` (the driver's N=1 run) has none.
+    launched = hqdist.env_launched()
+    backend = None
+    if launched:
         # HQ_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with every rank on cuda:0 (one-GPU box; gloo
         # all-reduces the CUDA buckets through host memory) — never for a measurement
         backend = os.environ.get("HQ_BENCH_BACKEND", "nccl")
         if backend != "nccl":
             os.environ["LOCAL_RANK"] = "0"
         info = hqdist.init_distributed(backend)
-        rank, device = info.rank, info.device
+        rank, device, world = info.rank, info.device, dist.get_world_size()
     else:
         rank, device = 0, torch.device("cuda", 0)
         torch.cuda.set_device(device)
@@ -101,6 +115,7 @@ def main():
     sched = get_linear_schedule_with_warmup(opt, int(0.05 * total), total)
     reducer = None
     if world > 1 or args.force_reducer:
+        # world > 1 or --force_reducer (1-rank communicator): every bucket goes through the native RCCL reducer
         reducer = GradReducer(model, bucket_cap_mb=args.bucket_cap_mb, allreduce_dtype=args.allreduce_dtype,
                               force=args.force_reducer, timing=os.environ.get("HQ_BENCH_COMM_TIMING", "1") == "1")
     # HQ_BENCH_REDUCER_IDLE=1 (diagnostic): the reducer and its RCCL communicator exist but the engine never
@@ -140,7 +155,7 @@ def main():
     torch.cuda.synchronize()
     if reducer is not None:
         reducer.pop_timings()  # drop the warmup steps' comm events
-    if world > 1:
+    if launched:
         hqdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -150,11 +165,11 @@ def main():
         for k, v in res.timings.items():
             phase[k] = phase.get(k, 0.0) + v
     torch.cuda.synchronize()
-    if world > 1:
+    if launched:
         hqdist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if launched:   # the slowest rank's clock (a 1-rank all_reduce at world 1)
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -165,7 +180,8 @@ def main():
     H, F, NL = cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers
     enc_linear = NL * (4 * H * H + 2 * H * F)  # 85.0 M (base), 302 M (large)
     flops_per_sample = 6 * enc_linear * L + 12 * L * L * H * NL  # SURVEY §6.2 model
-    out = {"metric": METRIC, "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+    from ml_recipe_distributed_pytorch_amd import hw_queue_info
+    out = {"metric": metric_name(args.model, L, B, args.precision), "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": (round(value / (BASELINE_VALUE * world), 4) if BASELINE_VALUE else None), "dtype": args.precision,
            "data": "synthetic (dummy-QA generator, random-init weights)",
@@ -173,6 +189,10 @@ def main():
                       "parallelism": f"dp{world}", "allreduce_dtype": args.allreduce_dtype,
                       "bucket_cap_mb": args.bucket_cap_mb,
                       "rccl_channels": os.environ.get("NCCL_MIN_NCHANNELS")},
+           "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+           "process_group": backend or "none",
+           "rccl_comm_ranks": reducer.comm_ranks if reducer is not None else None,
+           "hw_queues": hw_queue_info()["live"],
            "graph_replays": engine.graph_replays,
            "reducer": reducer.kind if reducer is not None else "none",
            "reducer_buckets": reducer.n_buckets if reducer is not None else 0,
@@ -192,7 +212,7 @@ def main():
                 f.write(line + "\n")
     if reducer is not None:
         reducer.close()
-    if world > 1:
+    if launched:
         hqdist.destroy()
 
 

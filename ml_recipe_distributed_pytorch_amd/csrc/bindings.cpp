@@ -202,7 +202,7 @@ void gemm_tn(Tensor dy, Tensor x, Tensor out, bool accumulate, int64_t splits, c
   const int64_t T = dy.size(0), N = dy.size(1), K = x.size(1);
   TORCH_CHECK(out.numel() == N * K, "gemm_tn: out must hold N*K");
   const int auto_s = hq_gemm_tn_splits((int)T, (int)N, (int)K);
-  TORCH_CHECK(auto_s > 0, "gemm_tn: unsupported shape T=", T, " N=", N, " K=", K, " (need N%256, K%256 == 0, T >= 128)");
+  TORCH_CHECK(auto_s > 0, "gemm_tn: unsupported shape T=", T, " N=", N, " K=", K, " (need N%128, K%128 == 0, T >= 128)");
   const int S = splits > 0 ? (int)splits : auto_s;
   TORCH_CHECK((T + 63) / 64 / S >= 2, "gemm_tn: too many splits");
   const bool has_bias = bias_out.has_value() && bias_out->defined();
@@ -616,6 +616,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("gemm_tn", &gemm_tn, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("accumulate") = false,
         py::arg("splits") = 0, py::arg("bias_out") = py::none());
   m.def("gemm_tn_splits", &gemm_tn_splits);
+  m.def("attn_set_force_slow", [](int64_t v) { hq_attn_set_force_slow((int)v); });
   m.def("transpose_tiles", &transpose_tiles);
   m.def("colsum_into", &colsum_into);
   m.def("fp8_quantize", &fp8_quantize);
@@ -671,5 +672,6 @@ PYBIND11_MODULE(_hq_kernels, m) {
       .def("synchronize", &HqReducer::synchronize, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("comm_stream", &HqReducer::comm_stream)
       .def_property_readonly("rank", &HqReducer::rank)
-      .def_property_readonly("world", &HqReducer::world);
+      .def_property_readonly("world", &HqReducer::world)
+      .def_property_readonly("comm_count", &HqReducer::comm_count);
 }

@@ -45,6 +45,7 @@ void hq_gelu_bwd(const uint16_t* dout, const uint16_t* pre, uint16_t* dpre, floa
 void hq_bias_grad(const uint16_t* dy, float* part, HqOuts outs, int T, int N, bool accumulate, hipStream_t s);
 
 // ---- attention.hip ----------------------------------------------------------------------------
+void hq_attn_set_force_slow(int v);          // tests: every ring-forward workgroup takes the slow path
 size_t hq_attn_mask_bytes(int B, int L, int nh);   // dropout keep-bits written by fwd, read by bwd
 // ctx8 / q8 / phase (optional, --precision fp8): ctx also written as e4m3 under the delayed-scaling state q8
 void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, float* lse, uint16_t* mbits, int B, int L,

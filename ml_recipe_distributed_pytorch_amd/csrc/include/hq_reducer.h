@@ -27,6 +27,8 @@ class HqReducer {
   int64_t comm_stream() const { return (int64_t)stream_; }
   int rank() const { return rank_; }
   int world() const { return world_; }
+  // ranks the RCCL communicator actually spans (ncclCommCount) — bench.py reports it as proof of world size
+  int comm_count() const;
 
  private:
   static constexpr int kEvents = 64;

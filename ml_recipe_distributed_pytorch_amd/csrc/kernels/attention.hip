@@ -244,166 +244,6 @@ __device__ __forceinline__ void load_heads2(uint16_t* dstA, const uint16_t* srcA
   }
 }
 
-// ============================================================================ forward
-// NT > 0: compile-time count of 32-key tiles (L = 32·NT, the common BERT lengths): the key loop is
-// fully unrolled so every LDS address is base + immediate.  NT = 0: runtime count, rolled loop.
-template <int NWB, bool DROP, bool EVEN, int NT>
-__global__ __launch_bounds__(NWB * 64) void attn_fwd_kernel(const uint16_t* __restrict__ qkv,
-                                                            const float* __restrict__ key_bias,
-                                                            uint16_t* __restrict__ ctx, float* __restrict__ lse,
-                                                            uint16_t* __restrict__ mbits, int L, int nh, float c_scale,
-                                                            HqDropKey kd_, uint32_t thr, float kscale) {
-  const uint32_t key = kd_.get();
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int UNR = NT > 0 ? NT : 1;
-  const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
-  uint16_t* sK = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* sV = sK + Lp * D;
-  float* sB = reinterpret_cast<float*>(sV + Lp * D);
-  const int H = nh * D, ld = 3 * H;
-  const int bh = blockIdx.x, b = bh / nh, h = bh % nh;
-  HQ_DASSERT(L > 0 && L <= 512 && (NT == 0 || L == NT * 32));
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, hh = lane >> 5;
-  const int qs = blockIdx.y * NWB + wave;  // 32-query subtile
-  const int qi = qs * 32 + (lane & 31);
-  const uint16_t* base = qkv + (size_t)b * L * ld + h * D;
-
-  bf16x8_t qf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s)
-    qf[s] = (qi < L) ? prescale8(*reinterpret_cast<const bf16x8_t*>(base + (size_t)qi * ld + 16 * s + 8 * hh), c_scale)
-                     : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-  load_heads2<NWB * 64>(sK, base + H, ld, sV, base + 2 * H, ld, L, Lp);
-  for (int t = threadIdx.x; t < Lp; t += NWB * 64) sB[t] = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -INFINITY;
-  __syncthreads();
-  if (qs * 32 >= L) return;
-  LdsOffsets lo_;
-  lo_.init(lane);
-  wave_prio(wave, NWB);
-
-  f32x16_t o[2];
-#pragma unroll
-  for (int d = 0; d < 2; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
-  float m_run = -INFINITY;
-  const float defer = g_attn_defer;
-  f2_t l2 = {0.f, 0.f};  // running row sum, two partial sums (packed adds)
-  const uint32_t row_idx = ((uint32_t)bh * L + (uint32_t)min(qi, L - 1)) * (uint32_t)L;
-  uint16_t* my_bits = mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane;
-
-  // Software pipeline (unrolled NT > 0 path): the per-tile rescale branch splits the loop body into
-  // basic blocks the scheduler cannot cross, so the K-row fragments and bias of tile kt+1 and the
-  // V fragments of tile kt are read explicitly before the softmax of tile kt, hiding LDS latency.
-  bf16x8_t kn[4];
-  float4 bn[4];
-  auto fetch_k = [&](int kt) {
-#pragma unroll
-    for (int s = 0; s < 4; ++s) kn[s] = row8(sK, kt * 32, lo_, s);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) bn[g] = *reinterpret_cast<const float4*>(sB + kt * 32 + 8 * g + 4 * hh);
-  };
-  if constexpr (NT > 0) fetch_k(0);
-
-#pragma unroll UNR
-  for (int kt = 0; kt < n32; ++kt) {
-    f32x16_t acc;
-    if constexpr (NT == 0) fetch_k(kt);
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {  // accumulator starts at the key-mask bias (log2 domain)
-      acc[4 * g + 0] = bn[g].x; acc[4 * g + 1] = bn[g].y; acc[4 * g + 2] = bn[g].z; acc[4 * g + 3] = bn[g].w;
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) acc = mfma32(kn[s], qf[s], acc);
-    bf16x8_t vt[2][2];
-    constexpr bool kVEarly = NT > 0 && !DROP;  // with dropout the early V fragments would spill (168 VGPRs)
-    if constexpr (NT > 0) {
-      if (kt + 1 < n32) fetch_k(kt + 1);
-    }
-    if constexpr (kVEarly) {
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int d = 0; d < 2; ++d) vt[s][d] = tr8(sV, kt * 32, lo_, s, d);
-    }
-    const float mx = xor32_max(max16(acc));
-    // deferred max (playbook T13): rescale only when some lane's tile max exceeds its running max by more
-    // than `defer`, so after the first tiles the branch (and its O-wide multiply) is rarely taken.  P
-    // then stays <= 2^defer: exact in the fp32 row sum and O accumulators, and bf16 P keeps its
-    // relative precision; LSE = m_run + log2(l) remains exact for the backward.
-    if (__any(mx > m_run + defer)) {
-      const float m_new = fmaxf(m_run, mx);
-      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-      m_run = m_new;
-      const f2_t a2 = {alpha, alpha};
-      l2 *= a2;
-#pragma unroll
-      for (int d = 0; d < 2; ++d)
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          f2_t v = {o[d][r], o[d][r + 1]};
-          v *= a2;
-          o[d][r] = v.x; o[d][r + 1] = v.y;
-        }
-    }
-    float sc[16];
-    const f2_t m2 = {m_run, m_run};
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) {
-      f2_t v = {acc[r], acc[r + 1]};
-      v -= m2;
-      sc[r] = __builtin_amdgcn_exp2f(v.x);
-      sc[r + 1] = __builtin_amdgcn_exp2f(v.y);
-      const f2_t e = {sc[r], sc[r + 1]};
-      l2 += e;  // the softmax denominator counts every key; dropout only thins the P·V product
-    }
-    if constexpr (DROP) {
-      // keep bits straight from the integer compares; the 1/(1-p) scale is applied once to O at the end
-      uint32_t bits = 0;
-      if constexpr (EVEN) {
-        // L % 32 == 0: the tile's 16 pair indices are pbase | (4g + 2hh + ip) with pbase % 16 == 0, so
-        // (pair ^ key) = pk ^ (4g + ip): ONE xor per hash instead of index arithmetic.
-        const uint32_t pk = (((row_idx >> 1) + (uint32_t)kt * 16u) ^ key) ^ (2u * (uint32_t)hh);
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-#pragma unroll
-          for (int ip = 0; ip < 2; ++ip) {
-            const uint32_t hsh = hq_mix24(pk ^ (uint32_t)(4 * g + ip));
-            const int r = 4 * g + 2 * ip;
-            const bool k0 = (hsh & 0xFFFFu) >= thr, k1 = (hsh >> 16) >= thr;
-            sc[r] = k0 ? sc[r] : 0.f;
-            sc[r + 1] = k1 ? sc[r + 1] : 0.f;
-            bits |= ((uint32_t)k0 << r) | ((uint32_t)k1 << (r + 1));
-          }
-      } else {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const uint32_t idx0 = row_idx + kt * 32 + 8 * g + 4 * hh;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const bool k = hq_keep(idx0 + i, key, thr);
-            sc[4 * g + i] = k ? sc[4 * g + i] : 0.f;
-            bits |= (uint32_t)k << (4 * g + i);
-          }
-        }
-      }
-      my_bits[(size_t)kt * 64] = (uint16_t)bits;
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8_t pb = pack_b(sc, s);
-#pragma unroll
-      for (int d = 0; d < 2; ++d) o[d] = mfma32(kVEarly ? vt[s][d] : tr8(sV, kt * 32, lo_, s, d), pb, o[d]);
-    }
-  }
-  const float l_tot = xor32_sum(l2.x + l2.y);
-  const float inv = (DROP ? kscale : 1.f) / l_tot;
-  if (qi < L) {  // lanes q and q+32 share qi: the permlane partners are active together
-    store_row64(ctx + ((size_t)b * L + qi) * H + h * D, o, inv, hh);
-    if (hh == 0) lse[(size_t)bh * L + qi] = (m_run + __builtin_amdgcn_logf(l_tot)) * LN2;  // v_log_f32 = log2
-  }
-}
-
 // ============================================================================ forward v3: LDS-DMA ring
 // The whole-head design above keeps K and V of a head resident (96 KB at L=384), so only ONE workgroup
 // fits a CU and its load prologue and store epilogue never overlap compute: measured 151 of 285 µs at
@@ -750,295 +590,6 @@ __global__ __launch_bounds__(RW * 64, DROP ? 3 : 4) void attn_fwd_ring_kernel(co
   if (qi < L) {  // lanes q and q+32 share qi: the permlane partners are active together
     store_row64(ctx + ((size_t)b * L + qi) * H + h * D, o, inv, hh);
     if (hh == 0) lse[(size_t)bh * L + qi] = (m_b + __builtin_amdgcn_logf(l_tot)) * LN2;  // v_log_f32 = log2
-  }
-}
-
-// ============================================================================ backward: dQ (+ δ)
-template <int NWB, bool DROP, int NT>
-__global__ __launch_bounds__(NWB * 64) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv,
-                                                               const uint16_t* __restrict__ dctx,
-                                                               const uint16_t* __restrict__ ctx,
-                                                               const float* __restrict__ lse,
-                                                               const float* __restrict__ key_bias,
-                                                               const uint16_t* __restrict__ mbits,
-                                                               float* __restrict__ delta, uint16_t* __restrict__ dqkv,
-                                                               int L, int nh, float c_scale, float scale, float kscale) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int UNR = NT > 0 ? NT : 1;
-  const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
-  uint16_t* sK = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* sV = sK + Lp * D;
-  float* sB = reinterpret_cast<float*>(sV + Lp * D);
-  const int H = nh * D, ld = 3 * H;
-  const int bh = blockIdx.x, b = bh / nh, h = bh % nh;
-  HQ_DASSERT(L > 0 && L <= 512);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, hh = lane >> 5;
-  const int qs = blockIdx.y * NWB + wave;
-  const int qi = qs * 32 + (lane & 31);
-  const bool qok = qi < L;
-  const uint16_t* base = qkv + (size_t)b * L * ld + h * D;
-  const size_t orow = ((size_t)b * L + qi) * H + h * D;
-
-  bf16x8_t qf[4], of[4];
-  float dpart = 0.f;
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    qf[s] = qok ? prescale8(*reinterpret_cast<const bf16x8_t*>(base + (size_t)qi * ld + 16 * s + 8 * hh), c_scale)
-                : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-    of[s] = qok ? *reinterpret_cast<const bf16x8_t*>(dctx + orow + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-    if (qok) {
-      float x[8], y[8];
-      hq_unpack8(__builtin_bit_cast(uint4, of[s]), x);
-      hq_unpack8(*reinterpret_cast<const uint4*>(ctx + orow + 16 * s + 8 * hh), y);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dpart += x[j] * y[j];
-    }
-  }
-  // this wave's dropout keep-bit words for all key tiles, staged in LDS with the K/V prologue: loaded
-  // per tile they exposed a full HBM round trip (global load → vmcnt(0)) in every iteration
-  uint16_t* sM = reinterpret_cast<uint16_t*>(sB + Lp) + wave * n32 * 64;
-  constexpr int kMaxT = 16;
-  uint16_t mw[kMaxT];
-  const uint16_t* gbits = mbits + (((size_t)bh * n32 + qs) * n32) * 64 + lane;
-  if constexpr (DROP) {
-#pragma unroll
-    for (int t = 0; t < kMaxT; ++t)
-      if (t < n32 && qs < n32) mw[t] = gbits[(size_t)t * 64];
-  }
-  load_heads2<NWB * 64>(sK, base + H, ld, sV, base + 2 * H, ld, L, Lp);
-  for (int t = threadIdx.x; t < Lp; t += NWB * 64) sB[t] = t < L ? bias_l2(key_bias[(size_t)b * L + t]) : -INFINITY;
-  if constexpr (DROP) {
-#pragma unroll
-    for (int t = 0; t < kMaxT; ++t)
-      if (t < n32 && qs < n32) sM[t * 64 + lane] = mw[t];
-  }
-  const float dlt = xor32_sum(dpart);  // δ = rowsum(dO·O) over all 64 dims
-  const float lq = qok ? lse[(size_t)bh * L + qi] * LOG2E : INFINITY;
-  if (qok && hh == 0) delta[(size_t)bh * L + qi] = dlt;
-  __syncthreads();
-  if (qs * 32 >= L) return;
-  LdsOffsets lo_;
-  lo_.init(lane);
-  wave_prio(wave, NWB);
-
-  f32x16_t dq[2];
-#pragma unroll
-  for (int d = 0; d < 2; ++d)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dq[d][r] = 0.f;
-  const f2_t dl2 = {dlt, dlt};
-#pragma unroll UNR
-  for (int kt = 0; kt < n32; ++kt) {
-    f32x16_t s_acc, p_acc;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {  // S' = c·q·k + bias − lse (log2 domain) straight out of the MFMA
-      const float4 bb = *reinterpret_cast<const float4*>(sB + kt * 32 + 8 * g + 4 * hh);
-      s_acc[4 * g + 0] = bb.x - lq; s_acc[4 * g + 1] = bb.y - lq;
-      s_acc[4 * g + 2] = bb.z - lq; s_acc[4 * g + 3] = bb.w - lq;
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) p_acc[r] = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      s_acc = mfma32(row8(sK, kt * 32, lo_, s), qf[s], s_acc);
-      p_acc = mfma32(row8(sV, kt * 32, lo_, s), of[s], p_acc);
-    }
-    uint32_t bits = 0xFFFFu;
-    float ks = 1.f;
-    if constexpr (DROP) {
-      bits = (uint32_t)sM[kt * 64 + lane];
-      ks = kscale;
-    }
-    float ds[16];
-#pragma unroll
-    for (int r = 0; r < 16; r += 2) {  // dS = P·(dP·mask − δ), two elements per packed FMA / multiply
-      const f2_t P = {__builtin_amdgcn_exp2f(s_acc[r]), __builtin_amdgcn_exp2f(s_acc[r + 1])};
-      const f2_t mk = {((bits >> r) & 1u) ? ks : 0.f, ((bits >> (r + 1)) & 1u) ? ks : 0.f};
-      const f2_t dp = {p_acc[r], p_acc[r + 1]};
-      const f2_t v = (dp * mk - dl2) * P;
-      ds[r] = v.x; ds[r + 1] = v.y;
-    }
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8_t sb = pack_b(ds, s);
-#pragma unroll
-      for (int d = 0; d < 2; ++d) dq[d] = mfma32(tr8(sK, kt * 32, lo_, s, d), sb, dq[d]);
-    }
-  }
-  if (qok) store_row64(dqkv + ((size_t)b * L + qi) * ld + h * D, dq, scale, hh);
-}
-
-// ============================================================================ backward: dK, dV
-template <int NWB, bool DROP, int NT>
-__global__ __launch_bounds__(NWB * 64) void attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv,
-                                                                 const uint16_t* __restrict__ dctx,
-                                                                 const float* __restrict__ lse,
-                                                                 const float* __restrict__ delta,
-                                                                 const float* __restrict__ key_bias,
-                                                                 const uint16_t* __restrict__ mbits,
-                                                                 uint16_t* __restrict__ dqkv, int L, int nh,
-                                                                 float c_scale, float scale, float kscale) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int UNR = NT > 0 ? (NWB >= 12 ? 4 : NT) : 1;  // full unroll spills at 12 waves
-  const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
-  uint16_t* sQ = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* sO = sQ + Lp * D;  // dO
-  float* sL = reinterpret_cast<float*>(sO + Lp * D);  // lse·log2e (+inf past L)
-  float* sD = sL + Lp;                                // δ
-  const int H = nh * D, ld = 3 * H;
-  const int bh = blockIdx.x, b = bh / nh, h = bh % nh;
-  HQ_DASSERT(L > 0 && L <= 512 && (NT == 0 || L == NT * 32));
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, hh = lane >> 5;
-  // this wave's keep-bit words of every query tile, [tile][64], staged in LDS by the prologue
-  uint16_t* sW = reinterpret_cast<uint16_t*>(sD + Lp) + wave * n32 * 64;
-  const int ks_idx = blockIdx.y * NWB + wave;  // 32-key subtile
-  const int kj = ks_idx * 32 + (lane & 31);
-  const bool kok = kj < L;
-  const uint16_t* base = qkv + (size_t)b * L * ld + h * D;
-
-  bf16x8_t kf[4], vf[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    kf[s] = kok ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)kj * ld + H + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-    vf[s] = kok ? *reinterpret_cast<const bf16x8_t*>(base + (size_t)kj * ld + 2 * H + 16 * s + 8 * hh) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
-  }
-  const float kb = kok ? bias_l2(key_bias[(size_t)b * L + kj]) : -INFINITY;
-  constexpr int kMaxT = 16;
-  uint16_t mw[kMaxT];
-  if constexpr (DROP) {
-#pragma unroll
-    for (int t = 0; t < kMaxT; ++t)
-      if (t < n32 && ks_idx < n32) mw[t] = mbits[(((size_t)bh * n32 + t) * n32 + ks_idx) * 64 + lane];
-  }
-  // Q·c (exactly as the forward's) and dO
-  load_heads2<NWB * 64, true>(sQ, base, ld, sO, dctx + (size_t)b * L * H + h * D, H, L, Lp, c_scale);
-  for (int t = threadIdx.x; t < Lp; t += NWB * 64) {
-    sL[t] = t < L ? lse[(size_t)bh * L + t] * LOG2E : INFINITY;
-    sD[t] = t < L ? delta[(size_t)bh * L + t] : 0.f;
-  }
-  if constexpr (DROP) {
-#pragma unroll
-    for (int t = 0; t < kMaxT; ++t)
-      if (t < n32 && ks_idx < n32) sW[t * 64 + lane] = mw[t];
-  }
-  __syncthreads();
-  if (ks_idx * 32 >= L) return;
-  LdsOffsets lo_;
-  lo_.init(lane);
-  wave_prio(wave, NWB);
-
-  // Two passes over the queries (dV, then dK with S recomputed): +25 % MFMA, but the live set of a
-  // single pass (K/V fragments + dV/dK accumulators + S/dP tiles ≈ 200 VGPRs) spills at the 168-VGPR
-  // budget of 12 waves per workgroup.
-  // Forward bit layout: the word of fwd-lane l' = q + 32·hh' holds bit r' for key acc_row(r', hh').  This
-  // lane (key krel) needs, for its 16 query rows acc_row(r, hh) = 8g + 4hh + i, bit r_f of the words of
-  // fwd-lanes 8g + 4hh + i + 32·hh_f: four consecutive words per g, i.e. one 8-byte LDS read per g.
-  const int krel = lane & 31;
-  const int hh_f = (krel >> 2) & 1;
-  const int r_f = (krel & 3) + 4 * (krel >> 3);
-  const float ksc = DROP ? kscale : 1.f;
-  auto tile_mask = [&](int qt, f2_t* mk) {  // mk[r/2] = {mask(r), mask(r+1)} ∈ {0, 1/(1-p)}
-    if constexpr (DROP) {
-      const uint16_t* wsrc = sW + qt * 64 + 4 * hh + 32 * hh_f;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint64_t w = *reinterpret_cast<const uint64_t*>(wsrc + 8 * g);
-        const uint32_t lo = (uint32_t)w >> r_f, hi = (uint32_t)(w >> 32) >> r_f;
-        mk[2 * g] = f2_t{(lo & 1u) ? ksc : 0.f, ((lo >> 16) & 1u) ? ksc : 0.f};
-        mk[2 * g + 1] = f2_t{(hi & 1u) ? ksc : 0.f, ((hi >> 16) & 1u) ? ksc : 0.f};
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) mk[i] = f2_t{1.f, 1.f};
-    }
-  };
-  const f2_t kb2 = {kb, kb};
-  auto score_init = [&](int qt, f32x16_t& s_acc) {  // S' = c·q·k + bias − lse (key on the lane)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const float4 l4 = *reinterpret_cast<const float4*>(sL + qt * 32 + 8 * g + 4 * hh);
-      const f2_t a = kb2 - f2_t{l4.x, l4.y}, c = kb2 - f2_t{l4.z, l4.w};
-      s_acc[4 * g + 0] = a.x; s_acc[4 * g + 1] = a.y; s_acc[4 * g + 2] = c.x; s_acc[4 * g + 3] = c.y;
-    }
-  };
-  uint16_t* out = dqkv + ((size_t)b * L + min(kj, L - 1)) * ld + h * D;
-
-  // ------------------------------------------------------------------ pass 1: dVᵀ += dOᵀ·Pd
-  {
-    f32x16_t dv[2];
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dv[d][r] = 0.f;
-#pragma unroll UNR
-    for (int qt = 0; qt < n32; ++qt) {
-      f32x16_t s_acc;
-      score_init(qt, s_acc);
-#pragma unroll
-      for (int s = 0; s < 4; ++s) s_acc = mfma32(row8(sQ, qt * 32, lo_, s), kf[s], s_acc);
-      f2_t mk[8];
-      tile_mask(qt, mk);
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        float pd[8];
-#pragma unroll
-        for (int j = 0; j < 8; j += 2) {
-          const int r = 8 * s + j;
-          const f2_t P = {__builtin_amdgcn_exp2f(s_acc[r]), __builtin_amdgcn_exp2f(s_acc[r + 1])};
-          const f2_t v = P * mk[r >> 1];
-          pd[j] = v.x; pd[j + 1] = v.y;
-        }
-        const bf16x8_t pb = pack_b(pd, 0);
-#pragma unroll
-        for (int d = 0; d < 2; ++d) dv[d] = mfma32(tr8(sO, qt * 32, lo_, s, d), pb, dv[d]);
-      }
-    }
-    if (kok) store_row64(out + 2 * H, dv, 1.f, hh);
-  }
-  // ------------------------------------------------------------------ pass 2: dKᵀ += Qᵀ·dS
-  {
-    f32x16_t dk[2];
-#pragma unroll
-    for (int d = 0; d < 2; ++d)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) dk[d][r] = 0.f;
-#pragma unroll UNR
-    for (int qt = 0; qt < n32; ++qt) {
-      f32x16_t s_acc, p_acc;
-      score_init(qt, s_acc);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) p_acc[r] = 0.f;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        s_acc = mfma32(row8(sQ, qt * 32, lo_, s), kf[s], s_acc);
-        p_acc = mfma32(row8(sO, qt * 32, lo_, s), vf[s], p_acc);
-      }
-      f2_t mk[8];
-      tile_mask(qt, mk);
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        float ds[8];
-#pragma unroll
-        for (int gg = 0; gg < 2; ++gg) {
-          const int g = 2 * s + gg;
-          const float4 d4 = *reinterpret_cast<const float4*>(sD + qt * 32 + 8 * g + 4 * hh);
-          const f2_t dl[2] = {f2_t{d4.x, d4.y}, f2_t{d4.z, d4.w}};
-#pragma unroll
-          for (int i = 0; i < 4; i += 2) {
-            const int r = 4 * g + i;
-            const f2_t P = {__builtin_amdgcn_exp2f(s_acc[r]), __builtin_amdgcn_exp2f(s_acc[r + 1])};
-            const f2_t dp = {p_acc[r], p_acc[r + 1]};
-            const f2_t v = (dp * mk[r >> 1] - dl[i >> 1]) * P;
-            ds[4 * gg + i] = v.x; ds[4 * gg + i + 1] = v.y;
-          }
-        }
-        const bf16x8_t sb = pack_b(ds, 0);
-#pragma unroll
-        for (int d = 0; d < 2; ++d) dk[d] = mfma32(tr8(sQ, qt * 32, lo_, s, d), sb, dk[d]);
-      }
-    }
-    // sQ holds Q·c (c = scale·log2e): dK = scale·Σ dS·q = Σ dS·(q·c) / log2e
-    if (kok) store_row64(out + H, dk, LN2, hh);
   }
 }
 
@@ -1390,274 +941,6 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
   }
 }
 
-// ============================================================================ backward v4: fused
-// One workgroup per (batch, head) for L <= 32·NW (NW <= 12): wave w owns keys 32w … 32w+31 for the whole
-// query sweep, so dK / dV stay in its registers (as in the v3 dK/dV kernel) AND the dQ of every 32-query
-// tile is summed over the workgroup's waves in LDS.  S, dP and the softmax / dropout work are therefore
-// computed ONCE per (query tile, key subtile) — v3 recomputes them in its separate dQ kernel (7 MFMA
-// units per tile pair instead of 5).  Per wave and query tile: S (4 + 1 aug MFMA: bias, −LSE), dP (4),
-// dVᵀ += dOᵀ·(P∘mask) (4), dKᵀ += Q'ᵀ·dS (4), dQ += dS·K (4: dS goes through a per-wave LDS image [key][q]
-// so that ds_read_b64_tr_b16 puts the keys on the MFMA K axis, K comes from the wave's LDS image the same
-// way), then 32 ds_add_f32 per lane into the tile's fp32 dQ accumulator — double-buffered and flushed as
-// bf16 by the first 256 threads during the next tile.  δ = rowsum(dO·O) is formed in the staging pass.
-// K and V of every wave live in LDS (register fragments would spill at 3 waves/SIMD); two waves share one
-// [32][64] dSᵀ image (32 query columns each).  LDS (NW = 12): 2 staging slots 20 KB + K / V images 96 KB
-// + dSᵀ images 24 KB + dQ accumulators 18 KB = 158 KB.
-constexpr int kDqStride = 72;   // fp32 row stride of the dQ accumulator: lanes q and q+4 land 32 banks apart
-
-template <bool DROP, int NW>
-__global__ __launch_bounds__(NW * 64, 1) void attn_bwd_fused_kernel(
-    const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dctx, const uint16_t* __restrict__ ctx,
-    const float* __restrict__ lse, const float* __restrict__ key_bias, const uint16_t* __restrict__ mbits,
-    uint16_t* __restrict__ dqkv, int L, int nh, float c_scale, float scale, float kscale, int dbg) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // slot: Q' [32][64] 4 KB | dO [32][64] 4 KB | A' words [32] uint4 512 B | δ [32] f32 128 B | bits [NW][64] u16
-  constexpr int SLOT = 2 * RTILE + 512 + 128 + NW * 128;
-  char* slots = reinterpret_cast<char*>(smem);
-  uint16_t* kimg = reinterpret_cast<uint16_t*>(slots + 2 * SLOT);  // [NW][32][64] K rows of each wave's keys
-  uint16_t* vimg = kimg + NW * 32 * D;                             // [NW][32][64] V rows
-  uint16_t* dsimg = vimg + NW * 32 * D;                            // [NW/2][32][64] dSᵀ: key rows, a wave pair's
-  float* dqacc = reinterpret_cast<float*>(dsimg + NW / 2 * 32 * D);  // query columns side by side; dQ fp32 [2][32][kDqStride]
-  const int Lp = (L + 31) & ~31, n32 = Lp >> 5;
-  const int nblk = gridDim.x, ob = blockIdx.x, xcd = ob & 7, qq = nblk >> 3, rr = nblk & 7;
-  const int bh = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (ob >> 3);
-  const int b = bh / nh, h = bh - b * nh;
-  const int H = nh * D, ld = 3 * H;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63, hh = lane >> 5;
-  const int tid = threadIdx.x;
-  const int kj = wave * 32 + (lane & 31);
-  const bool active = wave * 32 < L;
-  const bool kok = kj < L;
-  const uint16_t* base = qkv + (size_t)b * L * ld + h * D;
-  HQ_DASSERT(L > 0 && n32 <= NW);
-
-  // ---- prologue: this wave's K and V rows into its LDS images
-  const int kr = kok ? kj : L - 1;
-  uint16_t* tK = kimg + wave * 32 * D;
-  uint16_t* tV = vimg + wave * 32 * D;
-  uint16_t* tS = dsimg + (wave >> 1) * 32 * D;
-  const int scol = 32 * (wave & 1);   // this wave's query columns in the shared dSᵀ image
-  {
-    bf16x8_t kf[4], vv[4];
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kf[s] = *reinterpret_cast<const bf16x8_t*>(base + (size_t)kr * ld + H + 16 * s + 8 * hh);
-      vv[s] = *reinterpret_cast<const bf16x8_t*>(base + (size_t)kr * ld + 2 * H + 16 * s + 8 * hh);
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      *reinterpret_cast<bf16x8_t*>(tK + lds_off(lane & 31, 16 * s + 8 * hh)) = kf[s];
-      *reinterpret_cast<bf16x8_t*>(tV + lds_off(lane & 31, 16 * s + 8 * hh)) = vv[s];
-    }
-  }
-  typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
-  bf16x8_t kaug;
-  {
-    const float bl = kok ? key_bias[(size_t)b * L + kj] * LOG2E : -1e30f;
-    const uint16_t bhi = bf16_rne(bl), blo = kok ? bf16_rne(bl - hq_bf2f(bhi)) : 0;
-    const u32x4 w = hh ? u32x4{0u, 0u, 0u, 0u}
-                       : u32x4{0x3F803F80u, 0x3F80u | ((uint32_t)bhi << 16), (uint32_t)blo, 0u};
-    kaug = __builtin_bit_cast(bf16x8_t, w);
-  }
-  for (int i = tid; i < 2 * 32 * kDqStride; i += NW * 64) dqacc[i] = 0.f;
-
-  // ---- staging of query tile t by the first 256 threads (row tid>>3, 16-B chunk tid&7 of Q, dO and O;
-  // every thread issues the loads, rows folded mod 32, so no load is exec-masked): one register set,
-  // issued a full tile ahead of its commit
-  const int srow = (tid >> 3) & 31, schunk = tid & 7;
-  struct Stage {
-    uint4 q, o, c;
-    float l;
-    uint16_t bits;
-  };
-  auto issue = [&](int t, Stage& st) {
-    int u = tid;                      // laundered: per-lane addresses rebuilt here, not hoisted and spilled
-    asm volatile("" : "+v"(u));
-    const int q = min(t * 32 + ((u >> 3) & 31), L - 1), ch = u & 7;
-    const size_t orow = ((size_t)b * L + q) * H + h * D + ch * 8;
-    st.q = *reinterpret_cast<const uint4*>(base + (size_t)q * ld + ch * 8);
-    st.o = *reinterpret_cast<const uint4*>(dctx + orow);
-    st.c = *reinterpret_cast<const uint4*>(ctx + orow);
-    const int ql = t * 32 + (u & 31);
-    st.l = lse[(size_t)bh * L + min(ql, L - 1)];
-    if (ql >= L) st.l = 1e30f;   // queries past L: P = 0 (finite: split3)
-    st.bits = 0;
-    if constexpr (DROP) st.bits = mbits[(((size_t)bh * n32 + t) * n32 + min(wave, n32 - 1)) * 64 + lane];
-  };
-  auto commit = [&](int t, const Stage& st) {
-    char* slot = slots + (t & 1) * SLOT;
-    if (tid < 256) {   // waves 0-3: whole waves, so the shuffles below see full rows
-      uint16_t* sq = reinterpret_cast<uint16_t*>(slot);
-      uint16_t* so = sq + 32 * D;
-      float f[8], g[8];
-      hq_unpack8(st.q, f);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] *= c_scale;     // Q·c rounded exactly as the forward's prescale8
-      *reinterpret_cast<uint4*>(sq + lds_off(srow, schunk * 8)) = hq_pack8(f);
-      *reinterpret_cast<uint4*>(so + lds_off(srow, schunk * 8)) = st.o;
-      hq_unpack8(st.o, f);
-      hq_unpack8(st.c, g);
-      float d = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) d = fmaf(f[j], g[j], d);
-      d += __shfl_xor(d, 1, 64);
-      d += __shfl_xor(d, 2, 64);
-      d += __shfl_xor(d, 4, 64);
-      if (schunk == 0) reinterpret_cast<float*>(slot + 2 * RTILE + 512)[srow] = d;   // δ of query srow
-      if (tid < 32) {
-        uint16_t lh, lm, ll;
-        split3(-st.l * LOG2E, lh, lm, ll);
-        reinterpret_cast<uint4*>(slot + 2 * RTILE)[tid] =
-            make_uint4((uint32_t)lh | ((uint32_t)lm << 16), (uint32_t)ll | (0x3F80u << 16), 0x3F80u, 0u);
-      }
-    }
-    if constexpr (DROP) reinterpret_cast<uint16_t*>(slot + 2 * RTILE + 640)[wave * 64 + lane] = st.bits;
-  };
-  // dQ of query tile t (complete: every wave's adds precede the barrier that ended its iteration) -> bf16
-  auto flush = [&](int t) {
-    if (tid < 256) {
-      float* acc = dqacc + (t & 1) * 32 * kDqStride + srow * kDqStride + schunk * 8;
-      const float4 a = *reinterpret_cast<const float4*>(acc), c = *reinterpret_cast<const float4*>(acc + 4);
-      const float v[8] = {a.x * scale, a.y * scale, a.z * scale, a.w * scale,
-                          c.x * scale, c.y * scale, c.z * scale, c.w * scale};
-      const int q = t * 32 + srow;
-      if (q < L) *reinterpret_cast<uint4*>(dqkv + ((size_t)b * L + q) * ld + h * D + schunk * 8) = hq_pack8(v);
-      *reinterpret_cast<float4*>(acc) = make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(acc + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-
-  Stage st;
-  issue(0, st);
-  commit(0, st);
-  if (n32 > 1) issue(1, st);
-  __syncthreads();
-
-  const f32x16_t zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  f32x16_t dv[2] = {zero16, zero16}, dk[2] = {zero16, zero16};
-  const int krel = lane & 31;
-  const int hh_f = (krel >> 2) & 1;
-  const int r_f = (krel & 3) + 4 * (krel >> 3);
-  const float ksc = DROP ? kscale : 1.f;
-  for (int t = 0; t < n32; ++t) {
-    // fragment offsets recomputed per iteration from a laundered lane id (3 VALU each): without the
-    // launder the compiler hoists ~20 lane-constant LDS offsets out of the loop and, at 3 waves/SIMD
-    // (168-VGPR budget), spills them to scratch — each reload a vmcnt(0) wait behind the staged loads
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    auto R8 = [&](const uint16_t* tile, int s) { return lds_row8(tile, ln & 31, 16 * s + 8 * (ln >> 5)); };
-    auto T8 = [&](const uint16_t* tile, int s, int d) { return lds_tr8(tile, 0, s, d, ln); };
-    const char* slot = slots + (t & 1) * SLOT;
-    const uint16_t* tq = reinterpret_cast<const uint16_t*>(slot);
-    const uint16_t* to = tq + 32 * D;
-    if (t > 0) flush(t - 1);
-    if (active) {
-      const uint4 aw = reinterpret_cast<const uint4*>(slot + 2 * RTILE)[hh ? 0 : krel];
-      const bf16x8_t qa = hh ? bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0} : __builtin_bit_cast(bf16x8_t, u32x4{aw.x, aw.y, aw.z, aw.w});
-      f32x16_t s_acc = mfma32(R8(tq, 0), R8(tK, 0), zero16);
-#pragma unroll
-      for (int s = 1; s < 4; ++s) s_acc = mfma32(R8(tq, s), R8(tK, s), s_acc);
-      s_acc = mfma32(qa, kaug, s_acc);                   // S' = c·q·k + bias_k − lse_q (log2 domain)
-      f32x16_t p_acc = mfma32(R8(to, 0), R8(tV, 0), zero16);
-#pragma unroll
-      for (int s = 1; s < 4; ++s) p_acc = mfma32(R8(to, s), R8(tV, s), p_acc);
-      const uint16_t* wsrc = reinterpret_cast<const uint16_t*>(slot + 2 * RTILE + 640) + wave * 64 + 4 * hh + 32 * hh_f;
-      const float* sdl = reinterpret_cast<const float*>(slot + 2 * RTILE + 512);
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        float pd[8], dsv[8];
-#pragma unroll
-        for (int gg = 0; gg < 2; ++gg) {
-          const int g = 2 * s + gg;
-          uint32_t lo = 0xFFFFFFFFu, hi = 0xFFFFFFFFu;
-          if constexpr (DROP) {
-            const uint64_t w = *reinterpret_cast<const uint64_t*>(wsrc + 8 * g);
-            lo = (uint32_t)w >> r_f;
-            hi = (uint32_t)(w >> 32) >> r_f;
-          }
-          const float4 d4 = *reinterpret_cast<const float4*>(sdl + 8 * g + 4 * hh);
-          const float mk[4] = {(lo & 1u) ? ksc : 0.f, ((lo >> 16) & 1u) ? ksc : 0.f, (hi & 1u) ? ksc : 0.f,
-                               ((hi >> 16) & 1u) ? ksc : 0.f};
-          const float dl[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int r = 4 * g + i;
-            const float P = __builtin_amdgcn_exp2f(s_acc[r]);
-            pd[4 * gg + i] = P * mk[i];
-            dsv[4 * gg + i] = (p_acc[r] * mk[i] - dl[i]) * P;
-          }
-          // dSᵀ image: key row krel, query columns 16s + 8gg + 4hh … +3 (one 8-byte store)
-          *reinterpret_cast<uint2*>(tS + lds_off(krel, scol + 16 * s + 8 * gg + 4 * hh)) =
-              make_uint2(hq_pack2(dsv[4 * gg], dsv[4 * gg + 1]), hq_pack2(dsv[4 * gg + 2], dsv[4 * gg + 3]));
-        }
-        const bf16x8_t pb = pack_b(pd, 0), sb = pack_b(dsv, 0);
-#pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          dv[d] = mfma32(T8(to, s, d), pb, dv[d]);
-          dk[d] = mfma32(T8(tq, s, d), sb, dk[d]);
-        }
-      }
-      // dQ (queries on the rows, head dims on the lanes) = Σ_keys dS·K, keys on the MFMA K axis via the
-      // transposed reads of the dSᵀ and K images (same key order on both operands)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      float* accb = dqacc + (t & 1) * 32 * kDqStride;
-#pragma unroll
-      for (int d = 0; d < 2; ++d) {   // one 32-column half at a time: 16 accumulator registers live
-        f32x16_t dq = mfma32(T8(tS, 0, wave & 1), T8(tK, 0, d), zero16);
-        dq = mfma32(T8(tS, 1, wave & 1), T8(tK, 1, d), dq);
-        if (dbg & 1) {   // timing experiment only (wrong dQ): plain stores instead of LDS atomics
-#pragma unroll
-          for (int r = 0; r < 16; ++r) accb[acc_row(r, hh) * kDqStride + d * 32 + krel] = dq[r];
-        } else if (!(dbg & 2)) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) atomicAdd(accb + acc_row(r, hh) * kDqStride + d * 32 + krel, dq[r]);
-        }
-      }
-    }
-    if (t + 1 < n32) {
-      commit(t + 1, st);   // slot (t+1)&1: last read in iteration t-1, before the barrier that ended it
-      __syncthreads();
-      if (t + 2 < n32) issue(t + 2, st);
-    } else {
-      __syncthreads();
-    }
-  }
-  flush(n32 - 1);
-  if (active && kok) {
-    uint16_t* out = dqkv + ((size_t)b * L + kj) * ld + h * D;
-    store_row64(out + 2 * H, dv, 1.f, hh);
-    store_row64(out + H, dk, LN2, hh);                   // Q' = c·Q with c = scale·log2e: dK = Σ dS·Q'/log2e
-  }
-}
-
-// waves per workgroup for a sequence of L: all 32-row subtiles of a head in one workgroup up to
-// 12 waves (L <= 384: 3 waves/SIMD), else 8 waves with the head split over grid.y.
-int waves_for(int L) {
-  const int n32 = (L + 31) / 32;
-  return n32 <= 12 ? n32 : 8;
-}
-
-template <template <int> class K, typename F>
-void dispatch_waves(int nw, F&& f) {
-  switch (nw) {
-    case 1: f(std::integral_constant<int, 1>{}); break;
-    case 2: f(std::integral_constant<int, 2>{}); break;
-    case 3: f(std::integral_constant<int, 3>{}); break;
-    case 4: f(std::integral_constant<int, 4>{}); break;
-    case 5: f(std::integral_constant<int, 5>{}); break;
-    case 6: f(std::integral_constant<int, 6>{}); break;
-    case 7: f(std::integral_constant<int, 7>{}); break;
-    case 8: f(std::integral_constant<int, 8>{}); break;
-    case 9: f(std::integral_constant<int, 9>{}); break;
-    case 10: f(std::integral_constant<int, 10>{}); break;
-    case 11: f(std::integral_constant<int, 11>{}); break;
-    case 12: f(std::integral_constant<int, 12>{}); break;
-    default: fprintf(stderr, "hq attention: bad wave count %d\n", nw); abort();
-  }
-}
-
-template <int N> struct FwdTag {};
-
 }  // namespace
 
 size_t hq_attn_mask_bytes(int B, int L, int nh) {
@@ -1680,31 +963,27 @@ static void set_attn_prio() {
   (void)once;
 }
 
-static int attn_fwd_variant() {  // read per call: tools/attn_bench.py A/Bs the variants in one process
-  const char* e = getenv("HQ_ATTN_FWD");
-  return e ? atoi(e) : 3;
-}
-
-static int attn_force_slow() {  // tests: HQ_ATTN_FORCE_SLOW=1 sends every workgroup down the slow path
+// HQ_ATTN_FORCE_SLOW=1 / attn_set_force_slow(1): every workgroup of the ring forward takes its slow path
+// (tests only: the rare rescale branch gets its own coverage, kernel playbook rule 26)
+static int g_attn_force_slow = [] {
   const char* e = getenv("HQ_ATTN_FORCE_SLOW");
   return e && atoi(e) ? 1 : 0;
-}
+}();
+void hq_attn_set_force_slow(int v) { g_attn_force_slow = v ? 1 : 0; }
 
 void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, float* lse, uint16_t* mbits, int B, int L,
                  int nh, int dh, float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s, uint8_t* ctx8,
                  float* q8, int phase) {
   set_attn_prio();
   if (dh != D || L > 512) { fprintf(stderr, "hq_attn_fwd: head_dim %d / L %d unsupported\n", dh, L); abort(); }
-  if (ctx8 && attn_fwd_variant() != 3) { fprintf(stderr, "hq_attn_fwd: e4m3 ctx needs the ring forward (v3)\n"); abort(); }
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const HqDropKey key = hq_drop_key(seed, opid);
-  const int Lp = (L + 31) & ~31, n32 = Lp / 32;
-  if (attn_fwd_variant() == 3) {
+  const int Lp = (L + 31) & ~31;
+  {
     const int n_qb = (L + RQ - 1) / RQ;
-    const int force_slow = attn_force_slow();
-    const char* ea = getenv("HQ_ATTN_AHEAD");
-    const int ahead = ea ? atoi(ea) : 2;
-    const size_t lds = (size_t)(ahead == 2 ? 4 : 6) * 2 * RTILE + Lp * sizeof(uint2);
+    const int force_slow = g_attn_force_slow;
+    constexpr int ahead = 2;   // K/V tiles in flight (4-deep measured slower: profiles/r2_attn)
+    const size_t lds = (size_t)4 * 2 * RTILE + Lp * sizeof(uint2);
     const int nparts = B * nh * n_qb * RW;
     float* part8 = ctx8 ? hq_fp8_amax_parts((size_t)nparts) : nullptr;
     auto run = [&](auto cn) {
@@ -1717,17 +996,17 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
                            thr ? mbits : nullptr, L, nh, n_qb, scale * LOG2E, key, thr, hq_keep_scale(thr), force_slow,
                            ctx8, q8, part8, phase);
       };
-      auto launch = [&](auto k2, auto k4) { if (ahead == 2) launch1(k2); else launch1(k4); };
+      (void)ahead;
       // EVEN (L % 32 == 0) also selects the unclamped DMA addressing: never pass it for a ragged L
       // (NT > 0 implies L = 32·NT, so the ragged variants exist only for the rolled NT = 0 loop)
       if constexpr (NT > 0) {
-        if (!thr) launch(attn_fwd_ring_kernel<false, true, NT, 2>, attn_fwd_ring_kernel<false, true, NT, 4>);
-        else launch(attn_fwd_ring_kernel<true, true, NT, 2>, attn_fwd_ring_kernel<true, true, NT, 4>);
+        if (!thr) launch1(attn_fwd_ring_kernel<false, true, NT, 2>);
+        else launch1(attn_fwd_ring_kernel<true, true, NT, 2>);
       } else {
-        if (!thr && (L & 31) == 0) launch(attn_fwd_ring_kernel<false, true, 0, 2>, attn_fwd_ring_kernel<false, true, 0, 4>);
-        else if (!thr) launch(attn_fwd_ring_kernel<false, false, 0, 2>, attn_fwd_ring_kernel<false, false, 0, 4>);
-        else if ((L & 31) == 0) launch(attn_fwd_ring_kernel<true, true, 0, 2>, attn_fwd_ring_kernel<true, true, 0, 4>);
-        else launch(attn_fwd_ring_kernel<true, false, 0, 2>, attn_fwd_ring_kernel<true, false, 0, 4>);
+        if (!thr && (L & 31) == 0) launch1(attn_fwd_ring_kernel<false, true, 0, 2>);
+        else if (!thr) launch1(attn_fwd_ring_kernel<false, false, 0, 2>);
+        else if ((L & 31) == 0) launch1(attn_fwd_ring_kernel<true, true, 0, 2>);
+        else launch1(attn_fwd_ring_kernel<true, false, 0, 2>);
       }
     };
     if (L == 384) run(std::integral_constant<int, 12>{});
@@ -1736,30 +1015,7 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
     else if (L == 128) run(std::integral_constant<int, 4>{});
     else run(std::integral_constant<int, 0>{});
     if (ctx8) hq_fp8_amax_fold(part8, nparts, q8, phase, s);
-    return;
   }
-  const int nw = waves_for(L);
-  const size_t lds = (size_t)Lp * D * 2 * 2 + Lp * sizeof(float);
-  auto run = [&](auto cw, auto cn) {
-    constexpr int NW = decltype(cw)::value, NT = decltype(cn)::value;
-    auto launch = [&](auto kern) {
-      static bool attr =
-          (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess);
-      (void)attr;
-      hipLaunchKernelGGL(kern, dim3(B * nh, (n32 + NW - 1) / NW), dim3(NW * 64), lds, s, qkv, key_bias, ctx, lse,
-                         thr ? mbits : nullptr, L, nh, scale * LOG2E, key, thr, hq_keep_scale(thr));
-    };
-    if (!thr) launch(attn_fwd_kernel<NW, false, true, NT>);
-    else if constexpr (NT > 0) launch(attn_fwd_kernel<NW, true, true, NT>);  // L = 32·NT is always even
-    else if ((L & 31) == 0) launch(attn_fwd_kernel<NW, true, true, NT>);
-    else launch(attn_fwd_kernel<NW, true, false, NT>);
-  };
-  // unrolled specialisations for L = 128 / 256 / 384 / 512, rolled loop otherwise
-  if (L == 384) run(std::integral_constant<int, 12>{}, std::integral_constant<int, 12>{});
-  else if (L == 512) run(std::integral_constant<int, 8>{}, std::integral_constant<int, 16>{});
-  else if (L == 256) run(std::integral_constant<int, 8>{}, std::integral_constant<int, 8>{});
-  else if (L == 128) run(std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{});
-  else dispatch_waves<FwdTag>(nw, [&](auto c) { run(c, std::integral_constant<int, 0>{}); });
 }
 
 void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx, const float* lse, const float* key_bias,
@@ -1771,36 +1027,8 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
   const float ks = hq_keep_scale(thr);
   const uint16_t* bits = thr ? mbits : nullptr;
   const int Lp = (L + 31) & ~31, n32 = Lp / 32;
-  const char* ev = getenv("HQ_ATTN_BWD");
-  const int variant = ev ? atoi(ev) : 3;
-  // v4 fused (opt-in, HQ_ATTN_BWD=4): one workgroup per (batch, head); its dQ sums the waves' key slices
-  // with LDS float atomics, so the summation order (last bits of dQ) varies run to run -> deterministic
-  // mode takes the two-kernel path.  Measured at B=256 L=384 (profiles/r2_attn): 4.9 ms, of which 4.3 ms
-  // are the ds_add_f32 (≈190 clk per 64-lane instruction); with the adds replaced by plain stores 595 /
-  // 655 µs (p = 0 / 0.1) vs v3 668-745 µs, so the design's ceiling is small and v3 stays the default.
-  if (variant == 4 && n32 <= 12 && !deterministic) {
-    auto run = [&](auto cw) {
-      constexpr int NW = decltype(cw)::value;
-      const size_t lds = 2 * (size_t)(2 * RTILE + 512 + 128 + NW * 128) + (2 * (size_t)NW + NW / 2) * 32 * D * 2 +
-                         2 * 32 * kDqStride * sizeof(float);
-      auto launch = [&](auto kern) {
-        static bool attr =
-            (hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess);
-        (void)attr;
-        const char* ed = getenv("HQ_ATTN_FUSED_DBG");   // timing experiments (tools/attn_bench.py)
-        hipLaunchKernelGGL(kern, dim3(B * nh), dim3(NW * 64), lds, s, qkv, dctx, ctx, lse, key_bias, bits, dqkv, L, nh,
-                           scale * LOG2E, scale, ks, ed ? atoi(ed) : 0);
-      };
-      if (bits) launch(attn_bwd_fused_kernel<true, NW>);
-      else launch(attn_bwd_fused_kernel<false, NW>);
-    };
-    if (n32 <= 4) run(std::integral_constant<int, 4>{});
-    else if (n32 <= 8) run(std::integral_constant<int, 8>{});
-    else run(std::integral_constant<int, 12>{});
-    (void)delta;
-    return;
-  }
-  if (variant >= 3) {
+  (void)deterministic;   // both backward kernels are deterministic (no atomics)
+  {
     const int nb = (L + RQ - 1) / RQ;                 // 128-row blocks (queries for dQ, keys for dK/dV)
     constexpr int AH = 3;
     const size_t lds_dq = (size_t)(AH + 2) * 2 * RTILE + Lp * sizeof(uint4) + (bits ? (size_t)RW * n32 * 128 : 0);
@@ -1824,31 +1052,5 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
     else if (L == 256) run(std::integral_constant<int, 8>{});
     else if (L == 128) run(std::integral_constant<int, 4>{});
     else run(std::integral_constant<int, 0>{});
-    return;
   }
-  const int nw = waves_for(L);
-  const size_t lds_bits = bits ? (size_t)nw * n32 * 64 * sizeof(uint16_t) : 0;  // staged keep-bit words
-  const size_t lds_dq = (size_t)Lp * D * 2 * 2 + Lp * sizeof(float) + lds_bits;
-  const size_t lds_kv = (size_t)Lp * D * 2 * 2 + 2 * Lp * sizeof(float) + lds_bits;
-  auto run = [&](auto cw, auto cn) {
-    constexpr int NW = decltype(cw)::value, NT = decltype(cn)::value;
-    const dim3 grid(B * nh, (n32 + NW - 1) / NW);
-    auto launch = [&](auto kdq, auto kkv) {
-      static bool attr =
-          (hipFuncSetAttribute((const void*)kdq, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess) &&
-          (hipFuncSetAttribute((const void*)kkv, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess);
-      (void)attr;
-      hipLaunchKernelGGL(kdq, grid, dim3(NW * 64), lds_dq, s, qkv, dctx, ctx, lse, key_bias, bits, delta, dqkv, L, nh,
-                         scale * LOG2E, scale, ks);
-      hipLaunchKernelGGL(kkv, grid, dim3(NW * 64), lds_kv, s, qkv, dctx, lse, delta, key_bias, bits, dqkv, L, nh,
-                         scale * LOG2E, scale, ks);
-    };
-    if (bits) launch(attn_bwd_dq_kernel<NW, true, NT>, attn_bwd_dkdv_kernel<NW, true, NT>);
-    else launch(attn_bwd_dq_kernel<NW, false, NT>, attn_bwd_dkdv_kernel<NW, false, NT>);
-  };
-  if (L == 384) run(std::integral_constant<int, 12>{}, std::integral_constant<int, 12>{});
-  else if (L == 512) run(std::integral_constant<int, 8>{}, std::integral_constant<int, 16>{});
-  else if (L == 256) run(std::integral_constant<int, 8>{}, std::integral_constant<int, 8>{});
-  else if (L == 128) run(std::integral_constant<int, 4>{}, std::integral_constant<int, 4>{});
-  else dispatch_waves<FwdTag>(nw, [&](auto c) { run(c, std::integral_constant<int, 0>{}); });
 }

@@ -79,7 +79,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const uint16_t* __
   const int kt0 = (int)((long)split * nkt / S), kt1 = (int)((long)(split + 1) * nkt / S);
   const int nt = kt1 - kt0;
   const int rows = min(nt * BT, T - kt0 * BT);  // tokens of this split that exist: the descriptors end there
-  HQ_DASSERT(n0 + 256 <= N && k0 + 256 <= K && nt >= 2 && rows > 0);
+  // N, K multiples of 128: a last tile may stick out by 128 columns.  Its DMA reads the next row's bytes
+  // (or zeros past the descriptor's end) into the unused columns, which only feed outputs that are never
+  // stored: each output (n, k) depends on column n of dy and column k of x alone.
+  HQ_DASSERT(n0 + 128 <= N && k0 + 128 <= K && nt >= 2 && rows > 0);
 
   const uint16_t* Ab = A + (size_t)kt0 * BT * N + n0;
   const uint16_t* Bb = B + (size_t)kt0 * BT * K + k0;
@@ -226,11 +229,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const uint16_t* __
   // epilogue: fp32 slab, straight from the accumulators (lane: output row n, 4 consecutive k)
   float* out = part + (size_t)split * N * K;
   const int fr = lane & 15, fq = lane >> 4;
+  const bool n_full = n0 + 256 <= N, k_full = k0 + 256 <= K;   // block-uniform: a 128-column edge tile
 #pragma unroll
   for (int I = 0; I < 8; ++I) {
     const int row = n0 + (I >> 2) * 128 + wm * 64 + (I & 3) * 16 + fr;
+    if (!n_full && (I >> 2) == 1) continue;
 #pragma unroll
     for (int J = 0; J < 4; ++J) {
+      if (!k_full && (J >> 1) == 1) continue;
       const int col = k0 + (J >> 1) * 128 + wn * 32 + (J & 1) * 16 + fq * 4;
       *reinterpret_cast<float4*>(out + (size_t)row * K + col) = make_float4(acc[I][J][0], acc[I][J][1], acc[I][J][2], acc[I][J][3]);
     }
@@ -239,7 +245,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const uint16_t* __
     // every accumulator register of bacc holds the column sum of output row n = lane & 15 (+ subtile)
     if (do_bias && fq == 0) {
 #pragma unroll
-      for (int I = 0; I < 8; ++I) bpart[(size_t)split * N + n0 + (I >> 2) * 128 + wm * 64 + (I & 3) * 16 + fr] = bacc[I][0];
+      for (int I = 0; I < 8; ++I)
+        if (n_full || (I >> 2) == 0) bpart[(size_t)split * N + n0 + (I >> 2) * 128 + wm * 64 + (I & 3) * 16 + fr] = bacc[I][0];
     }
   }
 }
@@ -268,9 +275,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float4* __rest
 }  // namespace
 
 int hq_gemm_tn_splits(int T, int N, int K) {
-  if (T <= 0 || N % 256 || K % 256 || N < 256 || K < 256) return 0;
+  if (T <= 0 || N % 128 || K % 128 || N < 128 || K < 128) return 0;
   if ((size_t)T * N * 2 >= (1ull << 31) || (size_t)T * K * 2 >= (1ull << 31)) return 0;
-  const int tiles = (N / 256) * (K / 256);
+  const int tiles = ((N + 255) / 256) * ((K + 255) / 256);
   int S = 256 / tiles;                     // one full round of the 256 CUs
   if (S < 1) S = 1;
   const int nkt = (T + BT - 1) / BT;
@@ -294,7 +301,7 @@ void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, f
     return true;
   }();
   (void)init;
-  const int tiles_k = K / 256, tiles = (N / 256) * tiles_k;
+  const int tiles_k = (K + 255) / 256, tiles = ((N + 255) / 256) * tiles_k;
   if (bout)
     hipLaunchKernelGGL((gemm_tn_kernel<0, true>), dim3(tiles * S), dim3(kThreads), lds, s, A, B, part, bpart, T, N, K, S,
                        tiles_k);

@@ -117,4 +117,10 @@ void HqReducer::wait(int64_t compute_stream) {
   HIP_CHECK_THROW(hipStreamWaitEvent((hipStream_t)compute_stream, e, 0));
 }
 
+int HqReducer::comm_count() const {
+  int n = 0;
+  NCCL_CHECK(ncclCommCount((ncclComm_t)comm_, &n));
+  return n;
+}
+
 void HqReducer::synchronize() { HIP_CHECK_THROW(hipStreamSynchronize((hipStream_t)stream_)); }

@@ -5,12 +5,16 @@ Capability parity with the reference model (``modules/model/model/model.py:13-73
 ``reg_start``/``reg_end`` Linear(H,1)+Sigmoid), re-designed around fused kernels:
 
 * The encoder is a chain of ``torch.autograd.Function``s — one for the embeddings, one per
-  encoder layer — each with an explicit backward.  Per layer forward = 4 hipBLASLt GEMMs +
-  3 fused HIP kernels (flash attention, residual+dropout+LayerNorm ×2, GELU); backward = 8 GEMMs
-  + 4 fused kernels.  Weight gradients are written straight into the fp32 grad arena and the
-  layer then signals the gradient reducer, which overlaps its RCCL all-reduce with the rest of
-  the backward (replaces DDP's per-parameter autograd hooks).
-* Dropout masks are regenerated from a counter hash (``ops.rng``) — nothing is stored.
+  encoder layer — each with an explicit backward.  Per layer forward = 4 own MFMA GEMMs with fused
+  epilogues (QKV + bias, out-projection + bias, FFN1 + bias + GELU/GELU', FFN2 + bias) + flash attention
+  + 2 residual/dropout/LayerNorm kernels; backward = 4 dgrad GEMMs (residual-add and GELU' epilogues),
+  4 split-K weight-gradient GEMMs, the attention backward and 2 LayerNorm backwards.  Weight gradients
+  are written straight into the fp32 grad arena and the layer then signals the gradient reducer, which
+  overlaps its RCCL all-reduce with the rest of the backward (replaces DDP's per-parameter autograd
+  hooks).
+* Dropout: masks come from a counter hash (``ops.rng``, bit-identical in the HIP kernels).  The attention
+  forward stores its keep-bits (1 bit per probability) for the backward; every other dropout site
+  regenerates its mask from (seed, op id, element index) in the backward.
 * Pooler + the four heads (``heads.py``): on the GPU one fused fp32 kernel each way plus one fused
   loss kernel (``csrc/kernels/heads.hip``); elsewhere ordinary fp32 autograd on the master parameters.
 * ``state_dict()`` keys are the HF names under ``transformer.`` plus the reference head names, so
@@ -381,8 +385,6 @@ class BertForQuestionAnswering(nn.Module):
         self.store.to(probe.device)
         self.store.set_compute_dtype(self.compute_dtype_for(probe.device))
         if probe.device.type == "cuda":
-            from ..ops.tuning import enable_tuned_gemms
-            enable_tuned_gemms()
             if self._want_side_stream and self.grad_side_stream is None:
                 self.grad_side_stream = torch.cuda.Stream(device=probe.device)
         else:

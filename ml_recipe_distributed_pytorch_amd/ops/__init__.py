@@ -1,10 +1,9 @@
 """Fused-op API used by the model.  Dispatch is by device, not by a backend registry:
 
 * CUDA (ROCm/HIP) tensors → hand-written gfx950 kernels in ``_hq_kernels.so`` (fail loudly if absent):
-  embedding, LayerNorm, attention, optimizer, and the MFMA GEMMs (``gemm.hip`` NT with fused epilogues
-  for every encoder projection forward and dgrad, ``gemm_tn.hip`` split-K weight gradients).  hipBLASLt
-  (``torch.addmm/mm``) is only the fallback for shapes the MFMA kernels do not tile (see ``_mfma``) and
-  for the tiny pooler / QA-head GEMMs.
+  embedding, LayerNorm, attention, optimizer, heads, and the MFMA GEMMs (``gemm.hip`` NT with fused
+  epilogues for every encoder projection forward and dgrad, ``gemm_tn.hip`` split-K weight gradients).
+  No vendor BLAS: an untileable shape raises.
 * CPU tensors → ``ops.reference`` (pure PyTorch, fp32), which is also the numerics oracle.
 """
 from __future__ import annotations
@@ -113,23 +112,11 @@ def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale
 
 
 # --------------------------------------------------------------------------------------- linear
-# Which projection GEMMs run on the hand-written MFMA NT kernel (gemm.hip) instead of hipBLASLt.
-#   HQ_GEMM=auto (default): the GEMMs whose epilogue fuses an elementwise pass — FFN1 + GELU,
-#     FFN2-dgrad + dGELU + FFN1 bias-grad (1.08x / 1.40x vs hipBLASLt + separate kernel at b256,
-#     profiles/) and the QKV dgrad + residual-gradient add (torch.addmm first copies the residual
-#     into the output: +56 µs at b256), plus the plain dgrads, for every M (gemm.hip picks 256-row or
-#     128² tiles by M alignment and CU fill).  Weight gradients take the split-K TN kernel (gemm_tn.hip).
-#     Plain forward projections follow FWD_MFMA below (all three on the MFMA kernel by default);
-#   HQ_GEMM=mfma: every supported shape;  HQ_GEMM=blas: none.
+# Every projection GEMM on the GPU runs on the hand-written gfx950 MFMA kernels: ``gemm.hip`` (NT, C = A·Bᵀ
+# with fused epilogues, every forward projection and dgrad) and ``gemm_tn.hip`` (split-K weight gradients).
+# There is no vendor-BLAS fallback: a shape the kernels do not tile raises instead of silently running
+# something else (BERT / RoBERTa base and large, and the tiny test config, all tile).
 _EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID, _EPI_GELUD, _EPI_DMUL, _EPI_BDR = range(8)
-_GEMM_MODE = os.environ.get("HQ_GEMM", "auto").lower()
-# Plain forward projections (bias epilogue) that take the MFMA kernel in auto mode, by name: qkv | out | ffn2.
-# In the full b256 step hipBLASLt's QKV pick runs 381 µs vs 316 µs standalone while the MFMA kernel holds
-# ~337 µs (+0.4 % step); the out-projection / FFN2 forwards are step-neutral either way (profiles/s3_ab), so
-# all three default to the own kernel and the bf16 encoder runs no vendor GEMM (the tiny pooler/head
-# GEMMs stay in torch).
-FWD_MFMA = {k for k in os.environ.get("HQ_FWD_MFMA", "qkv,out,ffn2").split(",") if k}
-GELU_DERIV = os.environ.get("HQ_GELU_DERIV", "1") == "1"   # FFN1 stores gelu'(pre) (linear_gelu_fwd_d)
 # HQ_LN_FUSE=1: the out-projection / FFN2 GEMM writes z = dropout(x·Wᵀ + b) + resid itself (EPI_BDR) and the
 # LayerNorm that follows reads z alone — one HBM pass over [T, H] less per LayerNorm, bitwise the same
 # result.  Off by default: the epilogue's residual read and dropout hash are serial with the persistent GEMM's
@@ -137,24 +124,15 @@ GELU_DERIV = os.environ.get("HQ_GELU_DERIV", "1") == "1"   # FFN1 stores gelu'(p
 LN_FUSE = os.environ.get("HQ_LN_FUSE", "0") == "1"
 
 
-def set_gemm_mode(mode: str) -> str:
-    """Switch the projection-GEMM policy at runtime (auto | mfma | blas); returns the previous mode."""
-    global _GEMM_MODE
-    prev, _GEMM_MODE = _GEMM_MODE, mode.lower()
-    return prev
-
-
-def _mfma(M: int, N: int, K: int, kind: str = "plain") -> bool:
-    """Every projection shape with N % 128 == 0 and K % 64 == 0 runs on the own MFMA kernels: the
-    256-row kernels where M % 256 == 0 and the grid fills the CUs, the 128²-tile kernel otherwise
-    (M tails of dynamically padded batches, small micro-batches, low-fill grids) — gemm.hip picks."""
-    if _GEMM_MODE == "blas":
-        return False
+def _check_nt(M: int, N: int, K: int, what: str):
+    """Raise unless C[M, N] = A[M, K]·B[N, K]ᵀ tiles on gemm.hip (N % 128 == 0, K % 64 == 0; any M)."""
     if _k().gemm_nt_supported(int(M), int(N), int(K)) <= 0:
-        return False
-    if _GEMM_MODE == "mfma":
-        return True
-    return kind in ("dgelu", "gelu", "resid", "dgrad") or kind in FWD_MFMA
+        raise RuntimeError(f"{what}: GEMM M={M} N={N} K={K} does not tile on the gfx950 MFMA kernels "
+                           "(needs N % 128 == 0 and K % 64 == 0)")
+
+
+def _bias32(b, b32):
+    return b32 if b32 is not None else b.float().contiguous()
 
 
 def _part(M: int, N: int, K: int, device):
@@ -163,23 +141,21 @@ def _part(M: int, N: int, K: int, device):
 
 
 def linear_fwd(x, w, b, b32=None, kind: str = "plain"):
-    """y = x·Wᵀ + b.  GPU: hipBLASLt (bias epilogue) or the MFMA NT kernel (fp32 ``b32`` bias); ``kind``
-    names the projection (qkv | out | ffn2) for the FWD_MFMA policy."""
+    """y = x·Wᵀ + b (MFMA NT kernel with the fp32 bias ``b32`` in its epilogue on the GPU)."""
     if x.is_cuda:
-        if b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1], kind):
-            return _k().gemm_nt(x, w, _EPI_BIAS, bias=b32)
-        return torch.addmm(b, x, w.t()) if b is not None else torch.mm(x, w.t())
+        _check_nt(x.shape[0], w.shape[0], x.shape[1], f"linear_fwd[{kind}]")
+        return _k().gemm_nt(x, w, _EPI_BIAS, bias=_bias32(b, b32))
     return ref.linear_fwd(x, w, b)
 
 
 def linear_bdr_ln_fwd(x, w, b, b32, resid, kind, gamma, beta, eps, p, seed, opid):
     """LayerNorm(dropout_p(x·Wᵀ + b) + resid) -> (y, z, mean, rstd), bitwise what ``linear_fwd`` followed by
-    ``ln_fwd`` computes.  On the GPU with the own MFMA kernel the GEMM's EPI_BDR epilogue adds the dropped-out
+    ``ln_fwd`` computes.  On the GPU with ``HQ_LN_FUSE=1`` the GEMM's EPI_BDR epilogue adds the dropped-out
     projection to the residual and stores z, and the LayerNorm reads z alone (``ln_fwd`` with resid=None);
     otherwise the two ops run as before."""
-    if (x.is_cuda and LN_FUSE and b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1], kind)
-            and x.shape[0] * w.shape[0] < 2 ** 32):
-        z = _k().gemm_nt(x, w, _EPI_BDR, bias=b32, resid=resid, p=float(p), seed=int(seed), opid=int(opid))
+    if x.is_cuda and LN_FUSE and x.shape[0] * w.shape[0] < 2 ** 32:
+        _check_nt(x.shape[0], w.shape[0], x.shape[1], f"linear_bdr_ln_fwd[{kind}]")
+        z = _k().gemm_nt(x, w, _EPI_BDR, bias=_bias32(b, b32), resid=resid, p=float(p), seed=int(seed), opid=int(opid))
         return tuple(_k().ln_fwd(z, None, gamma, beta, float(eps), 0.0, 0, 0))
     return ln_fwd(linear_fwd(x, w, b, b32, kind), resid, gamma, beta, eps, p, seed, opid)
 
@@ -252,23 +228,25 @@ def linear_gelu_fwd_fp8(x, w8s, b32, in_state: Fp8DelayedState, out_state: Fp8De
 
 
 def linear_gelu_fwd(x, w, b, b32=None):
-    """(pre, act) with pre = x·Wᵀ + b, act = gelu(pre).  GPU: one MFMA GEMM with the GELU epilogue
-    (pre stored for the backward) when the shape allows, else GEMM + gelu kernel."""
-    if x.is_cuda and b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1], "gelu"):
+    """(pre, act) with pre = x·Wᵀ + b, act = gelu(pre) — the CPU oracle form; the GPU uses
+    ``linear_gelu_fwd_d`` (derivative stored instead of pre)."""
+    if x.is_cuda:
+        _check_nt(x.shape[0], w.shape[0], x.shape[1], "linear_gelu_fwd")
         pre = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
-        act = _k().gemm_nt(x, w, _EPI_GELU, bias=b32, pre=pre)
+        act = _k().gemm_nt(x, w, _EPI_GELU, bias=_bias32(b, b32), pre=pre)
         return pre, act
-    pre = linear_fwd(x, w, b, b32)
+    pre = ref.linear_fwd(x, w, b)
     return pre, gelu_fwd(pre)
 
 
 def linear_gelu_fwd_d(x, w, b, b32=None):
-    """(saved, act, is_deriv): like ``linear_gelu_fwd`` but, on the MFMA path, ``saved`` is gelu'(pre)
-    (bf16) instead of pre — the epilogue evaluates Φ and φ anyway, and the backward then needs one
-    multiply per element instead of a GELU-derivative evaluation (``linear_dgrad_gelu_d``)."""
-    if GELU_DERIV and x.is_cuda and b32 is not None and _mfma(x.shape[0], w.shape[0], x.shape[1], "gelu"):
+    """(saved, act, is_deriv).  GPU: one MFMA GEMM whose epilogue evaluates Φ and φ once and stores
+    gelu'(pre) (bf16) beside act, so the backward needs one multiply per element (``linear_dgrad_gelu_d``);
+    CPU: (pre, act, False)."""
+    if x.is_cuda:
+        _check_nt(x.shape[0], w.shape[0], x.shape[1], "linear_gelu_fwd_d")
         gd = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
-        act = _k().gemm_nt(x, w, _EPI_GELUD, bias=b32, pre=gd)
+        act = _k().gemm_nt(x, w, _EPI_GELUD, bias=_bias32(b, b32), pre=gd)
         return gd, act, True
     pre, act = linear_gelu_fwd(x, w, b, b32)
     return pre, act, False
@@ -279,7 +257,8 @@ def linear_dgrad_gelu_d(dy, w, saved, is_deriv, g_bias, accumulate, wt=None):
     if not is_deriv:
         return linear_dgrad_gelu(dy, w, saved, g_bias, accumulate, wt)
     M, N = dy.shape[0], w.shape[1]
-    assert wt is not None, "stored-derivative GELU backward needs the MFMA path (Wᵀ working copy)"
+    assert wt is not None, "stored-derivative GELU backward needs the Wᵀ working copy"
+    _check_nt(M, N, dy.shape[1], "linear_dgrad_gelu_d")
     part = _part(M, N, dy.shape[1], dy.device)
     dpre = _k().gemm_nt(dy, wt, _EPI_DMUL, pre=saved, part=part)
     if g_bias is not None:
@@ -288,76 +267,51 @@ def linear_dgrad_gelu_d(dy, w, saved, is_deriv, g_bias, accumulate, wt=None):
 
 
 def linear_dgrad(dy, w, wt=None):
-    """dy·W.  ``wt`` = Wᵀ working copy (ParamStore.view_t) enables the NT MFMA kernel."""
+    """dy·W.  GPU: NT kernel on the Wᵀ working copy ``wt`` (ParamStore.view_t)."""
     if dy.is_cuda:
-        if wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1], "dgrad"):
-            return _k().gemm_nt(dy, wt, _EPI_NONE)
-        return torch.mm(dy, w)
+        assert wt is not None, "GPU dgrad needs the Wᵀ working copy"
+        _check_nt(dy.shape[0], w.shape[1], dy.shape[1], "linear_dgrad")
+        return _k().gemm_nt(dy, wt, _EPI_NONE)
     return ref.linear_dgrad(dy, w)
 
 
 def linear_dgrad_add(dy, w, resid, wt=None):
     """resid + dy·W (fuses the residual-gradient add)."""
     if dy.is_cuda:
-        if wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1], "resid"):
-            return _k().gemm_nt(dy, wt, _EPI_RESID, resid=resid)
-        return torch.addmm(resid, dy, w)
+        assert wt is not None, "GPU dgrad needs the Wᵀ working copy"
+        _check_nt(dy.shape[0], w.shape[1], dy.shape[1], "linear_dgrad_add")
+        return _k().gemm_nt(dy, wt, _EPI_RESID, resid=resid)
     return ref.linear_dgrad_add(dy, w, resid)
 
 
 def linear_dgrad_gelu(dy, w, pre, g_bias, accumulate, wt=None):
     """dpre = (dy·W) ⊙ gelu'(pre) and g_bias (+)= Σ_rows dpre — the dgrad of the layer after GELU
     fused with the GELU backward and the bias gradient of the layer before it."""
-    if dy.is_cuda and wt is not None and _mfma(dy.shape[0], w.shape[1], dy.shape[1], "dgelu"):
+    if dy.is_cuda:
+        assert wt is not None, "GPU dgrad needs the Wᵀ working copy"
         M, N = dy.shape[0], w.shape[1]
+        _check_nt(M, N, dy.shape[1], "linear_dgrad_gelu")
         part = _part(M, N, dy.shape[1], dy.device)
         dpre = _k().gemm_nt(dy, wt, _EPI_DGELU, pre=pre, part=part)
         if g_bias is not None:
             _k().colsum_into(part, g_bias, bool(accumulate))
         return dpre
-    return gelu_bwd(linear_dgrad(dy, w, wt), pre, g_bias, accumulate)
-
-
-def _wgrad_splits(T: int, N: int, K: int) -> int:
-    """Split-K factor for dW = dyᵀ·x (reduction over T tokens, output only N×K): hipBLASLt runs these
-    long-K / small-MN GEMMs far below peak (a 768×768 output is 9 tiles of 256² for 256 CUs), so the
-    T axis is split into a batched GEMM with fp32 partials.  Factors from the MI355X sweep
-    (tools/wgrad_bench.py, profiles/): ~6k tokens per split for >= 32 output tiles, ~3k for 10-31,
-    ~1.5k for <= 9, at most 16 splits (T = 98304: 16 everywhere, 430-480 µs → 0.8-1.0 PF)."""
-    tiles = max(1, (N * K) // (256 * 256))
-    per = 6144 if tiles >= 32 else (3072 if tiles > 9 else 1536)
-    target = max(1, min(16, T // per))
-    s = 1
-    while s * 2 <= target and T % (s * 2) == 0 and T // (s * 2) >= 1024:
-        s *= 2
-    return s
+    return gelu_bwd(ref.linear_dgrad(dy, w), pre, g_bias, accumulate)
 
 
 def linear_wgrad(dy, x, g_w, g_b, accumulate):
     """g_w (fp32 arena view) (+)= dyᵀ·x with fp32 GEMM output; g_b (+)= column sums of dy.
-    GPU: the hand-written split-K TN MFMA kernel (gemm_tn.hip; 1.14-1.31x hipBLASLt's batched split-K
-    on the BERT shapes, profiles/) whenever the shape tiles (N, K multiples of 256, T of 64);
-    hipBLASLt otherwise (``HQ_GEMM=blas`` forces it)."""
+    GPU: the split-K TN MFMA kernel (gemm_tn.hip) with the bias gradient fused; raises for shapes it does
+    not tile (N, K multiples of 128)."""
     if dy.is_cuda:
         T, N = dy.shape
         K = x.shape[1]
-        if _GEMM_MODE != "blas" and g_w.is_contiguous() and _k().gemm_tn_splits(T, N, K) > 0:
-            _k().gemm_tn(dy, x, g_w, bool(accumulate), 0, g_b if (g_b is not None and g_b.is_contiguous()) else None)
-            if g_b is not None and not g_b.is_contiguous():
-                _k().bias_grad(dy, g_b, bool(accumulate))
-            return
-        s = _wgrad_splits(T, N, K)
-        if s > 1:
-            part = torch.bmm(dy.view(s, T // s, N).transpose(1, 2), x.view(s, T // s, K), out_dtype=torch.float32)
-            if accumulate:
-                g_w.add_(part.sum(0))
-            else:
-                torch.sum(part, 0, out=g_w)
-        elif accumulate:
-            g_w.add_(torch.mm(dy.t(), x, out_dtype=torch.float32))
-        else:
-            torch.mm(dy.t(), x, out_dtype=torch.float32, out=g_w)
-        if g_b is not None:
+        if not g_w.is_contiguous() or _k().gemm_tn_splits(T, N, K) <= 0:
+            raise RuntimeError(f"linear_wgrad: dW[{N}, {K}] over T={T} tokens does not tile on gemm_tn "
+                               "(needs N % 128 == 0, K % 128 == 0 and a contiguous fp32 gradient view)")
+        fuse_b = g_b is not None and g_b.is_contiguous()
+        _k().gemm_tn(dy, x, g_w, bool(accumulate), 0, g_b if fuse_b else None)
+        if g_b is not None and not fuse_b:
             _k().bias_grad(dy, g_b, bool(accumulate))
         return
     ref.linear_wgrad(dy, x, g_w, g_b, accumulate)

@@ -84,7 +84,8 @@ def init_distributed(backend: str, *, init_method: Optional[str] = None, world_s
 
 
 def barrier():
-    if dist.is_initialized() and dist.get_world_size() > 1:
+    """Barrier over the default group (also a 1-rank group: the world-1 rehearsal of the N-rank path)."""
+    if dist.is_initialized():
         if _INFO.backend == "nccl" and _INFO.device.type == "cuda":
             dist.barrier(device_ids=[_INFO.device.index])
         else:

@@ -112,11 +112,12 @@ class GradReducer:
         blocks hold CUs, and with the static schedule the GEMM workgroups that wait for those CUs run their
         whole share late (+160-180 µs per GEMM per 200 µs held, tools/gemm_contention_bench.py); the dynamic
         per-XCD ticket schedule costs ~0.9 % of the uncontended step, so it is switched on only here, when a
-        collective actually overlaps the backward.  HQ_GEMM_SCHED (0/1) overrides."""
+        collective actually overlaps the backward — or when ``force`` rehearses that path on one GPU.
+        HQ_GEMM_SCHED (0/1) overrides."""
         if not on_gpu:
             return "n/a"
         env = os.environ.get("HQ_GEMM_SCHED")
-        dynamic = (env == "1") if env in ("0", "1") else self.world > 1
+        dynamic = (env == "1") if env in ("0", "1") else (self.world > 1 or self.force)
         kernels().gemm_set_sched(1 if dynamic else 0)
         return "dynamic" if dynamic else "static"
 
@@ -175,6 +176,11 @@ class GradReducer:
     @property
     def n_buckets(self) -> int:
         return len(self.buckets)
+
+    @property
+    def comm_ranks(self) -> Optional[int]:
+        """Ranks the native RCCL communicator spans (``ncclCommCount``); None without one."""
+        return int(self._native.comm_count) if self._native is not None else None
 
     def prepare(self, sync: bool = True):
         self.active = sync and (self.world > 1 or self.force)

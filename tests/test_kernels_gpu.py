@@ -129,18 +129,13 @@ def _attn_case(cuda, B, L, nh, p, masked, ramp=0.0, amp=1.0, ctx_tol=2e-2, left_
 
 @pytest.mark.parametrize("L", [384, 512, 256, 128, 100, 24, 7])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-@pytest.mark.parametrize("det", [False, True], ids=["fused", "det"])
-def test_attention(cuda, monkeypatch, L, p, det):
-    """fused: the opt-in single-kernel backward (HQ_ATTN_BWD=4, L <= 384, LDS-atomic dQ); det: the
-    deterministic flag, which keeps the default two-kernel backward (ring dQ + dK/dV kernels) either way."""
-    if not det:
-        monkeypatch.setenv("HQ_ATTN_BWD", "4")
-    _attn_case(cuda, 2, L, 2, p, masked=True, det=det)
+def test_attention(cuda, L, p):
+    """Ring forward + the two-kernel backward (ring dQ + register dK/dV) against the fp32 oracle."""
+    _attn_case(cuda, 2, L, 2, p, masked=True, det=True)
 
 
-def test_attention_bwd_deterministic_mode_repeatable(cuda, monkeypatch):
-    """The deterministic backward is bitwise repeatable; the opt-in fused one agrees with it to fp32-sum
-    reordering."""
+def test_attention_bwd_deterministic_mode_repeatable(cuda):
+    """The backward (no atomics) is bitwise repeatable."""
     k = _native.kernels()
     torch.manual_seed(5)
     B, L, nh = 4, 384, 12
@@ -151,12 +146,8 @@ def test_attention_bwd_deterministic_mode_repeatable(cuda, monkeypatch):
     ctx, lse, bits = k.attn_fwd(qkv, kb, B, L, nh, 0.1, 7, 1, 0.125)
     dctx = _bf(torch.randn(B * L, H)).to(cuda)
     d0 = k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125, True)
-    for _ in range(3):
-        assert torch.equal(k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125, True), d0)
-    monkeypatch.setenv("HQ_ATTN_BWD", "4")
-    f = k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125, False).float()
-    _close(f[:, :H], d0[:, :H].float(), 1e-2, 1e-2, "fused dQ vs deterministic")
-    _close(f[:, H:], d0[:, H:].float(), 1e-2, 1e-2, "fused dK/dV vs deterministic")
+    for det in (True, False, True):
+        assert torch.equal(k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125, det), d0)
 
 
 def test_attention_bert_base_shape(cuda):
@@ -174,11 +165,15 @@ def test_attention_growing_row_max(cuda, ramp):
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("L", [384, 100])
-def test_attention_slow_path_forced(cuda, monkeypatch, p, L):
-    """HQ_ATTN_FORCE_SLOW=1 sends every workgroup of the ring forward down its slow path (per-tile max and
+def test_attention_slow_path_forced(cuda, p, L):
+    """attn_set_force_slow(1) sends every workgroup of the ring forward down its slow path (per-tile max and
     rescale, per-wave LDS staging): rule 26 of the kernel playbook — the rare branch gets its own test."""
-    monkeypatch.setenv("HQ_ATTN_FORCE_SLOW", "1")
-    _attn_case(cuda, 2, L, 2, p, masked=True)
+    k = _native.kernels()
+    k.attn_set_force_slow(1)
+    try:
+        _attn_case(cuda, 2, L, 2, p, masked=True)
+    finally:
+        k.attn_set_force_slow(0)
 
 
 def test_attention_left_padded(cuda):

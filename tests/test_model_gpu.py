@@ -20,17 +20,12 @@ def _inputs(B, L, V):
     return ids, ids > 0, tt
 
 
-@pytest.mark.parametrize("train,gemm,side", [(False, "auto", False), (True, "auto", False), (True, "mfma", False),
-                                             (True, "auto", True)])
-def test_tiny_model_gpu_matches_cpu(cuda, train, gemm, side):
-    """gemm="mfma" routes every projection (fwd + GELU epilogue, dgrad, residual and dGELU
-    epilogues on the transposed weight copies) through the hand-written MFMA GEMM."""
-    from ml_recipe_distributed_pytorch_amd import ops
-    prev = ops.set_gemm_mode(gemm)
-    try:
-        _tiny_parity(cuda, train, B=4 if gemm == "mfma" else 3, side=side)
-    finally:
-        ops.set_gemm_mode(prev)
+@pytest.mark.parametrize("train,B,side", [(False, 3, False), (True, 3, False), (True, 4, False), (True, 3, True)])
+def test_tiny_model_gpu_matches_cpu(cuda, train, B, side):
+    """Every projection (fwd + GELU epilogue, dgrad, residual and GELU' epilogues on the transposed
+    weight copies, split-K weight gradients at N, K = 128-multiples) runs on the own MFMA GEMMs;
+    B = 3 gives M = 192 (128² tiles with an M tail), B = 4 M = 256."""
+    _tiny_parity(cuda, train, B=B, side=side)
 
 
 def _tiny_parity(cuda, train, B, side=False):

@@ -142,15 +142,6 @@ def test_linear_ops():
     torch.testing.assert_close(gb, dy.sum(0))
 
 
-def test_wgrad_split_heuristic():
-    from ml_recipe_distributed_pytorch_amd.ops import _wgrad_splits
-    assert _wgrad_splits(24576, 768, 768) > 1       # small weight, long token dim → split-K
-    assert _wgrad_splits(128, 768, 768) == 1        # short token dim → no split
-    for T, N, K in ((24576, 768, 768), (24576, 2304, 768), (24576, 3072, 768), (32768, 768, 3072)):
-        s = _wgrad_splits(T, N, K)
-        assert T % s == 0
-
-
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_linear_bdr_ln_fwd_cpu_path(p):
     """The fused projection + dropout + residual + LayerNorm op (GPU: EPI_BDR epilogue + z-in LayerNorm)

@@ -4,7 +4,7 @@ per-step differences are not swamped by box-to-box variance.  Rounds alternate A
 median ms/step of each.
 
     python tools/ab_step.py --toggle gelu_deriv [--batch 256] [--rounds 4] [--steps 8]
-toggles: gelu_deriv (ops.GELU_DERIV), gemm_blas (ops GEMM mode auto vs blas), gemm_v1 (NT kernel v2 vs v1),
+toggles: gemm_v1 (NT kernel v2 vs v1),
          input_pipeline (on: bench.py's per-step host synthesis + pinned H2D; off: one resident batch)
 """
 import argparse
@@ -23,7 +23,6 @@ from ml_recipe_distributed_pytorch_amd.data.dummy import SpecialIds, synth_batch
 from ml_recipe_distributed_pytorch_amd.models.bert import BertForQuestionAnswering  # noqa: E402
 from ml_recipe_distributed_pytorch_amd.models.config import get_config  # noqa: E402
 from ml_recipe_distributed_pytorch_amd.models.losses import build_loss  # noqa: E402
-from ml_recipe_distributed_pytorch_amd.ops.tuning import enable_tuned_gemms  # noqa: E402
 from ml_recipe_distributed_pytorch_amd.train.engine import TrainEngine, to_device  # noqa: E402
 from ml_recipe_distributed_pytorch_amd.train.optim import FusedAdamW  # noqa: E402
 from ml_recipe_distributed_pytorch_amd.train.trainer import optimizer_groups  # noqa: E402
@@ -38,16 +37,10 @@ def set_toggle(name, on):
         if on and getattr(m, "_ab_side", None) is None:
             m._ab_side = torch.cuda.Stream(device=torch.device("cuda", 0))
         m.grad_side_stream = m._ab_side if on else None
-    elif name == "gelu_deriv":
-        ops.GELU_DERIV = on
-    elif name == "gemm_blas":
-        ops.set_gemm_mode("blas" if on else "auto")
     elif name == "gemm_v1":
         _native.kernels().gemm_set_variant(1 if on else 0)
     elif name == "gemm_v2":   # on: per-tile v2 everywhere; off: auto (persistent v3 for K <= 2304)
         _native.kernels().gemm_set_variant(2 if on else 0)
-    elif name.startswith("fwd_mfma="):  # e.g. fwd_mfma=qkv,out,ffn2 : B runs those forward projections on MFMA
-        ops.FWD_MFMA = set(name.split("=", 1)[1].split(",")) if on else set()
     elif name == "input_pipeline":
         pass
     else:
@@ -63,7 +56,6 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=8)
     a = ap.parse_args()
-    enable_tuned_gemms()
     dev = torch.device("cuda", 0)
     cfg = get_config(a.model)
     model = BertForQuestionAnswering(cfg, seed=0).to(dev).train()
