@@ -49,24 +49,6 @@ __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, 
 __device__ __forceinline__ float gelu_erf(float x) { return hq_gelu(x); }
 __device__ __forceinline__ float gelu_grad(float x) { return hq_gelu_grad(x); }
 
-// EPI_BDR dropout stream (unused by the other epilogues): key source, 16-bit keep threshold, keep scale
-struct HqDropArg {
-  HqDropKey kd;
-  uint32_t thr;
-  float ks;
-};
-// z = x·keep + r for 8 consecutive elements from flat index idx (even): ln_fwd's z, bit for bit
-__device__ __forceinline__ uint4 epi_bdr8(const uint4& piece, const uint4& r4, uint32_t idx, const HqDropArg& dr,
-                                          uint32_t key) {
-  float d[8], rr[8], m[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
-  hq_unpack8(piece, d);
-  hq_unpack8(r4, rr);
-  if (dr.thr) hq_keep8(idx, key, dr.thr, dr.ks, m);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) d[e] = d[e] * m[e] + rr[e];
-  return hq_pack8(d);
-}
-
 // Issue the LDS-DMA of one [ROWS × 64] bf16 panel (rows of 128 B) into lds (+ byte offset).
 // Each wave-instruction moves 8 rows (64 lanes × 16 B); this wave handles `n_instr` of them
 // starting at panel row `row0`.
@@ -269,7 +251,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt_kernel(const uint16_t* __
       for (int e = 0; e < 8; ++e) d[e] += rr[e];
       piece = hq_pack8(d);
     } else if constexpr (EPI == HQ_EPI_BDR) {
-      piece = epi_bdr8(piece, *reinterpret_cast<const uint4*>(R + goff), (uint32_t)goff, dr, key);
+      piece = hq_epi_bdr8(piece, *reinterpret_cast<const uint4*>(R + goff), (uint32_t)goff, dr, key);
     }
     *reinterpret_cast<uint4*>(C + goff) = piece;
   }
@@ -473,7 +455,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nts_kernel(const uint16_t* __rest
       for (int e = 0; e < 8; ++e) d[e] += rr[e];
       piece = hq_pack8(d);
     } else if constexpr (EPI == HQ_EPI_BDR) {
-      piece = epi_bdr8(piece, *reinterpret_cast<const uint4*>(R + goff), (uint32_t)goff, dr, key);
+      piece = hq_epi_bdr8(piece, *reinterpret_cast<const uint4*>(R + goff), (uint32_t)goff, dr, key);
     }
     *reinterpret_cast<uint4*>(C + goff) = piece;
   }
@@ -796,7 +778,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
       for (int e = 0; e < 8; ++e) d[e] += rr[e];
       piece = hq_pack8(d);
     } else if constexpr (EPI == HQ_EPI_BDR) {
-      piece = epi_bdr8(piece, aux[it], (uint32_t)goff, dr, key);
+      piece = hq_epi_bdr8(piece, aux[it], (uint32_t)goff, dr, key);
     }
     *reinterpret_cast<uint4*>(C + goff) = piece;
   }
@@ -1152,7 +1134,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
           for (int e = 0; e < 8; ++e) d[e] += rr[e];
           piece = hq_pack8(d);
         } else if constexpr (EPI == HQ_EPI_BDR) {
-          piece = epi_bdr8(piece, aux[it], (uint32_t)goff, dr, key);
+          piece = hq_epi_bdr8(piece, aux[it], (uint32_t)goff, dr, key);
         }
         if (!(epi_flags & kDbgNoStore)) store16(C + goff, piece, epi_flags & kNtC);
         else asm volatile("" :: "v"(piece.x), "v"(piece.y), "v"(piece.z), "v"(piece.w));
