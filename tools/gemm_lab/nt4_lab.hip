@@ -5,7 +5,7 @@
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I ml_recipe_distributed_pytorch_amd/csrc/include \
 //         tools/gemm_lab/nt4_lab.hip -o tools/gemm_lab/nt4_lab && tools/gemm_lab/nt4_lab [M]
 #include "../../ml_recipe_distributed_pytorch_amd/csrc/kernels/gemm.hip"
-#include "../../ml_recipe_distributed_pytorch_amd/csrc/kernels/gemm_nt4.hip"
+#include "nt4_kernel.hip"
 
 #include <algorithm>
 #include <cmath>
