@@ -21,12 +21,15 @@ from types import SimpleNamespace
 METRIC = "samples/sec (whole node) BERT-base QA fine-tune seq=384 at 1/2/4/8 MI355X"   # BASELINE.json
 
 
-def metric_name(model: str, seq: int, batch: int, precision: str) -> str:
-    """BASELINE.json's metric string for the headline config (BERT-base, seq 384, 256 samples per GPU, bf16);
-    any other --model / --seq / --batch / --precision gets a label that names what was measured."""
-    if model == "bert-base-uncased" and seq == 384 and batch == 256 and precision == "bf16":
+def metric_name(model: str, seq: int, batch: int, precision: str, split: int = 1) -> str:
+    """BASELINE.json's metric string for the headline config (BERT-base, seq 384, 256 samples per GPU in one
+    micro-batch, bf16); any other --model / --seq / --batch / --batch_split / --precision gets a label that
+    names what was measured."""
+    if model == "bert-base-uncased" and seq == 384 and batch == 256 and precision == "bf16" and split == 1:
         return METRIC
-    return f"samples/sec (whole node) {model} QA fine-tune seq={seq} batch={batch}/GPU {precision} (not the headline config)"
+    mb = f" as {split}x{batch // split}" if split > 1 else ""
+    return (f"samples/sec (whole node) {model} QA fine-tune seq={seq} batch={batch}/GPU{mb} {precision} "
+            "(not the headline config)")
 # The reference publishes no numbers; BASELINE.md's "baseline to beat" is the reference recipe re-run
 # on the same MI355X (HF BertModel + its QA heads/loss, autocast bf16 for apex O1, AdamW, clip):
 # tools/ref_recipe_bench.py --batch 256 --attn sdpa (the faster of its two attention paths) = 1611.65.
@@ -49,7 +52,11 @@ def parse():
     ap.add_argument("--bucket_cap_mb", type=float, default=32.0)
     ap.add_argument("--profile", action="store_true", help="per-phase timers (adds syncs; not for the headline)")
     ap.add_argument("--graph", action="store_true",
-                    help="replay the forward+backward from a captured HIP graph (single process, no reducer)")
+                    help="replay every micro-step (forward + backward, and the bucket all-reduces on the "
+                         "accumulation boundary) from captured HIP graphs")
+    ap.add_argument("--batch_split", type=int, default=1,
+                    help="micro-batches per optimizer step (reference --batch_split): micro-batch = batch / "
+                         "batch_split, gradients accumulated, all-reduce + optimizer once per step")
     ap.add_argument("--force_reducer", action="store_true",
                     help="keep the gradient reducer active at 1 GPU (1-rank RCCL communicator): rehearses the "
                          "multi-GPU fence → ncclAllReduce → wait path on every bucket of the real backward")
@@ -116,13 +123,18 @@ def main():
     reducer = None
     if world > 1 or args.force_reducer:
         # world > 1 or --force_reducer (1-rank communicator): every bucket goes through the native RCCL reducer
+        # comm timing records HIP timing events around the collectives: not capturable, so off under --graph
+        timing = os.environ.get("HQ_BENCH_COMM_TIMING", "0" if args.graph else "1") == "1"
         reducer = GradReducer(model, bucket_cap_mb=args.bucket_cap_mb, allreduce_dtype=args.allreduce_dtype,
-                              force=args.force_reducer, timing=os.environ.get("HQ_BENCH_COMM_TIMING", "1") == "1")
+                              force=args.force_reducer, timing=timing)
     # HQ_BENCH_REDUCER_IDLE=1 (diagnostic): the reducer and its RCCL communicator exist but the engine never
     # uses them — separates the cost of the communicator's presence from that of its all-reduces
     idle = os.environ.get("HQ_BENCH_REDUCER_IDLE", "0") == "1"
+    S = max(1, args.batch_split)
+    if args.batch % S:
+        raise SystemExit(f"--batch {args.batch} is not a multiple of --batch_split {S}")
     engine = TrainEngine(model, loss_fn, opt, scheduler=sched, reducer=None if idle else reducer, max_grad_norm=1.0,
-                         profile=args.profile, graph=args.graph)
+                         batch_split=S, profile=args.profile, graph=args.graph)
 
     sp = SpecialIds(cfg.vocab_size, cfg.pad_token_id, cfg.unk_token_id, cfg.cls_token_id, cfg.sep_token_id,
                     "bert" if cfg.family == "bert" else "roberta")
@@ -148,7 +160,11 @@ def main():
 
     def one_step():
         inputs, labels = next_batch()
-        return engine.step([(inputs, labels)])
+        if S == 1:
+            return engine.step([(inputs, labels)])
+        b = B // S   # the reference's micro-batches: contiguous slices of the step's batch
+        return engine.step([({k: v[i * b:(i + 1) * b] for k, v in inputs.items()},
+                             {k: v[i * b:(i + 1) * b] for k, v in labels.items()}) for i in range(S)])
 
     for _ in range(args.warmup):
         res = one_step()
@@ -181,11 +197,12 @@ def main():
     enc_linear = NL * (4 * H * H + 2 * H * F)  # 85.0 M (base), 302 M (large)
     flops_per_sample = 6 * enc_linear * L + 12 * L * L * H * NL  # SURVEY §6.2 model
     from ml_recipe_distributed_pytorch_amd import hw_queue_info
-    out = {"metric": metric_name(args.model, L, B, args.precision), "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
+    out = {"metric": metric_name(args.model, L, B, args.precision, S), "value": round(value, 2), "unit": "samples/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
            "vs_baseline": (round(value / (BASELINE_VALUE * world), 4) if BASELINE_VALUE else None), "dtype": args.precision,
            "data": "synthetic (dummy-QA generator, random-init weights)",
            "config": {"model": args.model, "global_batch": B * world, "per_gpu_batch": B, "seq_len": L,
+                      "batch_split": S, "micro_batch": B // S,
                       "parallelism": f"dp{world}", "allreduce_dtype": args.allreduce_dtype,
                       "bucket_cap_mb": args.bucket_cap_mb,
                       "rccl_channels": os.environ.get("NCCL_MIN_NCHANNELS")},

@@ -36,17 +36,23 @@ def build_trainer(params, model_params, device, *, rank: int, local_idx: int, us
                                             seed=params.seed, precision=params.precision)
     optimizer = factories.init_optimizer(params, model)
     auto = getattr(params, "auto_batch_split", None)
-    if device.type == "cuda" and auto is not False:  # default on for GPUs (None), off on CPU
+    if device.type == "cuda" and auto is not False:  # GPUs: on by default (raise-only), off on CPU
         from ..train.memory import device_hbm_bytes, estimate, plan_batch_split
         hbm = device_hbm_bytes(device)
-        split = plan_batch_split(model.config, params.max_seq_len, params.train_batch_size, hbm, params.batch_split)
+        merge = auto == "merge"
+        split = plan_batch_split(model.config, params.max_seq_len, params.train_batch_size, hbm, params.batch_split,
+                                 merge=merge)
         micro = params.train_batch_size // split
+        log = logging.getLogger(__name__)
         if split != params.batch_split:
-            logging.getLogger(__name__).info(
-                f"auto_batch_split: batch_split {params.batch_split} -> {split} (micro-batch "
-                f"{params.train_batch_size // params.batch_split} -> {micro}, modelled "
-                f"{estimate(model.config, params.max_seq_len).total(micro) / 1e9:.1f} GB of {hbm / 1e9:.0f} GB HBM; "
-                f"--auto_batch_split False keeps the configured split)")
+            log.info(f"auto_batch_split: batch_split {params.batch_split} -> {split} (micro-batch "
+                     f"{params.train_batch_size // params.batch_split} -> {micro}, modelled "
+                     f"{estimate(model.config, params.max_seq_len).total(micro) / 1e9:.1f} GB of {hbm / 1e9:.0f} GB HBM; "
+                     f"--auto_batch_split False keeps the configured split)")
+        if split < params.batch_split:
+            log.warning("auto_batch_split=merge: micro-batches merged, so the loss is no longer the reference's mean of "
+                        "per-micro-batch means (span CE over valid spans, weighted class CE, batchmean KL are "
+                        "normalised over the merged batch) — drop 'merge' for the reference objective")
         params.batch_split = split
     dist_rank = rank if hqdist.info().distributed else -1
     if dist_rank in (-1, 0):  # prepare (and cache) the dataset in the main process first
@@ -70,7 +76,8 @@ def build_trainer(params, model_params, device, *, rank: int, local_idx: int, us
                    no_sync_accum=bool(params.no_sync_accum), log_every=params.log_every, profile=params.profile,
                    cuda_graph=bool(getattr(params, "cuda_graph", False)),
                    eval_shard=params.eval_shard, precision=params.precision,
-                   torch_profile_dir=params.torch_profile_dir, torch_profile_steps=params.torch_profile_steps)
+                   torch_profile_dir=params.torch_profile_dir, torch_profile_steps=params.torch_profile_steps,
+                   sampler_seed=params.seed if params.seed is not None else 0)
 
 
 def run_worker(local_idx, plan, params, model_params):

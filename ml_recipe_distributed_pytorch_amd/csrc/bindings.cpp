@@ -187,9 +187,13 @@ Tensor gemm_nt(Tensor A, Tensor B, int64_t epi, c10::optional<Tensor> bias, c10:
     TORCH_CHECK(part->numel() == (int64_t)hq_gemm_nt_part_rows((int)M, (int)N, (int)K) * N,
                 "gemm_nt: part must hold [gemm_nt_part_rows(M, N, K), N]");
   }
+  // split-K slabs (128² kernel, low-fill long-K grids) from the stream-aware caching allocator: safe beside
+  // other streams and inside graph captures once the shape has run eagerly
+  const size_t wsf = hq_gemm_nt_ws_floats((int)M, (int)N, (int)K, (int)epi);
+  Tensor ws = wsf ? at::empty({(int64_t)wsf}, A.options().dtype(at::kFloat)) : Tensor();
   hq_gemm_nt(ptr<uint16_t>(A), ptr<uint16_t>(B), ptr<uint16_t>(C), optr<float>(bias), optr<uint16_t>(pre),
              optr<uint16_t>(resid), optr<float>(part), (int)M, (int)N, (int)K, (int)K, (int)K, (int)N, (int)epi, bn,
-             cur_stream(), (float)p, u32(seed), u32(opid));
+             cur_stream(), (float)p, u32(seed), u32(opid), wsf ? ws.data_ptr<float>() : nullptr);
   return C;
 }
 

@@ -103,9 +103,12 @@ void hq_cu_hog(int blocks, int usec, hipStream_t s);
 // R = residual (EPI_RESID, EPI_BDR); part = [M/256][N] column partial sums (EPI_DGELU)
 // EPI_BDR: C = z = dropout_p(bf16(acc + bias)) + R with the counter-hash stream (seed, opid) at element
 // index m·ldc + n — exactly what ln_fwd computes as z, so the following LayerNorm reads z alone
+// ws: fp32 split-K workspace of hq_gemm_nt_ws_floats(M, N, K, epi) floats (caller-allocated on stream s, e.g.
+// from the stream-aware caching allocator; may be null when that size is 0)
+size_t hq_gemm_nt_ws_floats(int M, int N, int K, int epi);
 void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,
                 float* part, int M, int N, int K, int lda, int ldb, int ldc, int epi, int bn, hipStream_t s,
-                float drop_p = 0.f, uint32_t drop_seed = 0, uint32_t drop_opid = 0);
+                float drop_p = 0.f, uint32_t drop_seed = 0, uint32_t drop_opid = 0, float* ws = nullptr);
 
 // Weight-gradient GEMM (gemm_tn.hip): out[N,K] (+)= Aᵀ·B, A = dy [T,N] bf16, B = x [T,K] bf16 (token-major),
 // split-K over T into S fp32 slabs part[S][N][K] (caller-provided) reduced into out; with bout != null

@@ -1270,20 +1270,6 @@ int nts_ksplit(int tiles, int nk) {
   return ks > 1 ? ks : 1;
 }
 
-float* hq_splitk_ws(size_t n) {   // per-device fp32 scratch for split-K slabs (same stream as its consumer)
-  static std::vector<std::pair<float*, size_t>> bufs;
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  if ((int)bufs.size() <= dev) bufs.resize(dev + 1, {nullptr, 0});
-  auto& b = bufs[dev];
-  if (b.second < n) {
-    float* p = nullptr;
-    if (hipMalloc(&p, n * sizeof(float)) != hipSuccess) { fprintf(stderr, "hq_splitk_ws: hipMalloc failed\n"); abort(); }
-    b = {p, n};   // the old block is kept (kernels may still read it): grows happen a few times per process
-  }
-  return b.first;
-}
-
 constexpr size_t epi_lds(int bn) {
   const size_t stage = 2 * (size_t)(BM * 128 + bn * 128);
   const size_t epi = 8 * 128 * (size_t)(bn / 4 * 2 + 16);
@@ -1292,7 +1278,8 @@ constexpr size_t epi_lds(int bn) {
 
 template <int EPI>
 void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,
-                float* part, int M, int N, int K, int lda, int ldb, int ldc, int bn, hipStream_t s, const HqDropArg& dr) {
+                float* part, int M, int N, int K, int lda, int ldb, int ldc, int bn, hipStream_t s, const HqDropArg& dr,
+                float* ws) {
   if (bn == 1) {   // vS: 128×128 tiles, M tail
     constexpr size_t lds = 2 * 2 * 128 * 128;
     static bool init = [] {
@@ -1301,8 +1288,10 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
     }();
     (void)init;
     const int grid_s = ((M + 127) / 128) * (N / 128);
-    const int ks = nts_ksplit<EPI>(grid_s, K / BK);
-    float* ws = ks > 1 ? hq_splitk_ws((size_t)ks * M * N) : nullptr;
+    int ks = nts_ksplit<EPI>(grid_s, K / BK);
+    if (ks > 1 && !ws) {   // no workspace from the caller: run unsplit rather than share a scratch buffer
+      ks = 1;
+    }
     hipLaunchKernelGGL((gemm_nts_kernel<EPI>), dim3(grid_s * ks), dim3(256), lds, s, A, B, C, bias, P, R, part, M, N, K,
                        lda, ldb, ldc, ks, ws, dr);
     if (ks > 1) {
@@ -1415,22 +1404,35 @@ int hq_gemm_nt_part_rows(int M, int N, int K) {
   return k == 1 ? (M + 127) / 128 : M / BM;
 }
 
+size_t hq_gemm_nt_ws_floats(int M, int N, int K, int epi) {
+  if (hq_gemm_nt_supported(M, N, K) != 1) return 0;   // split-K exists on the 128² (vS) kernel only
+  const int grid_s = ((M + 127) / 128) * (N / 128);
+  int ks = 1;
+  switch (epi) {
+    case HQ_EPI_NONE: ks = nts_ksplit<HQ_EPI_NONE>(grid_s, K / BK); break;
+    case HQ_EPI_BIAS: ks = nts_ksplit<HQ_EPI_BIAS>(grid_s, K / BK); break;
+    case HQ_EPI_RESID: ks = nts_ksplit<HQ_EPI_RESID>(grid_s, K / BK); break;
+    default: ks = 1;
+  }
+  return ks > 1 ? (size_t)ks * M * N : 0;
+}
+
 void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* bias, uint16_t* P, const uint16_t* R,
                 float* part, int M, int N, int K, int lda, int ldb, int ldc, int epi, int bn, hipStream_t s, float drop_p,
-                uint32_t drop_seed, uint32_t drop_opid) {
+                uint32_t drop_seed, uint32_t drop_opid, float* ws) {
   HqDropArg dr{hq_drop_key(drop_seed, drop_opid), 0u, 1.f};
   if (epi == HQ_EPI_BDR && drop_p > 0.f) {
     dr.thr = hq_threshold(drop_p);
     dr.ks = hq_keep_scale(dr.thr);
   }
   switch (epi) {
-    case HQ_EPI_NONE: launch_epi<HQ_EPI_NONE>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
-    case HQ_EPI_BIAS: launch_epi<HQ_EPI_BIAS>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
-    case HQ_EPI_GELU: launch_epi<HQ_EPI_GELU>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
-    case HQ_EPI_DGELU: launch_epi<HQ_EPI_DGELU>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
-    case HQ_EPI_RESID: launch_epi<HQ_EPI_RESID>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
-    case HQ_EPI_GELUD: launch_epi<HQ_EPI_GELUD>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
-    case HQ_EPI_DMUL: launch_epi<HQ_EPI_DMUL>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
-    case HQ_EPI_BDR: launch_epi<HQ_EPI_BDR>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr); break;
+    case HQ_EPI_NONE: launch_epi<HQ_EPI_NONE>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr, ws); break;
+    case HQ_EPI_BIAS: launch_epi<HQ_EPI_BIAS>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr, ws); break;
+    case HQ_EPI_GELU: launch_epi<HQ_EPI_GELU>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr, ws); break;
+    case HQ_EPI_DGELU: launch_epi<HQ_EPI_DGELU>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr, ws); break;
+    case HQ_EPI_RESID: launch_epi<HQ_EPI_RESID>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr, ws); break;
+    case HQ_EPI_GELUD: launch_epi<HQ_EPI_GELUD>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr, ws); break;
+    case HQ_EPI_DMUL: launch_epi<HQ_EPI_DMUL>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr, ws); break;
+    case HQ_EPI_BDR: launch_epi<HQ_EPI_BDR>(A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc, bn, s, dr, ws); break;
   }
 }

@@ -67,15 +67,18 @@ def head_views(store, which: str) -> List[torch.Tensor]:
     return [store.view(k, which) for k in _W_KEYS]
 
 
-def fused_heads_available(model, seq: torch.Tensor) -> bool:
+def fused_heads_possible(model) -> bool:
+    """The model's forward will take the fused head kernels on a bf16 GPU sequence (config / flags only)."""
     cfg = model.config
     if os.environ.get("HQ_FUSED_HEADS", "1") == "0":
-        return False
-    if not (seq.is_cuda and seq.dtype == torch.bfloat16):
         return False
     if cfg.hidden_size % 64 or cfg.hidden_size > 2048 or not 1 <= cfg.num_labels <= 8:
         return False
     return all(model.store.params[k].requires_grad for k in _W_KEYS)
+
+
+def fused_heads_available(model, seq: torch.Tensor) -> bool:
+    return seq.is_cuda and seq.dtype == torch.bfloat16 and fused_heads_possible(model)
 
 
 class _FusedHeadsFn(torch.autograd.Function):
@@ -108,6 +111,14 @@ class _FusedHeadsFn(torch.autograd.Function):
                 dheads[:, 8] = d_rs.float()
             if d_re is not None:
                 dheads[:, 9] = d_re.float()
+            if st.gscale is not None and st.dlog is not None:
+                # the fused loss handed its UNSCALED d(loss)/d(preds) buffers to autograd (the fast path scales
+                # them in the kernel); here autograd has summed them with other gradients, so add the missing
+                # (g - 1)·buffer to get g·fused + other
+                c = st.gscale - 1.0
+                dlog = dlog + c * st.dlog
+                dheads[:, :NL] += c * st.dheads[:, :NL]
+                dheads[:, 8:10] += c * st.dheads[:, 8:10]
             gscale = None
         st.gscale = None
         m = st.model

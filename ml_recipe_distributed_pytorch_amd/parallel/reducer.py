@@ -119,6 +119,7 @@ class GradReducer:
         env = os.environ.get("HQ_GEMM_SCHED")
         dynamic = (env == "1") if env in ("0", "1") else (self.world > 1 or self.force)
         kernels().gemm_set_sched(1 if dynamic else 0)
+        self._set_sched = dynamic
         return "dynamic" if dynamic else "static"
 
     def _make_native(self):
@@ -316,4 +317,7 @@ class GradReducer:
         if self._native is not None:
             self._native.synchronize()
             self._native = None
+        if getattr(self, "_set_sched", False):   # back to the single-GPU default (process-wide setting)
+            kernels().gemm_set_sched(0)
+            self._set_sched = False
         self.model.set_grad_listener(None)

@@ -79,12 +79,20 @@ class StepResult:
 
 
 class TrainEngine:
-    """``graph=True`` (GPU, bf16, one micro-batch per step, no gradient reducer): after two eager warm-up
-    steps the forward + loss + backward of a micro-batch is captured once into a HIP graph and replayed for
-    every later batch of the same shape (inputs copied into the captured tensors, the dropout seed written
-    to the model's device seed word); the clip + fused optimizer step stays eager (its learning rate
-    changes every step).  At small micro-batches the step is launch-bound (the reference's 2 × 512):
-    one graph launch replaces ~300 kernel launches.  Other shapes fall back to the eager path."""
+    """``graph=True`` (GPU, bf16 training, no grad side stream, fused QA heads): after two eager warm-up
+    micro-steps, every kind of micro-step is captured once into a HIP graph and replayed for every later
+    micro-batch of the same shape (inputs copied into the captured tensors, the dropout seed written to the
+    model's device seed word).  A micro-step's kind is (fresh, sync):
+
+    * fresh — the first micro-batch of an accumulation cycle overwrites the gradient arena (its graph also
+      holds the Wᵀ refresh of the just-updated weights); later ones accumulate;
+    * sync — the gradient reducer's bucket all-reduces run in it (the accumulation boundary, or every
+      micro-batch with ``no_sync_accum=False``): RCCL collectives on the reducer's comm stream are captured
+      as a fork/join of the capturing stream, so the 8-GPU DP step replays as one graph per micro-batch.
+
+    So batch_split = 1 uses one graph, the reference's 128 × 2 accumulation three (first, middle, last).  The
+    clip + fused optimizer step stays eager (its learning rate changes every step).  At small micro-batches
+    the step is launch-bound (the reference's 2 × 512): one graph launch replaces ~300 kernel launches."""
 
     def __init__(self, model, loss_fn, optimizer, *, scheduler=None, reducer=None, max_grad_norm: float = 1.0,
                  batch_split: int = 1, no_sync_accum: bool = True, profile: bool = False, graph: bool = False):
@@ -100,9 +108,8 @@ class TrainEngine:
         self.micro = 0
         self._timer = PhaseTimer(profile, model.store.device)
         self.graph = bool(graph)
-        self._graph = None
+        self._graphs: Dict[tuple, tuple] = {}   # (shape key, fresh, sync) -> (graph, static_in, static_lab, record)
         self._graph_warm = 0
-        self._static = None
         self.graph_replays = 0
 
     @property
@@ -111,72 +118,102 @@ class TrainEngine:
 
     # ------------------------------------------------------------------ HIP graph path
     def _graph_eligible(self) -> bool:
+        from ..models.heads import fused_heads_possible
         m = self.model
-        return (self.graph and self.batch_split == 1 and self.reducer is None and not self.profile
-                and m.store.device.type == "cuda" and getattr(m, "precision", "bf16") == "bf16"
-                and getattr(m, "grad_side_stream", None) is None and m.training)
+        r = self.reducer
+        return (self.graph and not self.profile and m.store.device.type == "cuda"
+                and getattr(m, "precision", "bf16") == "bf16" and getattr(m, "grad_side_stream", None) is None
+                and m.training
+                # the reference-heads path draws its classifier dropout key on the host: a captured graph
+                # would replay one mask forever (only the fused kernels read the device seed word)
+                and fused_heads_possible(m)
+                and (r is None or (not r.timing and not r.verify)))
 
     @staticmethod
     def _shape_key(inputs, labels):
         return tuple((k, tuple(v.shape), v.dtype) for d in (inputs, labels) for k, v in sorted(d.items())
                      if torch.is_tensor(v))
 
-    def _capture(self, inputs, labels):
+    def _kind(self):
+        k = self.micro % self.batch_split
+        fresh = k == 0
+        boundary = k == self.batch_split - 1
+        sync = self.reducer is not None and (boundary or not self.no_sync_accum)
+        return fresh, sync, boundary
+
+    def _set_fresh(self, fresh: bool):
+        m = self.model
+        if fresh:
+            m.zero_grad()
+        else:
+            for g, _, _ in m.store.group_ranges():
+                m._fresh[g] = False
+
+    def _capture(self, inputs, labels, key, fresh: bool, sync: bool):
         m = self.model
         static_in = {k: v.clone() if torch.is_tensor(v) else v for k, v in inputs.items()}
         static_lab = {k: v.clone() if torch.is_tensor(v) else v for k, v in labels.items()}
         m.use_device_seed(True)
-        m.store._t_dirty = True   # the Wᵀ refresh belongs in the graph: the weights change every step
-        m.zero_grad()             # "fresh" groups: the captured backward overwrites the arena gradients
+        # the Wᵀ refresh of the updated weights belongs in the fresh (first micro-batch) graph only
+        m.store._t_dirty = fresh
+        self._set_fresh(fresh)
+        if self.reducer is not None:
+            self.reducer.prepare(sync=sync)
         side = torch.cuda.Stream(device=m.store.device)
         side.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
         rng = torch.get_rng_state()   # the capture's forward draws a (unused) host seed: keep the stream aligned
         with torch.cuda.graph(g, stream=side):
             loss = self.loss_fn(m(**static_in), static_lab)
-            loss.backward()
+            (loss / self.batch_split).backward()
+            if sync:
+                self.reducer.finalize()   # the comm stream joins the capturing stream inside the graph
         torch.set_rng_state(rng)
         torch.cuda.current_stream().wait_stream(side)
-        self._graph, self._static = g, (static_in, static_lab, self._shape_key(inputs, labels), self.loss_fn.last)
+        self._graphs[key] = (g, static_in, static_lab, self.loss_fn.last)
 
     def _graph_micro_step(self, inputs, labels) -> Optional[StepResult]:
-        if self._graph is None:
-            if self._graph_warm < 2:          # eager warm-up: kernel attributes, Wᵀ copies, allocator pools
-                self._graph_warm += 1
-                return None
-            self._capture(inputs, labels)
-        elif self._shape_key(inputs, labels) != self._static[2]:
-            return None
-        static_in, static_lab, _, record = self._static
+        fresh, sync, boundary = self._kind()
+        key = (self._shape_key(inputs, labels), fresh, sync)
+        if key not in self._graphs:
+            self._capture(inputs, labels, key, fresh, sync)
+        g, static_in, static_lab, record = self._graphs[key]
         for src, dst in ((inputs, static_in), (labels, static_lab)):
             for k, v in src.items():
                 if torch.is_tensor(v):
                     dst[k].copy_(v, non_blocking=True)
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
         self.model.seed_device.fill_(seed)
-        self._timer.reset()
+        if fresh:
+            self._timer.reset()
         self._timer.mark()
-        self._graph.replay()
+        g.replay()
         self.graph_replays += 1
+        # host-side state the replayed kernels changed: every gradient group now accumulates, Wᵀ is fresh
+        self._set_fresh(False)
+        if fresh:
+            self.model.store._t_dirty = False
         self.loss_fn.last = record
         self._timer.mark("bwd")
         self.micro += 1
+        if not boundary:
+            return None
         return self._apply()
 
     def release_graph(self):
-        if self._graph is not None:
+        if self._graphs:
             self.model.use_device_seed(False)
-        self._graph, self._static, self._graph_warm = None, None, 0
+        self._graphs, self._graph_warm = {}, 0
 
     def micro_step(self, inputs, labels) -> Optional[StepResult]:
         """Forward+backward of one micro-batch; runs the optimizer on the accumulation boundary."""
         if self._graph_eligible():
-            res = self._graph_micro_step(inputs, labels)
-            if res is not None:
-                return res
-        elif self._graph is not None:
+            if self._graph_warm >= 2 or self._graphs:
+                return self._graph_micro_step(inputs, labels)
+            self._graph_warm += 1   # eager warm-up: kernel attributes, Wᵀ copies, allocator pools
+        elif self._graphs:
             self.release_graph()
-        if self._graph is not None:   # eager step beside a live graph: host seeds again
+        if self._graphs:   # eager step beside live graphs (an uncaptured shape): host seeds again
             self.model.use_device_seed(False)
             try:
                 return self._eager_micro_step(inputs, labels)

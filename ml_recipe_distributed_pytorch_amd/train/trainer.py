@@ -126,6 +126,7 @@ class Trainer:
     precision: Optional[str] = None
     torch_profile_dir: Optional[str] = None
     torch_profile_steps: str = "3:5"
+    sampler_seed: int = 0   # per-epoch sampler permutation = f(sampler_seed, epoch): reproducible on resume
     extra_state: dict = field(default_factory=dict)
 
     def __post_init__(self):
@@ -176,18 +177,34 @@ class Trainer:
 
     # ------------------------------------------------------------------ setup helpers
     def _init_train_sampler(self):
+        """Every sampler draws its epoch permutation from (sampler_seed, epoch) alone — DistributedSampler via
+        seed + set_epoch, the world-1 samplers via their own torch.Generator re-seeded at each epoch start — so
+        a run resumed from interrupt.ch replays the interrupted epoch's permutation exactly (the global RNG,
+        which dropout seeds consume, is not part of it)."""
         if self.train_dataset is None:
             return None
+        self._sampler_gen = torch.Generator()
         if self.world > 1:
-            sampler = DistributedSampler(self.train_dataset)
+            sampler = DistributedSampler(self.train_dataset, seed=int(self.sampler_seed))
         elif self.train_weights is not None and self.train_weights.get("sampler_weights") is not None:
             w = self.train_weights["sampler_weights"]
             assert len(w) == len(self.train_dataset)
-            sampler = WeightedRandomSampler(w, len(self.train_dataset))
+            sampler = WeightedRandomSampler(w, len(self.train_dataset), generator=self._sampler_gen)
         else:
-            sampler = RandomSampler(self.train_dataset)
+            sampler = RandomSampler(self.train_dataset, generator=self._sampler_gen)
         logger.info(f"Used train sampler: {type(sampler).__name__}.")
         return sampler
+
+    def _seed_sampler(self, epoch_i: int):
+        if isinstance(self.train_sampler, DistributedSampler):
+            self.train_sampler.set_epoch(epoch_i)  # reference never did (D6)
+        elif self.train_sampler is not None:
+            self._sampler_gen.manual_seed(int(self.sampler_seed) * 1_000_003 + int(epoch_i))
+
+    def epoch_indices(self, epoch_i: int):
+        """The sample order of epoch ``epoch_i`` on this rank (re-seeds the sampler, as _train does)."""
+        self._seed_sampler(epoch_i)
+        return list(iter(self.train_sampler))
 
     def _init_dataloader(self, dataset, name, *, batch_size=1, sampler=None, drop_last=False):
         if dataset is None:
@@ -255,8 +272,7 @@ class Trainer:
         from tqdm.auto import tqdm
         self.set_train()
         self.optimizer.zero_grad()
-        if isinstance(self.train_sampler, DistributedSampler):
-            self.train_sampler.set_epoch(epoch_i)  # reference never did (D6)
+        self._seed_sampler(epoch_i)
         self.engine.micro = 0
         avg = {}
         last_t, last_step = time.perf_counter(), self.global_step
@@ -268,15 +284,27 @@ class Trainer:
         if skip:
             # re-enter an interrupted epoch: drop the samples it had consumed (whole optimizer steps)
             micro_bs = int(self.train_batch_size // self.batch_split)
-            rest = list(iter(self.train_sampler))[skip * micro_bs:]
+            rest = self.epoch_indices(epoch_i)[skip * micro_bs:]
             logger.info(f"Resuming epoch {epoch_i} after {skip} consumed micro-batches ({len(rest)} samples left).")
             loader = DataLoader(self.train_dataset, batch_size=micro_bs, num_workers=self.n_jobs, sampler=rest,
                                 drop_last=True, shuffle=False, collate_fn=self.collate_fun,
                                 pin_memory=self.device.type == "cuda")
         self._epoch_start_step = self.global_step - skip // max(1, self.batch_split)
+        # HQ_TRACE_SAMPLES=<file> (tests): append each consumed micro-batch's sample indices as a JSON line
+        trace = os.environ.get("HQ_TRACE_SAMPLES")
+        if trace:
+            order = self.epoch_indices(epoch_i)
+            self._seed_sampler(epoch_i)   # the loader draws the same permutation again
+            trace_mb = int(self.train_batch_size // self.batch_split)
         data = tqdm(loader, desc=f"Train (epoch #{epoch_i} / {self.n_epochs})",
                     disable=self.rank != 0 or not logger.isEnabledFor(logging.INFO))
         for i, (inputs, labels) in enumerate(data):
+            if trace:
+                import json
+                with open(trace, "a") as f:
+                    f.write(json.dumps({"epoch": epoch_i, "rank": self.rank,
+                                        "idx": [int(x) for x in order[(skip + i) * trace_mb:(skip + i + 1) * trace_mb]]})
+                            + "\n")
             inputs, labels = self._to_device((inputs, labels))
             res = self.engine.micro_step(inputs, labels)
             if res is None:

@@ -169,16 +169,20 @@ def get_trainer_parser() -> ArgumentParser:
     parser.add_argument("--no_sync_accum", type=cast2(int), default=1,
                         help="1: all-reduce only at the accumulation boundary (fix of D1); 0: every micro-batch.")
     parser.add_argument("--dist_timeout", type=float, default=1800.0, help="Process-group timeout in seconds.")
-    parser.add_argument("--auto_batch_split", type=_opt_bool, default=None, nargs="?", const=True,
-                        help="GPU only (default on; False disables): pick the smallest --batch_split whose micro-batch "
-                             "train_batch_size // batch_split fits the HBM memory model (train/memory.py) — merges the "
-                             "reference's 128 micro-batches of 2 into one of 256 on a 288 GB MI355X, or raises the "
-                             "split when a micro-batch would not fit.  The per-step gradient is the same mean over "
-                             "train_batch_size samples (up to the per-micro-batch CE normalisation over valid spans).")
+    parser.add_argument("--auto_batch_split", type=_auto_split, default=None, nargs="?", const=True,
+                        help="GPU only.  Default (unset / True): raise --batch_split when a micro-batch "
+                             "train_batch_size // batch_split would not fit the HBM memory model (train/memory.py); "
+                             "never lowers it, so the objective is the reference's.  'merge': also LOWER it to the "
+                             "smallest split that fits (the reference's 128 micro-batches of 2 become one of 256 on a "
+                             "288 GB MI355X) — faster, but the span CE (ignore_index=-1, mean over valid spans), the "
+                             "weighted class CE and the batchmean KL are then normalised over the merged micro-batch "
+                             "instead of averaged per micro-batch.  False: off.")
     parser.add_argument("--profile", action="store_true", help="Per-phase step timers + perf/* TB scalars.")
     parser.add_argument("--cuda_graph", type=_opt_bool, default=False, nargs="?", const=True,
-                        help="GPU, one micro-batch per step, single process: capture the forward+backward into a HIP "
-                             "graph after two warm-up steps and replay it (launch-bound small micro-batches).")
+                        help="GPU, bf16: capture each kind of micro-step (forward + backward; first / middle / last "
+                             "micro-batch of an accumulation cycle, the last one with the gradient all-reduces) into "
+                             "a HIP graph after two eager warm-up micro-steps and replay them (launch-bound small "
+                             "micro-batches, e.g. the reference's 128 x 2).")
     parser.add_argument("--torch_profile_dir", type=cast2(str), default=None,
                         help="Export a torch.profiler Chrome trace of optimizer steps --torch_profile_steps here.")
     parser.add_argument("--torch_profile_steps", type=str, default="3:5",
@@ -191,6 +195,13 @@ def get_trainer_parser() -> ArgumentParser:
     parser.add_argument("--nproc_per_node", type=cast2(int), default=None,
                         help="Processes per node (default: #visible GPUs, or 1 on CPU). On CPU >1 spawns gloo ranks.")
     return parser
+
+
+def _auto_split(v):
+    """--auto_batch_split: None / True (raise only), 'merge' (may lower the split), False (off)."""
+    if isinstance(v, str) and v.strip().lower() == "merge":
+        return "merge"
+    return _opt_bool(v)
 
 
 def _opt_bool(v):

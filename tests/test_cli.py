@@ -73,6 +73,8 @@ def test_train_resume_and_interrupt(tmp_path, monkeypatch):
     assert sorted(lrs) == [5, 6, 7, 8] and all(v > 0 for s_, v in lrs.items() if s_ < 8), lrs
     # fault injection: KeyboardInterrupt at step 3 → interrupt.ch holds step 3
     monkeypatch.setenv("HQ_FAULT", "0:3:interrupt")
+    trace = tmp_path / "samples.jsonl"
+    monkeypatch.setenv("HQ_TRACE_SAMPLES", str(trace))
     cfg3 = _cfg(tmp_path, debug="False", n_epochs="1", train_batch_size="8", batch_split="1",
                 dummy_dataset_len="32", experiment_name="exp3")
     _train(["-c", cfg3, "--dump_dir", str(tmp_path)] + TINY)
@@ -83,6 +85,13 @@ def test_train_resume_and_interrupt(tmp_path, monkeypatch):
     _train(["-c", cfg3, "--dump_dir", str(tmp_path), "--last", str(tmp_path / "exp3" / "interrupt.ch")] + TINY)
     st4 = torch.load(tmp_path / "exp3" / "last.ch", weights_only=True)
     assert st4["global_step"] == 4 and st4["epoch"] == 1 and st4["epoch_complete"] is True
+    # the interrupted run consumed 3 micro-batches, the resumed one the 4th: together exactly one permutation
+    # of the 32 samples, none repeated (the sampler order depends on (seed, epoch) only, not the global RNG)
+    import json
+    rec = [json.loads(x) for x in trace.read_text().splitlines()]
+    assert [r["epoch"] for r in rec] == [1, 1, 1, 1]
+    idx = [i for r in rec for i in r["idx"]]
+    assert sorted(idx) == list(range(32)), idx
 
 
 def test_profiling_outputs(tmp_path):
@@ -181,3 +190,24 @@ def test_reference_config_verbatim_runs(tmp_path):
     ev = list((tmp_path / "board" / "test").glob("events.out.tfevents.*"))
     steps = sorted({s for s, t, _ in read_events(str(ev[0])) if t == "train/loss"})
     assert steps == [1, 2]  # debug: one optimizer step per epoch, two epochs
+
+
+def test_resume_mid_second_epoch_replays_its_permutation(tmp_path, monkeypatch):
+    """Interrupt in epoch 2 (after the first epoch and the dropout seeds have consumed the global RNG): the
+    resumed run must finish exactly the rest of epoch 2's permutation (world 1: RandomSampler)."""
+    import json
+    cfg = _cfg(tmp_path, debug="False", n_epochs="2", train_batch_size="8", batch_split="2",
+               dummy_dataset_len="32", experiment_name="ep2")
+    trace = tmp_path / "s.jsonl"
+    monkeypatch.setenv("HQ_TRACE_SAMPLES", str(trace))
+    monkeypatch.setenv("HQ_FAULT", "0:6:interrupt")
+    _train(["-c", cfg, "--dump_dir", str(tmp_path)] + TINY)
+    st = torch.load(tmp_path / "ep2" / "interrupt.ch", weights_only=True)
+    assert st["global_step"] == 6 and st["epoch"] == 2 and st["epoch_complete"] is False
+    monkeypatch.delenv("HQ_FAULT")
+    _train(["-c", cfg, "--dump_dir", str(tmp_path), "--last", str(tmp_path / "ep2" / "interrupt.ch")] + TINY)
+    rec = [json.loads(x) for x in trace.read_text().splitlines()]
+    e2 = [i for r in rec if r["epoch"] == 2 for i in r["idx"]]
+    assert sorted(e2) == list(range(32)), e2            # 4 micro-batches before, 4 after, no repeats
+    e1 = [i for r in rec if r["epoch"] == 1 for i in r["idx"]]
+    assert sorted(e1) == list(range(32)) and e1 != e2   # a new permutation each epoch

@@ -1,18 +1,22 @@
 """HIP-graph replay of the training step (TrainEngine(graph=True)) against the eager step: same batches,
 same dropout seeds (host-drawn, written to the model's device seed word before each replay), so losses and
-weights must agree (bitwise except the float-atomic embedding-gradient scatter)."""
+weights must agree (bitwise except the float-atomic embedding-gradient scatter).  Covered: one micro-batch
+per step; gradient accumulation (first / middle / last micro-batch graphs); the native RCCL reducer's bucket
+all-reduces captured inside the boundary graph (forced 1-rank communicator); and the reference-heads path,
+which must stay eager (its classifier dropout key is drawn on the host)."""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
 
-def _run(cuda, graph, steps=5, B=2, L=512):
+def _run(cuda, graph, steps=5, B=2, L=512, split=1, reducer=False):
     from types import SimpleNamespace
     from ml_recipe_distributed_pytorch_amd.data.dummy import SpecialIds, synth_batch_native
     from ml_recipe_distributed_pytorch_amd.models.bert import BertForQuestionAnswering
     from ml_recipe_distributed_pytorch_amd.models.config import get_config
     from ml_recipe_distributed_pytorch_amd.models.losses import build_loss
+    from ml_recipe_distributed_pytorch_amd.parallel.reducer import GradReducer
     from ml_recipe_distributed_pytorch_amd.train.engine import TrainEngine, to_device
     from ml_recipe_distributed_pytorch_amd.train.optim import FusedAdamW
     from ml_recipe_distributed_pytorch_amd.train.trainer import optimizer_groups
@@ -22,24 +26,28 @@ def _run(cuda, graph, steps=5, B=2, L=512):
                          w_start_reg=1, w_end_reg=1, w_cls=1)
     opt = FusedAdamW(optimizer_groups(model.named_parameters(), 1e-4), model.store, lr=1e-4, eps=1e-6,
                      correct_bias=False, zero_grad_fn=model.zero_grad)
-    eng = TrainEngine(model, build_loss(lp), opt, max_grad_norm=1.0, graph=graph)
-    torch.manual_seed(77)   # the per-step dropout seeds
+    red = GradReducer(model, bucket_cap_mb=8, force=True) if reducer else None
+    eng = TrainEngine(model, build_loss(lp), opt, max_grad_norm=1.0, graph=graph, batch_split=split, reducer=red)
+    torch.manual_seed(77)   # the per-micro-step dropout seeds
     losses = []
     for i in range(steps):
-        inputs, labels = synth_batch_native(B, L, 64, SpecialIds(), seed=10 + i)
-        res = eng.step([(to_device(inputs, cuda), to_device(labels, cuda))])
+        mbs = []
+        for j in range(split):
+            inputs, labels = synth_batch_native(B, L, 64, SpecialIds(), seed=10 + i * split + j)
+            mbs.append((to_device(inputs, cuda), to_device(labels, cuda)))
+        res = eng.step(mbs)
         losses.append(res.losses["loss"].item())
     torch.cuda.synchronize()
     master = model.store.master.clone()
     replays = eng.graph_replays
+    kinds = sorted((k[1], k[2]) for k in eng._graphs)
     eng.release_graph()
-    return losses, master, replays, model
+    if red is not None:
+        red.close()
+    return losses, master, replays, model, kinds
 
 
-def test_graph_replay_matches_eager(cuda):
-    le, me, r0, model = _run(cuda, graph=False)
-    lg, mg, r1, _ = _run(cuda, graph=True)
-    assert r0 == 0 and r1 == 3          # two eager warm-up steps, then capture + 3 replays
+def _same(model, le, me, lg, mg):
     for a, b in zip(le, lg):
         assert a == pytest.approx(b, rel=1e-5, abs=1e-6)
     atomic = torch.zeros_like(me, dtype=torch.bool)
@@ -48,3 +56,40 @@ def test_graph_replay_matches_eager(cuda):
             atomic[e.offset:e.offset + e.numel] = True
     assert torch.equal(mg[~atomic], me[~atomic]) or torch.allclose(mg, me, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(mg[atomic], me[atomic], rtol=1e-4, atol=1e-6)
+
+
+def test_graph_replay_matches_eager(cuda):
+    le, me, r0, model, _ = _run(cuda, graph=False)
+    lg, mg, r1, _, kinds = _run(cuda, graph=True)
+    assert r0 == 0 and r1 == 3          # two eager warm-up steps, then capture + 3 replays
+    assert kinds == [(True, False)]
+    _same(model, le, me, lg, mg)
+
+
+def test_graph_replay_with_accumulation(cuda):
+    """batch_split 4: the first micro-batch overwrites the arena (and refreshes Wᵀ in its graph), the middle
+    ones and the last accumulate — three graphs, replayed 4 × 4 − 2 times."""
+    le, me, _, model, _ = _run(cuda, graph=False, steps=4, split=4)
+    lg, mg, r1, _, kinds = _run(cuda, graph=True, steps=4, split=4)
+    assert r1 == 14 and kinds == [(False, False), (True, False)]
+    _same(model, le, me, lg, mg)
+
+
+def test_graph_replay_with_reducer_and_accumulation(cuda):
+    """The forced 1-rank native RCCL reducer: its bucket all-reduces (fence → ncclAllReduce on the comm
+    stream → join) are captured in the boundary micro-batch's graph; averaging over one rank is the identity,
+    so graph + reducer must equal eager without a reducer."""
+    le, me, _, model, _ = _run(cuda, graph=False, steps=4, split=3)
+    lg, mg, r1, _, kinds = _run(cuda, graph=True, steps=4, split=3, reducer=True)
+    assert r1 == 10 and kinds == [(False, False), (False, True), (True, False)]
+    _same(model, le, me, lg, mg)
+
+
+def test_graph_not_used_with_reference_heads(cuda, monkeypatch):
+    """HQ_FUSED_HEADS=0: the autograd heads draw their classifier-dropout key on the host, so a graph would
+    freeze one mask — the engine must stay eager and match the plain eager run."""
+    monkeypatch.setenv("HQ_FUSED_HEADS", "0")
+    le, me, _, model, _ = _run(cuda, graph=False, steps=3)
+    lg, mg, r1, _, _ = _run(cuda, graph=True, steps=3)
+    assert r1 == 0
+    _same(model, le, me, lg, mg)

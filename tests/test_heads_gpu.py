@@ -114,6 +114,33 @@ def test_fused_heads_general_gradient_path(cuda):
     _close(res[0][1], res[1][1], "dseq", rtol=1e-2, atol=1e-2)
 
 
+def test_fused_loss_plus_extra_term_scales_correctly(cuda):
+    """fused loss × 1/3 + an extra objective on the same predictions: autograd sums the fused loss's unscaled
+    buffers with the extra gradient, so the heads backward takes the general path and must add the missing
+    (g − 1)·buffer (models/heads.py) — against the all-autograd reference heads + loss modules."""
+    B, L, H, NL = 24, 48, 768, 5
+    m = _model(cuda, H=H, NL=NL, p=0.0)
+    seq0 = (torch.randn(B, L, H, device=cuda) * 0.8).to(torch.bfloat16)
+    t = _targets(cuda, B, L, NL)
+    from ml_recipe_distributed_pytorch_amd.models.heads import fused_heads, reference_heads
+    res = []
+    for fused in (True, False):
+        loss_fn = _loss("ce", NL)
+        seq = seq0.clone().requires_grad_(True)
+        m.zero_grad()
+        if not fused:
+            m.store.grad.zero_()
+            loss_fn._fused_cfg = None
+        out = (fused_heads if fused else reference_heads)(m, seq, 7, True)
+        obj = loss_fn(out, t) / 3 + 0.25 * (out["start_class"] ** 2).mean() + out["cls"][:, 2].sum()
+        obj.backward()
+        torch.cuda.synchronize()
+        res.append((_head_grads(m), seq.grad.float()))
+    for k in res[1][0]:
+        _close(res[0][0][k], res[1][0][k], "grad " + k, rtol=1e-3, atol=1e-4)
+    _close(res[0][1], res[1][1], "dseq", rtol=1e-2, atol=1e-2)
+
+
 def test_fused_heads_accumulate_and_eval(cuda):
     """Two micro-batches accumulate into the arena (no zero_grad between); eval uses p = 0 and the
     fused loss also runs under no_grad (validation)."""
