@@ -48,7 +48,10 @@ def parse():
     ap.add_argument("--model", default="bert-base-uncased")
     ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
-                    help="compute precision; fp8 = OCP e4m3 forward projections (BASELINE config #5)")
+                    help="compute precision; fp8 = OCP e4m3 forward projections and e5m2-gradient dgrads "
+                         "(BASELINE config #5)")
+    ap.add_argument("--fp8_dgrad", type=int, default=1, choices=[0, 1],
+                    help="with --precision fp8: 0 keeps the backward dgrads in bf16 (A/B of the fp8 backward)")
     ap.add_argument("--bucket_cap_mb", type=float, default=32.0)
     ap.add_argument("--profile", action="store_true", help="per-phase timers (adds syncs; not for the headline)")
     ap.add_argument("--graph", action="store_true",
@@ -112,6 +115,7 @@ def main():
 
     cfg = get_config(args.model)
     model = BertForQuestionAnswering(cfg, seed=1234, precision=args.precision).to(device).train()
+    model.fp8_dgrad = bool(args.fp8_dgrad)
     # config/test_bert.cfg: loss=smooth(0.01), all five loss weights 1, lr 1e-5, wd 1e-4, clip 1
     lp = SimpleNamespace(loss="smooth", smooth_alpha=0.01, focal_alpha=1, focal_gamma=2, w_start=1, w_end=1,
                          w_start_reg=1, w_end_reg=1, w_cls=1)
@@ -205,7 +209,8 @@ def main():
                       "batch_split": S, "micro_batch": B // S,
                       "parallelism": f"dp{world}", "allreduce_dtype": args.allreduce_dtype,
                       "bucket_cap_mb": args.bucket_cap_mb,
-                      "rccl_channels": os.environ.get("NCCL_MIN_NCHANNELS")},
+                      "rccl_channels": os.environ.get("NCCL_MIN_NCHANNELS"),
+                      "fp8_dgrad": bool(args.fp8_dgrad) if args.precision == "fp8" else None},
            "world_size": dist.get_world_size() if dist.is_initialized() else 1,
            "process_group": backend or "none",
            "rccl_comm_ranks": reducer.comm_ranks if reducer is not None else None,

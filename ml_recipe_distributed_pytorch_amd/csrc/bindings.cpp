@@ -121,9 +121,10 @@ std::vector<Tensor> ln_fwd(Tensor a, c10::optional<Tensor> resid_opt, Tensor gam
   return {y, z, mean, rstd};
 }
 
+// q8 (f32[4] delayed-scaling state of the fp8 dgrad GEMM that consumes da): also returns da as e5m2
 std::vector<Tensor> ln_bwd(Tensor dy, c10::optional<Tensor> dy2, Tensor z, Tensor gamma, Tensor mean, Tensor rstd, double p,
                            int64_t seed, int64_t opid, c10::optional<Tensor> g_gamma, c10::optional<Tensor> g_beta,
-                           c10::optional<Tensor> g_bias, bool accumulate) {
+                           c10::optional<Tensor> g_bias, bool accumulate, c10::optional<Tensor> q8, int64_t phase) {
   check(dy, BF16, "dy"); check_opt(dy2, BF16, "dy2"); check(z, BF16, "z"); check(gamma, F32, "gamma");
   check(mean, F32, "mean"); check(rstd, F32, "rstd");
   check_opt(g_gamma, F32, "g_gamma"); check_opt(g_beta, F32, "g_beta"); check_opt(g_bias, F32, "g_bias");
@@ -135,10 +136,20 @@ std::vector<Tensor> ln_bwd(Tensor dy, c10::optional<Tensor> dy2, Tensor z, Tenso
   auto dz = at::empty_like(dy), da = at::empty_like(dy);
   const int nb = hq_ln_bwd_partials((int)T);
   auto part = at::empty({nb, 3 * H}, gamma.options());
+  const bool want8 = q8.has_value() && q8->defined();
+  Tensor da8;
+  if (want8) {
+    check(*q8, F32, "q8");
+    TORCH_CHECK(q8->numel() == 4, "ln_bwd: q8 must be f32[4]");
+    TORCH_CHECK(H % 4 == 0, "ln_bwd: e5m2 output needs H % 4 == 0");
+    da8 = at::empty(dy.sizes(), dy.options().dtype(at::kFloat8_e5m2));
+  }
   hq_ln_bwd(ptr<uint16_t>(dy), optr<uint16_t>(dy2), ptr<uint16_t>(z), ptr<float>(gamma), ptr<float>(mean), ptr<float>(rstd),
             ptr<uint16_t>(dz), ptr<uint16_t>(da), ptr<float>(part),
             outs4(optr<float>(g_gamma), optr<float>(g_beta), optr<float>(g_bias)), (int)T, (int)H, (float)p, u32(seed),
-            u32(opid), accumulate, cur_stream());
+            u32(opid), accumulate, cur_stream(), want8 ? reinterpret_cast<uint8_t*>(da8.data_ptr()) : nullptr,
+            want8 ? ptr<float>(*q8) : nullptr, (int)(phase % 3));
+  if (want8) return {dz, da, da8};
   return {dz, da};
 }
 
@@ -221,31 +232,52 @@ void gemm_tn(Tensor dy, Tensor x, Tensor out, bool accumulate, int64_t splits, c
              has_bias ? ptr<float>(*bias_out) : nullptr, (int)T, (int)N, (int)K, S, accumulate, cur_stream());
 }
 
-// fp8 forward projection: C (bf16) = A8·B8ᵀ·sa·sb + bias (f32); GELUD: returns act, writes gelu' into `pre`
-// and, with out8/state given, act as e4m3 (delayed scaling, state f32[4], phase = step % 3).
+// fp8 projection GEMM, C (bf16) = A8·B8ᵀ·sa·sb (+ epilogue), B8 e4m3.  Forward (A8 e4m3): BIAS / GELUD
+// (+ bias f32; GELUD returns act, writes gelu' into `pre` and, with out8/state given, act as e4m3).
+// Backward dgrad (A8 e5m2): NONE / DMUL (C ⊙ pre, column sums into part [M/256, N]; with out8/state,
+// C also as e5m2).  Delayed scaling: state f32[4], phase = step % 3.
 int64_t gemm_fp8_supported(int64_t M, int64_t N, int64_t K) { return hq_gemm_fp8_supported((int)M, (int)N, (int)K); }
 
-Tensor gemm_fp8(Tensor A8, Tensor B8, int64_t epi, Tensor bias, Tensor sa, Tensor sb, c10::optional<Tensor> pre,
-                c10::optional<Tensor> out8, c10::optional<Tensor> state, int64_t phase) {
+Tensor gemm_fp8(Tensor A8, Tensor B8, int64_t epi, c10::optional<Tensor> bias, Tensor sa, Tensor sb,
+                c10::optional<Tensor> pre, c10::optional<Tensor> out8, c10::optional<Tensor> state, int64_t phase,
+                c10::optional<Tensor> part) {
   TORCH_CHECK(A8.is_cuda() && A8.element_size() == 1 && A8.is_contiguous() && B8.is_cuda() && B8.element_size() == 1 &&
-              B8.is_contiguous(), "gemm_fp8: A8 / B8 must be contiguous 1-byte (e4m3) GPU tensors");
+              B8.is_contiguous(), "gemm_fp8: A8 / B8 must be contiguous 1-byte (fp8) GPU tensors");
   TORCH_CHECK(A8.dim() == 2 && B8.dim() == 2 && A8.size(1) == B8.size(1), "gemm_fp8: A8[M,K], B8[N,K]");
+  TORCH_CHECK(B8.scalar_type() == at::kFloat8_e4m3fn, "gemm_fp8: B8 (weights) must be float8_e4m3fn");
   const int64_t M = A8.size(0), K = A8.size(1), N = B8.size(0);
   TORCH_CHECK(hq_gemm_fp8_supported((int)M, (int)N, (int)K), "gemm_fp8: unsupported shape M=", M, " N=", N, " K=", K);
-  TORCH_CHECK(epi == HQ_EPI_BIAS || epi == HQ_EPI_GELUD, "gemm_fp8: epilogue must be BIAS or GELUD");
-  check(bias, F32, "bias"); check(sa, F32, "sa"); check(sb, F32, "sb");
-  TORCH_CHECK(bias.numel() == N && sa.numel() >= 1 && sb.numel() >= 1, "gemm_fp8: bias[N], sa, sb");
+  const bool fwd = epi == HQ_EPI_BIAS || epi == HQ_EPI_GELUD, bwd = epi == HQ_EPI_NONE || epi == HQ_EPI_DMUL;
+  TORCH_CHECK(fwd || bwd, "gemm_fp8: epilogue must be BIAS / GELUD (forward) or NONE / DMUL (dgrad)");
+  TORCH_CHECK(A8.scalar_type() == (fwd ? at::kFloat8_e4m3fn : at::kFloat8_e5m2),
+              "gemm_fp8: A8 must be float8_e4m3fn for the forward epilogues, float8_e5m2 for the dgrad ones");
+  check(sa, F32, "sa"); check(sb, F32, "sb");
+  TORCH_CHECK(sa.numel() >= 1 && sb.numel() >= 1, "gemm_fp8: sa, sb");
+  if (fwd) {
+    TORCH_CHECK(bias.has_value() && bias->defined(), "gemm_fp8: forward epilogues need the fp32 bias");
+    check(*bias, F32, "bias");
+    TORCH_CHECK(bias->numel() == N, "gemm_fp8: bias[N]");
+  }
   c10::DeviceGuard g(A8.device());
   Tensor C = at::empty({M, N}, A8.options().dtype(BF16));
   uint16_t* P = nullptr;
   uint8_t* C8 = nullptr;
   float* q8 = nullptr;
-  if (epi == HQ_EPI_GELUD) {
-    TORCH_CHECK(pre.has_value() && pre->defined(), "gemm_fp8: GELUD needs `pre` (gelu' output)");
+  float* pp = nullptr;
+  if (epi == HQ_EPI_DMUL) {
+    TORCH_CHECK(part.has_value() && part->defined(), "gemm_fp8: DMUL needs `part` [M/256, N]");
+    check(*part, F32, "part");
+    TORCH_CHECK(part->numel() == (M / 256) * N, "gemm_fp8: part must hold [M/256, N]");
+    pp = ptr<float>(*part);
+  }
+  if (epi == HQ_EPI_GELUD || epi == HQ_EPI_DMUL) {
+    TORCH_CHECK(pre.has_value() && pre->defined(), "gemm_fp8: GELUD / DMUL need `pre` (gelu')");
     check(*pre, BF16, "pre");
     TORCH_CHECK(pre->size(0) == M && pre->size(1) == N, "gemm_fp8: pre shape");
     P = ptr<uint16_t>(*pre);
     if (out8.has_value() && out8->defined()) {
+      TORCH_CHECK(out8->scalar_type() == (fwd ? at::kFloat8_e4m3fn : at::kFloat8_e5m2),
+                  "gemm_fp8: out8 must be float8_e4m3fn (GELUD) / float8_e5m2 (DMUL)");
       TORCH_CHECK(out8->is_cuda() && out8->element_size() == 1 && out8->is_contiguous() && out8->numel() == M * N,
                   "gemm_fp8: out8 must be a contiguous 1-byte [M,N] tensor");
       TORCH_CHECK(state.has_value() && state->defined(), "gemm_fp8: out8 needs the delayed-scaling state");
@@ -256,8 +288,8 @@ Tensor gemm_fp8(Tensor A8, Tensor B8, int64_t epi, Tensor bias, Tensor sa, Tenso
     }
   }
   hq_gemm_fp8(reinterpret_cast<const uint8_t*>(A8.data_ptr()), reinterpret_cast<const uint8_t*>(B8.data_ptr()), ptr<uint16_t>(C),
-              ptr<float>(bias), P, ptr<float>(sa), ptr<float>(sb), C8, q8, (int)(phase % 3), (int)M, (int)N, (int)K,
-              (int)epi, cur_stream());
+              optr<float>(bias), P, ptr<float>(sa), ptr<float>(sb), C8, q8, (int)(phase % 3), (int)M, (int)N, (int)K,
+              (int)epi, cur_stream(), pp);
   return C;
 }
 
@@ -294,6 +326,17 @@ void transpose_tiles(Tensor src, Tensor dst, Tensor tiles) {
               tiles.size(1) == 6, "tiles must be a contiguous int32 [n,6] GPU tensor");
   c10::DeviceGuard g(src.device());
   hq_transpose_tiles(ptr<uint16_t>(src), ptr<uint16_t>(dst), ptr<int>(tiles), (int)tiles.size(0), cur_stream());
+}
+
+// fp8 weights (1-byte elements): the e4m3 Wᵀ copies for the fp8 dgrad GEMMs
+void transpose_tiles8(Tensor src, Tensor dst, Tensor tiles) {
+  TORCH_CHECK(src.is_cuda() && dst.is_cuda() && src.element_size() == 1 && dst.element_size() == 1 && src.is_contiguous() &&
+              dst.is_contiguous(), "transpose_tiles8: contiguous 1-byte GPU tensors");
+  TORCH_CHECK(tiles.device().is_cuda() && tiles.scalar_type() == at::kInt && tiles.is_contiguous() && tiles.dim() == 2 &&
+              tiles.size(1) == 6, "tiles must be a contiguous int32 [n,6] GPU tensor");
+  c10::DeviceGuard g(src.device());
+  hq_transpose_tiles8(reinterpret_cast<const uint8_t*>(src.data_ptr()), reinterpret_cast<uint8_t*>(dst.data_ptr()),
+                      ptr<int>(tiles), (int)tiles.size(0), cur_stream());
 }
 
 // out (+)= Σ_rows part.  `part` is scratch: the two-pass reduction overwrites some of its rows.
@@ -602,7 +645,9 @@ PYBIND11_MODULE(_hq_kernels, m) {
         py::arg("accumulate"), py::arg("pad_word"), py::arg("pad_pos"), py::arg("seq_len") = 0);
   m.def("ln_fwd", &ln_fwd, py::arg("a"), py::arg("resid"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("p"),
         py::arg("seed"), py::arg("opid"), py::arg("q8") = py::none(), py::arg("phase") = 0);
-  m.def("ln_bwd", &ln_bwd);
+  m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("dy2"), py::arg("z"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
+        py::arg("p"), py::arg("seed"), py::arg("opid"), py::arg("g_gamma"), py::arg("g_beta"), py::arg("g_bias"),
+        py::arg("accumulate"), py::arg("q8") = py::none(), py::arg("phase") = 0);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("epi"), py::arg("bias") = py::none(),
         py::arg("pre") = py::none(), py::arg("resid") = py::none(), py::arg("part") = py::none(),
@@ -622,6 +667,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("gemm_tn_splits", &gemm_tn_splits);
   m.def("attn_set_force_slow", [](int64_t v) { hq_attn_set_force_slow((int)v); });
   m.def("transpose_tiles", &transpose_tiles);
+  m.def("transpose_tiles8", &transpose_tiles8);
   m.def("colsum_into", &colsum_into);
   m.def("fp8_quantize", &fp8_quantize);
   m.def("fp8_quant_delayed", &fp8_quant_delayed);
@@ -629,7 +675,8 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("fp8_quant_multi_blocks", &fp8_quant_multi_blocks);
   m.def("gemm_fp8_supported", &gemm_fp8_supported);
   m.def("gemm_fp8", &gemm_fp8, py::arg("A8"), py::arg("B8"), py::arg("epi"), py::arg("bias"), py::arg("sa"), py::arg("sb"),
-        py::arg("pre") = py::none(), py::arg("out8") = py::none(), py::arg("state") = py::none(), py::arg("phase") = 0);
+        py::arg("pre") = py::none(), py::arg("out8") = py::none(), py::arg("state") = py::none(), py::arg("phase") = 0,
+        py::arg("part") = py::none());
   m.def("span_fwd", &span_fwd);
   m.def("span_bwd", &span_bwd);
   m.def("set_dropout_seed", [](c10::optional<Tensor> t) {

@@ -208,10 +208,19 @@ __device__ __forceinline__ void hq_keep4(uint32_t idx0, uint32_t key, uint32_t t
 // 4-float state per quantisation site: slots 0-2 rotate as (this step's amax, next step's (cleared), last
 // step's amax) by phase = step % 3; state[3] = the scale this step's e4m3 tensor was written with.
 // s = 2·amax_prev / 448 (unit scale before the first amax exists).
-constexpr float kHqFp8Max = 448.f;
-__device__ __forceinline__ float hq_fp8_delayed_scale(const float* st, int phase) {
+constexpr float kHqFp8Max = 448.f;      // OCP e4m3 (forward activations / weights)
+constexpr float kHqBf8Max = 57344.f;    // OCP e5m2 (backward activation gradients)
+__device__ __forceinline__ float hq_fp8_delayed_scale(const float* st, int phase, float fmax = kHqFp8Max) {
   const float prev = __uint_as_float(reinterpret_cast<const unsigned*>(st)[(phase + 2) % 3]);
-  return prev > 0.f ? prev * 2.f / kHqFp8Max : 1.f;
+  return prev > 0.f ? prev * 2.f / fmax : 1.f;
+}
+// 4 values -> 4 e5m2 bytes (x·inv, saturated to ±57344)
+__device__ __forceinline__ uint32_t hq_pack_bf8x4(const float* f, float inv) {
+  float g[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) g[i] = fminf(fmaxf(f[i] * inv, -kHqBf8Max), kHqBf8Max);
+  uint32_t w = __builtin_amdgcn_cvt_pk_bf8_f32(g[0], g[1], 0, false);
+  return __builtin_amdgcn_cvt_pk_bf8_f32(g[2], g[3], w, true);
 }
 // 4 values -> 4 e4m3 bytes (x·inv, saturated to ±448)
 __device__ __forceinline__ uint32_t hq_pack_fp8x4(const float* f, float inv) {

@@ -26,9 +26,11 @@ int hq_rowblock_partials(int T);
 void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, const float* beta, uint16_t* y, uint16_t* z,
                float* mean, float* rstd, int T, int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s,
                uint8_t* y8 = nullptr, float* q8 = nullptr, int phase = 0);
+// da8 != null (--precision fp8 backward): da also as e5m2 under the delayed-scaling state q8 at `phase`
 void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const float* gamma, const float* mean,
                const float* rstd, uint16_t* dz, uint16_t* da, float* part, HqOuts outs, int T, int H, float p,
-               uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s);
+               uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s, uint8_t* da8 = nullptr,
+               float* q8 = nullptr, int phase = 0);
 void hq_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww, const uint16_t* wp,
                   const uint16_t* wt, const float* gamma, const float* beta, uint16_t* y, float* mean, float* rstd, int T,
                   int H, float eps, float p, uint32_t seed, uint32_t opid, int V, int P, int NTY, hipStream_t s);
@@ -119,23 +121,27 @@ int hq_gemm_tn_splits(int T, int N, int K);
 void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, float* bpart, float* bout, int T, int N, int K,
                 int S, bool accumulate, hipStream_t s);
 
-// fp8 (OCP e4m3) NT GEMM (gemm_fp8.hip): C = A8·B8ᵀ·sa·sb + bias, epi ∈ {HQ_EPI_BIAS, HQ_EPI_GELUD};
-// with C8 != null (GELUD) also act as e4m3 under delayed scaling driven by the 4-float state q8 / phase.
+// fp8 NT GEMM (gemm_fp8.hip): C = A8·B8ᵀ·sa·sb (+ epilogue), B8 e4m3.  Forward epi ∈ {HQ_EPI_BIAS,
+// HQ_EPI_GELUD} with A8 e4m3; backward epi ∈ {HQ_EPI_NONE, HQ_EPI_DMUL (C ⊙ P, column sums into
+// part[M/256][N])} with A8 e5m2.  C8 != null (GELUD / DMUL): the output also as e4m3 / e5m2 under
+// delayed scaling driven by the 4-float state q8 / phase.
 int hq_gemm_fp8_supported(int M, int N, int K);
 void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, uint16_t* P, const float* sa,
-                 const float* sb, uint8_t* C8, float* q8, int phase, int M, int N, int K, int epi, hipStream_t s);
+                 const float* sb, uint8_t* C8, float* q8, int phase, int M, int N, int K, int epi, hipStream_t s,
+                 float* part = nullptr);
 // delayed-scaling e4m3 quantiser (one pass): y = x / s(prev amax), amax tracked in q8 (see gemm_fp8.hip)
 void hq_fp8_quant_delayed(const uint16_t* x, uint8_t* y, size_t n, float* q8, int phase, hipStream_t s);
 long long hq_fp8_quant_multi_blocks(long long n8);   // blocks of one segment of n8 8-element groups
 // fp8 producers write per-wave amax partials into this device scratch (>= n floats, current device) and
 // hq_fp8_amax_fold folds them into the delayed-scaling state q8 (slot `phase`, clears (phase+1)%3, q8[3])
 float* hq_fp8_amax_parts(size_t n);
-void hq_fp8_amax_fold(const float* part, int n, float* q8, int phase, hipStream_t s);
+void hq_fp8_amax_fold(const float* part, int n, float* q8, int phase, hipStream_t s, float fmax = 448.f);
 void hq_fp8_quant_delayed_multi(const uint16_t* x, uint8_t* y, const long long* seg, int nseg, long long blocks,
                                 float* states, int phase, hipStream_t s);
 
 // tiles: int32 [ntiles][6] = (src_off, dst_off, rows, cols, r0, c0); src [rows][cols] -> dst [cols][rows]
 void hq_transpose_tiles(const uint16_t* src, uint16_t* dst, const int* tiles, int ntiles, hipStream_t s);
+void hq_transpose_tiles8(const uint8_t* src, uint8_t* dst, const int* tiles, int ntiles, hipStream_t s);
 // out[c] (+)= sum_p part[p][c], part f32 [P][N]
 void hq_colsum(const float* part, int P, int N, float* out, bool accumulate, hipStream_t s);
 

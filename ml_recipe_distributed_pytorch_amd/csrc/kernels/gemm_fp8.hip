@@ -13,11 +13,16 @@
 // A[row l&15][32·(l>>4) … +31] and B[col l&15][same k] — 32 contiguous bytes = two swizzled 16-B
 // LDS slots (2·fq, 2·fq+1); C/D is the standard 16×16 map.
 //
-// Epilogues: EPI_BIAS (QKV / out-proj / FFN2) and EPI_GELUD (FFN1: act = gelu(pre), P = gelu'(pre));
-// Q8 additionally writes act as e4m3 for the next fp8 GEMM under DELAYED scaling: the scale is derived
-// from the previous step's amax (slot (phase+2)%3 of the 4-float state), this step's amax accumulates
-// into slot `phase`, slot (phase+1)%3 is cleared for the step after, and the scale used is stored in
-// state[3] for the consumer GEMM's dequantisation.  No host synchronisation anywhere.
+// Epilogues, forward (A = e4m3 activations): EPI_BIAS (QKV / out-proj / FFN2) and EPI_GELUD (FFN1:
+// act = gelu(pre), P = gelu'(pre)); Q8 additionally writes act as e4m3 for the next fp8 GEMM.
+// Backward dgrad (A = e5m2 activation gradient, B = e4m3 Wᵀ): EPI_NONE (FFN1 / out-proj dgrad) and
+// EPI_DMUL (FFN2 dgrad: dpre = (dy·W) ⊙ P with P = the stored gelu', plus per-tile column sums of dpre
+// for the FFN1 bias gradient); Q8 on DMUL writes dpre as e5m2 for the FFN1 dgrad.  The e5m2 range
+// (±57344) is what gradients need; the mixed-format MFMA takes the operand formats as immediates.
+// Every Q8 output is under DELAYED scaling: the scale is derived from the previous step's amax (slot
+// (phase+2)%3 of the 4-float state), this step's amax accumulates into slot `phase`, slot (phase+1)%3
+// is cleared for the step after, and the scale used is stored in state[3] for the consumer GEMM's
+// dequantisation.  No host synchronisation anywhere.
 #include <algorithm>
 #include <cstdio>
 #include <vector>
@@ -35,8 +40,11 @@ constexpr float kMargin = 2.f;               // delayed-scaling headroom over la
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 
-__device__ __forceinline__ f32x4_t mfma_fp8(const i32x8& a, const i32x8& b, const f32x4_t& c) {
-  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+// w: the weight fragment (always e4m3, format code 0); x: the activation fragment, e4m3 (0) in the
+// forward or e5m2 (1) for the backward's gradients.  Unit e8m0 block scales (127).
+template <int FX>
+__device__ __forceinline__ f32x4_t mfma_fp8(const i32x8& w, const i32x8& x, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w, x, c, 0, FX, 0, 127, 0, 127);
 }
 
 // 32-byte fragment (k = 32·fq … +31) of LDS row `row`: slots 2fq and 2fq+1, source swizzle undone.
@@ -61,13 +69,17 @@ __device__ __forceinline__ float delayed_scale(const float* st, int phase) {
   return hq_fp8_delayed_scale(st, phase);   // first step: unit scale
 }
 
+constexpr bool grad_epi(int epi) { return epi == HQ_EPI_NONE || epi == HQ_EPI_DMUL; }
+
 template <int EPI, bool Q8>
 __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                                uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                                uint16_t* __restrict__ P, const float* __restrict__ sa,
                                                                const float* __restrict__ sb, uint8_t* __restrict__ C8,
                                                                const float* __restrict__ q8, float* __restrict__ part8,
-                                                               int phase, int M, int N, int K, int lda, int ldb, int ldc) {
+                                                               float* __restrict__ part, int phase, int M, int N, int K,
+                                                               int lda, int ldb, int ldc) {
+  constexpr int FX = grad_epi(EPI) ? 1 : 0;   // A operand: e5m2 gradient (backward) or e4m3 activation
   constexpr int PANEL = 256 * 128, STAGE = 2 * PANEL;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -130,7 +142,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[mh * 4 + i][nh * 2 + j] = mfma_fp8(bf[j], af[i], acc[mh * 4 + i][nh * 2 + j]);
+      for (int j = 0; j < 2; ++j) acc[mh * 4 + i][nh * 2 + j] = mfma_fp8<FX>(bf[j], af[i], acc[mh * 4 + i][nh * 2 + j]);
     __builtin_amdgcn_s_setprio(0);
   };
   auto bar = []() {
@@ -182,12 +194,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
   // ---- epilogue: acc · (sa·sb) (+bias) -> bf16 staging (as gemm.hip v2), then row-coalesced pieces
   const float dq = sa[0] * sb[0];
   constexpr int WN = 64, RS = WN * 2 + 16;
+  constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELUD;
   char* wreg = smem + wave * (128 * RS);
 #pragma unroll
   for (int J = 0; J < 4; ++J) {
     const int nh = J >> 1, j = J & 1;
     const int lc = nh * 32 + j * 16 + fq * 4;
-    const float4 bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
+    float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
 #pragma unroll
     for (int I = 0; I < 8; ++I) {
       float v[4] = {fmaf(acc[I][J][0], dq, bv.x), fmaf(acc[I][J][1], dq, bv.y), fmaf(acc[I][J][2], dq, bv.z),
@@ -197,19 +211,43 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
   }
   float s8 = 1.f, inv8 = 1.f, amax = 0.f;
   if constexpr (Q8) {
-    s8 = delayed_scale(q8, phase);
+    s8 = hq_fp8_delayed_scale(q8, phase, EPI == HQ_EPI_DMUL ? kHqBf8Max : kHqFp8Max);
     inv8 = 1.f / s8;
   }
-  constexpr int SEGS = WN / 8, ROWS_PER_IT = 64 / SEGS;
+  constexpr int SEGS = WN / 8, ROWS_PER_IT = 64 / SEGS, NIT = 128 / ROWS_PER_IT;
   const int seg = lane % SEGS, rsub = lane / SEGS;
   const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;
-#pragma unroll 4
-  for (int it = 0; it < 128 / ROWS_PER_IT; ++it) {
+  auto grow_of = [&](int it) {
     const int lr = it * ROWS_PER_IT + rsub;
-    const int grow = m0 + (lr >> 6) * 128 + wm * 64 + (lr & 63);
+    return m0 + (lr >> 6) * 128 + wm * 64 + (lr & 63);
+  };
+  // DMUL's gelu' operand: all 16 pieces of this lane issued at once (one exposed HBM latency, gemm.hip v2)
+  uint4 aux[EPI == HQ_EPI_DMUL ? NIT : 1];
+  float csum[8];
+  if constexpr (EPI == HQ_EPI_DMUL) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) aux[it] = *reinterpret_cast<const uint4*>(P + (size_t)grow_of(it) * ldc + gcol);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+  }
+  auto piece_out = [&](int it) {
+    const int lr = it * ROWS_PER_IT + rsub;
     uint4 piece = *reinterpret_cast<const uint4*>(wreg + lr * RS + seg * 16);
-    const size_t goff = (size_t)grow * ldc + gcol;
-    if constexpr (EPI == HQ_EPI_GELUD) {
+    const size_t goff = (size_t)grow_of(it) * ldc + gcol;
+    if constexpr (EPI == HQ_EPI_DMUL) {
+      float d[8], gd[8];
+      hq_unpack8(piece, d);
+      hq_unpack8(aux[it], gd);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { d[e] *= gd[e]; csum[e] += d[e]; }
+      piece = hq_pack8(d);
+      if constexpr (Q8) {   // e5m2 dpre for the FFN1 dgrad, from the bf16-rounded values the bf16 copy holds
+        hq_unpack8(piece, d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(d[e]));
+        *reinterpret_cast<uint2*>(C8 + goff) = make_uint2(hq_pack_bf8x4(d, inv8), hq_pack_bf8x4(d + 4, inv8));
+      }
+    } else if constexpr (EPI == HQ_EPI_GELUD) {
       float x[8], g[8];
       hq_unpack8(piece, x);
       hq_gelu_grad8(x, g);   // g = gelu'(x), x = gelu(x)
@@ -231,10 +269,30 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
       }
     }
     *reinterpret_cast<uint4*>(C + goff) = piece;
+  };
+  if constexpr (EPI == HQ_EPI_DMUL) {   // fully unrolled: aux[] must stay in registers
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) piece_out(it);
+  } else {
+#pragma unroll 4
+    for (int it = 0; it < NIT; ++it) piece_out(it);
   }
   if constexpr (Q8) {   // this wave's amax -> its own partial slot (hq_fp8_amax_fold reduces them)
     amax = hq_wave_max(amax);
     if (lane == 0) part8[blockIdx.x * (kThreads / 64) + wave] = amax;
+  }
+  if constexpr (EPI == HQ_EPI_DMUL) {   // column sums of dpre over this tile's 256 rows -> part[tm][n]
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      for (int o = SEGS; o < 64; o <<= 1) csum[e] += __shfl_xor(csum[e], o, 64);
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);  // [2][BN] by tile column, one row per wm
+    if (rsub == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[wm * BN + (gcol - n0) + e] = csum[e];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += kThreads) part[(size_t)tm * N + n0 + c] = red[c] + red[BN + c];
   }
 }
 
@@ -246,7 +304,7 @@ constexpr size_t lds_bytes() {
 
 template <int EPI, bool Q8>
 void launch(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, uint16_t* P, const float* sa,
-            const float* sb, uint8_t* C8, float* q8, int phase, int M, int N, int K, hipStream_t s) {
+            const float* sb, uint8_t* C8, float* q8, float* part, int phase, int M, int N, int K, hipStream_t s) {
   constexpr size_t lds = lds_bytes();
   static bool init = [] {
     (void)hipFuncSetAttribute((const void*)gemm_fp8_kernel<EPI, Q8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -256,8 +314,8 @@ void launch(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, 
   const int grid = (M / BM) * (N / BN);
   float* part8 = Q8 ? hq_fp8_amax_parts((size_t)grid * (kThreads / 64)) : nullptr;
   hipLaunchKernelGGL((gemm_fp8_kernel<EPI, Q8>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, sa, sb,
-                     C8, q8, part8, phase, M, N, K, K, K, N);
-  if (Q8) hq_fp8_amax_fold(part8, grid * (kThreads / 64), q8, phase, s);
+                     C8, q8, part8, part, phase, M, N, K, K, K, N);
+  if (Q8) hq_fp8_amax_fold(part8, grid * (kThreads / 64), q8, phase, s, EPI == HQ_EPI_DMUL ? kHqBf8Max : kHqFp8Max);
 }
 
 // ------------------------------------------------------------------ delayed-scaling quantiser
@@ -336,7 +394,7 @@ __global__ __launch_bounds__(256) void quant_delayed_multi_kernel(const uint16_t
 // (blockIdx.x = g) folds partials [4·blk[g], 4·blk[g+1]).
 __global__ __launch_bounds__(1024) void amax_fold_kernel(const float* __restrict__ part, const long long* __restrict__ seg,
                                                          int nseg, long long nblk, int n, float* __restrict__ states,
-                                                         int phase) {
+                                                         int phase, float fmax) {
   const int g = blockIdx.x;
   long long i0 = 0, i1 = n;
   if (seg != nullptr) {
@@ -369,7 +427,7 @@ __global__ __launch_bounds__(1024) void amax_fold_kernel(const float* __restrict
 #pragma unroll
     for (int w = 1; w < 16; ++w) m = fmaxf(m, red[w]);   // m = red[0] here (thread 0's wave)
     unsigned* st = reinterpret_cast<unsigned*>(q8);
-    const float s = delayed_scale(q8, phase);
+    const float s = hq_fp8_delayed_scale(q8, phase, fmax);   // 448 (e4m3) or 57344 (e5m2 gradients)
     st[phase] = __float_as_uint(fmaxf(__uint_as_float(st[phase]), m));
     st[(phase + 1) % 3] = 0u;   // cleared for the step after next's accumulation
     q8[3] = s;                  // dequant scale of this step's e4m3 output
@@ -386,7 +444,7 @@ void hq_fp8_quant_delayed_multi(const uint16_t* x, uint8_t* y, const long long* 
   float* part = hq_fp8_amax_parts((size_t)blocks * 4);
   hipLaunchKernelGGL(quant_delayed_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, y, seg, nseg, states, part,
                      phase);
-  hipLaunchKernelGGL(amax_fold_kernel, dim3(nseg), dim3(1024), 0, s, part, seg, nseg, blocks, 0, states, phase);
+  hipLaunchKernelGGL(amax_fold_kernel, dim3(nseg), dim3(1024), 0, s, part, seg, nseg, blocks, 0, states, phase, kFp8Max);
 }
 
 float* hq_fp8_amax_parts(size_t n) {
@@ -406,9 +464,9 @@ float* hq_fp8_amax_parts(size_t n) {
   return b.first;
 }
 
-void hq_fp8_amax_fold(const float* part, int n, float* q8, int phase, hipStream_t s) {
+void hq_fp8_amax_fold(const float* part, int n, float* q8, int phase, hipStream_t s, float fmax) {
   if (n % 4 != 0) { fprintf(stderr, "hq_fp8_amax_fold: %d partials (must be a multiple of 4)\n", n); abort(); }
-  hipLaunchKernelGGL(amax_fold_kernel, dim3(1), dim3(1024), 0, s, part, nullptr, 1, 0LL, n, q8, phase);
+  hipLaunchKernelGGL(amax_fold_kernel, dim3(1), dim3(1024), 0, s, part, nullptr, 1, 0LL, n, q8, phase, fmax);
 }
 
 int hq_gemm_fp8_supported(int M, int N, int K) {
@@ -417,12 +475,19 @@ int hq_gemm_fp8_supported(int M, int N, int K) {
 }
 
 void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, uint16_t* P, const float* sa,
-                 const float* sb, uint8_t* C8, float* q8, int phase, int M, int N, int K, int epi, hipStream_t s) {
-  if (epi == HQ_EPI_GELUD) {
-    if (C8) launch<HQ_EPI_GELUD, true>(A, B, C, bias, P, sa, sb, C8, q8, phase, M, N, K, s);
-    else launch<HQ_EPI_GELUD, false>(A, B, C, bias, P, sa, sb, C8, q8, phase, M, N, K, s);
-  } else {
-    launch<HQ_EPI_BIAS, false>(A, B, C, bias, P, sa, sb, C8, q8, phase, M, N, K, s);
+                 const float* sb, uint8_t* C8, float* q8, int phase, int M, int N, int K, int epi, hipStream_t s,
+                 float* part) {
+  switch (epi) {
+    case HQ_EPI_GELUD:
+      if (C8) launch<HQ_EPI_GELUD, true>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
+      else launch<HQ_EPI_GELUD, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
+      break;
+    case HQ_EPI_DMUL:
+      if (C8) launch<HQ_EPI_DMUL, true>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
+      else launch<HQ_EPI_DMUL, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
+      break;
+    case HQ_EPI_NONE: launch<HQ_EPI_NONE, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s); break;
+    default: launch<HQ_EPI_BIAS, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s); break;
   }
 }
 

@@ -208,14 +208,19 @@ __device__ __forceinline__ void ln_bwd_load(const uint16_t* __restrict__ dy, con
 
 // RPW rows per wave: 8 at large T (partials amortised), 2 for small token counts (T = 1024: 32 blocks of
 // 8-row waves left most CUs idle and each wave latency-bound — see ln_rows_per_wave)
-template <int NCH, int RPW = kRowsPerWave>
+template <int NCH, int RPW = kRowsPerWave, bool Q8 = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dy2,
                                                      const uint16_t* __restrict__ z, const float* __restrict__ gamma,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      uint16_t* __restrict__ dz_out, uint16_t* __restrict__ da_out,
                                                      float* __restrict__ part, int T, int H, HqDropKey kd_, uint32_t thr,
-                                                     float kscale) {
+                                                     float kscale, uint8_t* __restrict__ da8, const float* __restrict__ q8,
+                                                     float* __restrict__ part8, int phase) {
   const uint32_t key = kd_.get();
+  // Q8 (--precision fp8 backward): da also as e5m2 under the delayed scale of the dgrad GEMM that consumes
+  // it (state q8), so that GEMM runs on fp8 operands without a separate quantisation pass
+  float inv8 = 1.f, amax8 = 0.f;
+  if constexpr (Q8) inv8 = 1.f / hq_fp8_delayed_scale(q8, phase, kHqBf8Max);
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float acc[3][NCH][4];
@@ -300,6 +305,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
 #pragma unroll
           for (int i = 0; i < 4; ++i) { da[i] = dz[i] * m[i]; acc[2][c][i] += da[i]; }
           *reinterpret_cast<uint2*>(da_out + base + col) = hq_pack4(da);
+          if constexpr (Q8) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) amax8 = fmaxf(amax8, fabsf(da[i]));
+            *reinterpret_cast<uint32_t*>(da8 + base + col) = hq_pack_bf8x4(da, inv8);
+          }
         }
       }
 #pragma unroll
@@ -310,6 +320,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
       cmu = nmu; crs = nrs;
       nmu = fmu; nrs = frs;
     }
+  }
+  if constexpr (Q8) {   // this wave's amax -> its own partial slot (hq_fp8_amax_fold reduces them)
+    amax8 = hq_wave_max(amax8);
+    if (lane == 0) part8[blockIdx.x * kWaves + wave] = amax8;
   }
   block_partials<NCH, 3>(acc, lds, part, H);
 }
@@ -789,19 +803,27 @@ int hq_embed_bwd_partials(int T, int L) {
 
 void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const float* gamma, const float* mean,
                const float* rstd, uint16_t* dz, uint16_t* da, float* part, HqOuts outs, int T, int H, float p,
-               uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s) {
+               uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s, uint8_t* da8, float* q8, int phase) {
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const HqDropKey key = hq_drop_key(seed, opid);
   const float ks = hq_keep_scale(thr);
   const int nb = hq_ln_bwd_partials(T);
+  float* part8 = da8 ? hq_fp8_amax_parts((size_t)nb * kWaves) : nullptr;
   dispatch_nch(H, [&](auto nch) {
-    if (ln_rows_per_wave(T) == kRowsPerWave)
-      hipLaunchKernelGGL((ln_bwd_kernel<decltype(nch)::value, kRowsPerWave>), dim3(nb), dim3(256), 4 * H * sizeof(float), s,
-                         dy, dy2, z, gamma, mean, rstd, dz, da, part, T, H, key, thr, ks);
-    else
-      hipLaunchKernelGGL((ln_bwd_kernel<decltype(nch)::value, 2>), dim3(nb), dim3(256), 4 * H * sizeof(float), s, dy, dy2,
-                         z, gamma, mean, rstd, dz, da, part, T, H, key, thr, ks);
+    constexpr int C = decltype(nch)::value;
+    auto go = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 4 * H * sizeof(float), s, dy, dy2, z, gamma, mean, rstd, dz, da, part,
+                         T, H, key, thr, ks, da8, q8, part8, phase);
+    };
+    if (ln_rows_per_wave(T) == kRowsPerWave) {
+      if (da8) go(ln_bwd_kernel<C, kRowsPerWave, true>);
+      else go(ln_bwd_kernel<C, kRowsPerWave, false>);
+    } else {
+      if (da8) go(ln_bwd_kernel<C, 2, true>);
+      else go(ln_bwd_kernel<C, 2, false>);
+    }
   });
+  if (da8) hq_fp8_amax_fold(part8, nb * kWaves, q8, phase, s, kHqBf8Max);
   colsum(part, nb, 3 * H, outs, H, accumulate, s);
 }
 

@@ -5,7 +5,11 @@ SplitDataset, collate) and ``validation_dataset.py`` (ChunkDataset), restructure
 
 * ``RawPreprocessor``: one ``{i}.json`` per jsonl line (lazy line index instead of ``linecache``),
   5-way labels yes/no/short/long/unknown, stratified 95/5 split (sklearn, ``random_state=0``).
-  Caches are JSON (``label.info``, ``split.info``) — never pickles.
+  Caches are JSON (``label.info``, ``split.info``) — never pickles.  A ``processed_data_path`` prepared
+  by the reference (whose two ``.info`` caches are pickles) is reused without unpickling anything: the
+  per-example ``{i}.json`` files are the same format, the labels are re-derived from them and the split
+  recomputed by the same per-class ``train_test_split(random_state=0)`` (identical indexes), cached in
+  ``*.info.json`` side files so the reference's own files stay untouched.
 * One shared document encoder (word-by-word WordPiece with word↔token maps, HTML tags dropped)
   and two window enumerators (token stride; whole-sentence packing with optional truncation) used
   by both the training dataset (samples ONE window, answer-bearing windows weighted 1 vs 1e-3)
@@ -75,11 +79,35 @@ class RawPreprocessor:
         self.raw_json = raw_json
         self.out_dir = Path(out_dir)
         os.makedirs(self.out_dir, exist_ok=True)
-        self.label_info_path = self.out_dir / "label.info"
-        self.split_info_path = self.out_dir / "split.info"
         if clear:
             for f in self.out_dir.glob("*"):
                 os.remove(f)
+        self.label_info_path = self._cache_path(self.out_dir / "label.info")
+        self.split_info_path = self._cache_path(self.out_dir / "split.info")
+        self.from_reference = self.label_info_path.name.endswith(".json")
+
+    @staticmethod
+    def _cache_path(path: Path) -> Path:
+        """``path`` unless it holds a pickle (the reference's cache format, opcode PROTO = 0x80 first):
+        then the JSON side file next to it."""
+        if path.exists():
+            with open(path, "rb") as f:
+                if f.read(1) == b"\x80":
+                    logger.warning(f"{path} is a pickle written by the reference; it is not loaded — the "
+                                   f"cache is rebuilt from the JSON example files into {path.name}.json")
+                    return path.with_name(path.name + ".json")
+        return path
+
+    def _labels_from_items(self) -> np.ndarray:
+        """Labels of an existing example directory ({i}.json, contiguous from 0), no raw jsonl pass."""
+        n = 0
+        while (self.out_dir / f"{n}.json").exists():
+            n += 1
+        lab = np.zeros(n, dtype=np.int64)
+        for i in range(n):
+            with open(self.out_dir / f"{i}.json") as f:
+                lab[i] = self.labels2id[self._get_target(json.load(f))[0]]
+        return lab
 
     @staticmethod
     def _process_line(raw: dict) -> dict:
@@ -112,6 +140,11 @@ class RawPreprocessor:
             counter = {int(k): v for k, v in info["counter"].items()}
             labels = np.asarray(info["labels"], dtype=np.int64)
             logger.info(f"Labels info was loaded from {self.label_info_path}.")
+        elif self.from_reference:
+            labels = self._labels_from_items()
+            counter = {int(y): int((labels == y).sum()) for y in np.unique(labels)}
+            with open(self.label_info_path, "w") as f:
+                json.dump({"counter": counter, "labels": labels.tolist()}, f)
         else:
             counter, lab = defaultdict(int), []
             for i, raw in enumerate(LineIndex(self.raw_json)):

@@ -186,7 +186,8 @@ class _LayerFn(torch.autograd.Function):
         # PRODUCERS under delayed scaling: QKV's by the previous layer's second LayerNorm (layer 0: one
         # quantisation pass over the embeddings), the out-projection's by the attention forward's ctx store,
         # FFN1's by this layer's first LayerNorm, FFN2's by FFN1's epilogue — so no standalone quantiser
-        # runs per layer.  Backward GEMMs are bf16 throughout.
+        # runs per layer.  In the backward the dgrads of FFN2, FFN1 and the out-projection run in fp8 too
+        # (e5m2 gradients, see backward); weight gradients and the QKV dgrad stay bf16.
         fp8 = fp8 and ops.fp8_gemm_ok(x.shape[0], 3 * cfg.hidden_size, cfg.hidden_size)
         s8 = m.fp8_states(idx) if fp8 else None
         if fp8:
@@ -269,21 +270,52 @@ class _LayerFn(torch.autograd.Function):
                 ops.linear_wgrad(dy, xin, gw, gb, acc)
         Wm = lambda k: st.view(p + k, "master")  # noqa: E731
         dh2 = dh2.contiguous()
+        # --precision fp8: the FFN2 / FFN1 / out-projection dgrads run on the fp8 MFMA kernel with e5m2
+        # gradients (range ±57344; e4m3's ±448 is too narrow for gradients) against the e4m3 Wᵀ copies —
+        # each gradient written in e5m2 by its PRODUCER under delayed scaling: da2 and da1 by the LayerNorm
+        # backwards, dpre by the FFN2 dgrad's DMUL epilogue.  A gradient state has no current-scaling seed,
+        # so its consumer runs in bf16 until one production has recorded an amax (``calibrated``).
+        T = dh2.shape[0]
+        fp8 = (m.precision == "fp8" and dh2.is_cuda and m.fp8_dgrad and ctx.gelu_deriv
+               and ops.fp8_gemm_ok(T, cfg.intermediate_size, cfg.hidden_size)
+               and ops.fp8_gemm_ok(T, cfg.hidden_size, cfg.intermediate_size)
+               and ops.fp8_gemm_ok(T, cfg.hidden_size, cfg.hidden_size))
+        s8 = m.fp8_states(idx) if fp8 else None
+        W8T = lambda k: st.view_fp8_t(p + k)  # noqa: E731  (e4m3 Wᵀ + dequant scale)
 
         # --- FFN block ------------------------------------------------------------------------
-        dz2, da2 = ops.ln_bwd(dh2, None, z2, Wm("output.LayerNorm.weight"), m2, r2, ctx.ph, info.seed, op0 + 2,
-                              G("output.LayerNorm.weight"), G("output.LayerNorm.bias"), G("output.dense.bias"), acc)
+        ln2b = (dh2, None, z2, Wm("output.LayerNorm.weight"), m2, r2, ctx.ph, info.seed, op0 + 2,
+                G("output.LayerNorm.weight"), G("output.LayerNorm.bias"), G("output.dense.bias"), acc)
+        if fp8:
+            dz2, da2, da2_8 = ops.ln_bwd_q8(*ln2b, s8["dffn2"])
+        else:
+            dz2, da2 = ops.ln_bwd(*ln2b)
         wgrad(da2, act, G("output.dense.weight"), None)
-        dpre = ops.linear_dgrad_gelu_d(da2, W("output.dense.weight"), pre, ctx.gelu_deriv,
-                                       G("intermediate.dense.bias"), acc, wt=WT("output.dense.weight"))
+        dpre8 = None
+        if fp8 and s8["dffn2"].calibrated:
+            dpre, dpre8 = ops.linear_dgrad_gelu_fp8(da2_8, s8["dffn2"], W8T("output.dense.weight"), pre,
+                                                    G("intermediate.dense.bias"), acc, s8["dffn1"])
+        else:
+            dpre = ops.linear_dgrad_gelu_d(da2, W("output.dense.weight"), pre, ctx.gelu_deriv,
+                                           G("intermediate.dense.bias"), acc, wt=WT("output.dense.weight"))
         wgrad(dpre, h1, G("intermediate.dense.weight"), None)
-        dh1_ffn = ops.linear_dgrad(dpre, W("intermediate.dense.weight"), wt=WT("intermediate.dense.weight"))
+        if dpre8 is not None and s8["dffn1"].calibrated:
+            dh1_ffn = ops.linear_dgrad_fp8(dpre8, s8["dffn1"], W8T("intermediate.dense.weight"))
+        else:
+            dh1_ffn = ops.linear_dgrad(dpre, W("intermediate.dense.weight"), wt=WT("intermediate.dense.weight"))
         # --- attention block ------------------------------------------------------------------
-        dz1, da1 = ops.ln_bwd(dz2, dh1_ffn, z1, Wm("attention.output.LayerNorm.weight"), m1, r1, ctx.ph, info.seed,
-                              op0 + 1, G("attention.output.LayerNorm.weight"), G("attention.output.LayerNorm.bias"),
-                              G("attention.output.dense.bias"), acc)
+        ln1b = (dz2, dh1_ffn, z1, Wm("attention.output.LayerNorm.weight"), m1, r1, ctx.ph, info.seed, op0 + 1,
+                G("attention.output.LayerNorm.weight"), G("attention.output.LayerNorm.bias"),
+                G("attention.output.dense.bias"), acc)
+        if fp8:
+            dz1, da1, da1_8 = ops.ln_bwd_q8(*ln1b, s8["dout"])
+        else:
+            dz1, da1 = ops.ln_bwd(*ln1b)
         wgrad(da1, ctxv, G("attention.output.dense.weight"), None)
-        dctx = ops.linear_dgrad(da1, W("attention.output.dense.weight"), wt=WT("attention.output.dense.weight"))
+        if fp8 and s8["dout"].calibrated:
+            dctx = ops.linear_dgrad_fp8(da1_8, s8["dout"], W8T("attention.output.dense.weight"))
+        else:
+            dctx = ops.linear_dgrad(da1, W("attention.output.dense.weight"), wt=WT("attention.output.dense.weight"))
         dqkv = ops.attn_bwd(dctx, qkv, ctxv, lse, key_bias, ctx.bits, B, L, nh, ctx.pa, info.seed, op0, ctx.scale)
         ctx.bits = None
         wgrad(dqkv, x, G("qkv.weight"), G("qkv.bias"))
@@ -334,6 +366,7 @@ class BertForQuestionAnswering(nn.Module):
         super().__init__()
         self.config = config
         self.precision = precision
+        self.fp8_dgrad = True   # --precision fp8: run the FFN / out-projection dgrads in fp8 as well
         gen = torch.Generator().manual_seed(seed) if seed is not None else None
         self.store = ParamStore(build_entries(config))
         _init_store(self.store, config, gen)
@@ -423,6 +456,8 @@ class BertForQuestionAnswering(nn.Module):
         st = self._fp8_states.get(idx)
         if st is None or st["qkv"].buf.device != self.store.device:
             st = {k: ops.Fp8DelayedState(self.store.device) for k in ("qkv", "out", "ffn1", "ffn2")}
+            # activation gradients (e5m2): the inputs of the FFN2 / FFN1 / out-projection dgrads
+            st.update({k: ops.Fp8DelayedState(self.store.device, grad=True) for k in ("dffn2", "dffn1", "dout")})
             self._fp8_states[idx] = st
         return st
 

@@ -74,6 +74,7 @@ class ParamStore:
         self._fp8_state: Dict[str, object] = {}
         self._fp8_states_buf: Optional[torch.Tensor] = None
         self._fp8_dirty = True
+        self._fp8_t_dirty = True   # e4m3 Wᵀ copies (fp8 dgrad GEMMs), transposed from the forward e4m3 bytes
 
     # ------------------------------------------------------------------ allocation
     def allocate(self, device, init_std: float, generator: Optional[torch.Generator] = None):
@@ -199,6 +200,32 @@ class ParamStore:
                                           self._fp8_blocks, phase)
         self._fp8 = {kk: (self._fp8_views[kk], self._fp8_state[kk].scale) for kk in self._t_keys}
         self._fp8_dirty = False
+        self._fp8_t_dirty = True
+
+    def view_fp8_t(self, key: str):
+        """(Wᵀ as float8_e4m3fn [in, out], dequant scale) for the fp8 dgrad GEMMs: the bytes of the forward
+        e4m3 copy transposed (one batched launch for every weight, after each re-quantisation), so forward
+        and backward see the same quantised weight under the same scale."""
+        from .._native import kernels
+        if self.view_fp8(key) is None:
+            return None
+        if self._fp8_t_dirty:
+            if getattr(self, "_fp8_ty", None) is None or self._fp8_ty.numel() != self._fp8_y.numel() \
+                    or self._fp8_ty.device != self._fp8_y.device:
+                self._fp8_ty = torch.empty_like(self._fp8_y)
+                rows = []
+                for kk, r in zip(self._t_keys, self._fp8_seg.tolist()):
+                    R, Cc = self.by_key[kk].shape
+                    for r0 in range(0, R, 64):
+                        for c0 in range(0, Cc, 64):
+                            rows.append([r[1], r[1], R, Cc, r0, c0])
+                self._fp8_t_tiles = torch.tensor(rows, dtype=torch.int32).to(self._fp8_y.device)
+                self._fp8_t_views = {kk: self._fp8_ty[r[1]:r[1] + self.by_key[kk].numel].view(torch.float8_e4m3fn)
+                                     .view(self.by_key[kk].shape[1], self.by_key[kk].shape[0])
+                                     for kk, r in zip(self._t_keys, self._fp8_seg.tolist())}
+            kernels().transpose_tiles8(self._fp8_y, self._fp8_ty, self._fp8_t_tiles)
+            self._fp8_t_dirty = False
+        return self._fp8_t_views[key], self._fp8_state[key].scale
 
     def view_t(self, key: str) -> Optional[torch.Tensor]:
         """Wᵀ of a registered weight, or None when unavailable (CPU / fp32 / not registered)."""

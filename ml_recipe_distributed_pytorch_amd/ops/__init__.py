@@ -63,6 +63,14 @@ def ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias
     return ref.ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate)
 
 
+def ln_bwd_q8(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate,
+              state: "Fp8DelayedState"):
+    """``ln_bwd`` that also writes da in e5m2 under ``state`` — the delayed-scaling state of the fp8 dgrad
+    GEMM that consumes da: (dz, da, da8)."""
+    return tuple(_k().ln_bwd(dy, dy2, z, gamma, mean, rstd, float(p), int(seed), int(opid), g_gamma, g_beta, g_bias,
+                             bool(accumulate), q8=state.buf, phase=state.next_phase()))
+
+
 # ------------------------------------------------------------------------------------------ GELU
 def gelu_fwd(pre):
     if pre.is_cuda:
@@ -173,11 +181,19 @@ def linear_fwd_fp8(x, w8s, b):
 class Fp8DelayedState:
     """Per-site delayed-scaling state of an fp8 GEMM input: a device f32[4] (three rotating amax slots
     + the scale in use, see gemm_fp8.hip) and a host step counter selecting the slots — so neither the
-    quantiser nor the GEMM ever synchronises with the host."""
+    quantiser nor the GEMM ever synchronises with the host.  Forward inputs are e4m3 (scale = 2·amax/448);
+    backward activation gradients are e5m2 (scale = 2·amax/57344, ``grad=True``)."""
 
-    def __init__(self, device, buf: Optional[torch.Tensor] = None):
+    def __init__(self, device, buf: Optional[torch.Tensor] = None, grad: bool = False):
         self.buf = torch.zeros(4, dtype=torch.float32, device=device) if buf is None else buf
         self.step = 0
+        self.grad = grad
+
+    @property
+    def calibrated(self) -> bool:
+        """True once a previous production recorded an amax, i.e. the scale in use now is derived from
+        real data (a gradient state has no current-scaling seed: its consumer runs in bf16 until then)."""
+        return self.step >= 2
 
     def next_phase(self) -> int:
         ph = self.step % 3
@@ -225,6 +241,29 @@ def linear_gelu_fwd_fp8(x, w8s, b32, in_state: Fp8DelayedState, out_state: Fp8De
     act = _k().gemm_fp8(x8, w8, _EPI_GELUD, b32, in_state.scale, sw.reshape(1).float(), pre=gd, out8=act8,
                         state=out_state.buf, phase=out_state.next_phase())
     return gd, act, act8
+
+
+def linear_dgrad_fp8(dy8, dy_state: Fp8DelayedState, wt8s):
+    """dy·W for an e5m2 gradient ``dy8`` written by its producer under ``dy_state``, on the fp8 MFMA kernel
+    (gemm_fp8.hip EPI_NONE) against the e4m3 Wᵀ copy ``wt8s`` = (Wᵀ fp8 [in, out], dequant scale) from
+    ParamStore.view_fp8_t; bf16 out."""
+    wt8, sw = wt8s
+    return _k().gemm_fp8(dy8, wt8, _EPI_NONE, None, dy_state.scale, sw.reshape(1).float())
+
+
+def linear_dgrad_gelu_fp8(dy8, dy_state: Fp8DelayedState, wt8s, gd, g_bias, accumulate, out_state: Fp8DelayedState):
+    """FFN2 dgrad in fp8: dpre = (dy·W) ⊙ gelu'(pre) (``gd``: the gelu' stored by the forward), the FFN1 bias
+    gradient from the epilogue's column sums, and dpre also in e5m2 under ``out_state`` for the FFN1 dgrad:
+    (dpre, dpre8)."""
+    wt8, sw = wt8s
+    M, N = dy8.shape[0], wt8.shape[0]
+    part = torch.empty(M // 256, N, dtype=torch.float32, device=dy8.device)
+    dpre8 = torch.empty(M, N, dtype=torch.float8_e5m2, device=dy8.device)
+    dpre = _k().gemm_fp8(dy8, wt8, _EPI_DMUL, None, dy_state.scale, sw.reshape(1).float(), pre=gd, out8=dpre8,
+                         state=out_state.buf, phase=out_state.next_phase(), part=part)
+    if g_bias is not None:
+        _k().colsum_into(part, g_bias, bool(accumulate))
+    return dpre, dpre8
 
 
 def linear_gelu_fwd(x, w, b, b32=None):

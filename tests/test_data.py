@@ -117,6 +117,35 @@ def test_preprocessor_labels_and_split(nq):
     assert (d / "proc" / "label.info").exists() and (d / "proc" / "split.info").exists()
 
 
+def test_reference_prepared_directory_is_reused_without_unpickling(nq, tmp_path):
+    """A processed_data_path written by the reference: {i}.json examples (same format) + PICKLED
+    label.info / split.info.  The pickles are detected by their first byte and never loaded; labels come
+    from the example files, the split is recomputed (same per-class random_state=0 rule), JSON side files
+    hold the caches, and the reference's files are left byte-identical."""
+    import pickle
+    import shutil
+    from ml_recipe_distributed_pytorch_amd.data.nq import RawPreprocessor
+    d, (counter, labels, (tr, trl, te, tel)), _ = nq
+    ref_dir = tmp_path / "ref_proc"
+    ref_dir.mkdir()
+    for i in range(len(labels)):
+        shutil.copy(d / "proc" / f"{i}.json", ref_dir / f"{i}.json")
+    blobs = {"label.info": pickle.dumps(({0: 1}, np.zeros(3)), protocol=4),   # content deliberately wrong:
+             "split.info": pickle.dumps((np.zeros(1),) * 4, protocol=4)}       # it must never be read
+    for name, b in blobs.items():
+        (ref_dir / name).write_bytes(b)
+    pre = RawPreprocessor(str(d / "missing.jsonl"), str(ref_dir))   # no raw pass: the jsonl is not needed
+    assert pre.from_reference
+    c2, l2, (tr2, trl2, te2, tel2) = pre()
+    assert c2 == counter and (l2 == labels).all()
+    assert (tr2 == tr).all() and (te2 == te).all() and (trl2 == trl).all() and (tel2 == tel).all()
+    for name, b in blobs.items():
+        assert (ref_dir / name).read_bytes() == b
+        assert (ref_dir / (name + ".json")).exists()
+    c3, l3, _ = RawPreprocessor(str(d / "missing.jsonl"), str(ref_dir))()   # second run: the side files
+    assert c3 == counter and (l3 == labels).all()
+
+
 def _answer_text(tok, line):
     from ml_recipe_distributed_pytorch_amd.data.nq import RawPreprocessor
     _, s, e = RawPreprocessor._get_target(line)

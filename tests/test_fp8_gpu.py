@@ -202,3 +202,152 @@ def test_attn_fwd_fp8_ctx_output(cuda, p):
     exp = (ctx / s).clamp(-448, 448).to(torch.float8_e4m3fn)
     diff = (out2[3].view(torch.uint8).int() - exp.view(torch.uint8).int()).abs()
     assert diff.max().item() <= 1 and (diff > 0).float().mean().item() < 1e-4   # x·(1/s) vs x/s rounding
+
+
+# ----------------------------------------------------------------------------- fp8 backward (e5m2)
+EPI_NONE, EPI_DMUL = 0, 6
+
+
+def _q5(x, s):
+    """e5m2(x / s) the way the kernels round it (saturated, RNE)."""
+    return (x.float() / s).clamp(-57344, 57344).to(torch.float8_e5m2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(256, 768, 768), (512, 3072, 768), (512, 768, 3072)])
+def test_gemm_fp8_dgrad_e5m2(cuda, M, N, K):
+    """dgrad form: A = e5m2 gradient (mixed-format MFMA, blgp = e5m2), B = e4m3 Wᵀ, no epilogue."""
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(M * 3 + N + K)
+    dy = torch.randn(M, K, device=cuda, generator=g) * 1e-3
+    sa = torch.full((1,), 1e-3 * 4 / 57344, device=cuda)
+    A8 = _q5(dy, sa)
+    B8, sb = _q((torch.randn(N, K, device=cuda, generator=g) * 0.05).bfloat16())
+    C = k.gemm_fp8(A8, B8, EPI_NONE, None, sa, sb)
+    ref = (A8.float() * sa) @ (B8.float() * sb).t()
+    err = (C.float() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item(), err
+
+
+@pytest.mark.gpu
+def test_gemm_fp8_dgrad_exact(cuda):
+    """Small integers (exact in e5m2, e4m3 and fp32): the e5m2 operand's lane map and format code."""
+    k = _native.kernels()
+    M, N, K = 256, 512, 256
+    i = torch.arange(M, device=cuda)[:, None]
+    kk = torch.arange(K, device=cuda)[None, :]
+    n = torch.arange(N, device=cuda)[:, None]
+    A = ((i * 5 + kk * 3) % 7 - 3).float()     # -3..3: 3 is exact in e5m2 (1.1b × 2^1)
+    B = ((n * 11 + kk * 5 + 1) % 5 - 2).float()
+    one = torch.ones(1, device=cuda)
+    C = k.gemm_fp8(A.to(torch.float8_e5m2), B.to(torch.float8_e4m3fn), EPI_NONE, None, one, one)
+    assert torch.equal(C.float(), (A @ B.t()).bfloat16().float())
+
+
+@pytest.mark.gpu
+def test_gemm_fp8_dmul_colsum_q8(cuda):
+    """FFN2 dgrad epilogue: dpre = bf16(dy·W) ⊙ gelu', per-256-row column sums (FFN1 bias gradient) and
+    dpre in e5m2 under the gradient's delayed scale (2·amax_prev/57344), over three phases."""
+    k = _native.kernels()
+    M, N, K = 768, 3072, 768
+    g = torch.Generator(device=cuda).manual_seed(21)
+    sa = torch.full((1,), 1e-2 * 4 / 57344, device=cuda)
+    A8 = _q5(torch.randn(M, K, device=cuda, generator=g) * 1e-2, sa)
+    B8, sb = _q((torch.randn(N, K, device=cuda, generator=g) * 0.05).bfloat16())
+    gd = (torch.rand(M, N, device=cuda, generator=g) * 1.2 - 0.1).bfloat16()
+    mm = ((A8.float() * sa) @ (B8.float() * sb).t()).bfloat16().float()
+    ref = mm * gd.float()
+    state = torch.zeros(4, device=cuda)
+    for phase in range(3):
+        part = torch.empty(M // 256, N, device=cuda)
+        out8 = torch.empty(M, N, device=cuda, dtype=torch.float8_e5m2)
+        C = k.gemm_fp8(A8, B8, EPI_DMUL, None, sa, sb, pre=gd, out8=out8, state=state, phase=phase, part=part)
+        torch.testing.assert_close(C.float(), ref, atol=2e-3 * ref.abs().max().item(), rtol=2e-2)
+        torch.testing.assert_close(part, ref.view(M // 256, 256, N).sum(1), atol=1e-2 * ref.abs().max().item(),
+                                   rtol=2e-2)
+        s = state[3].item()
+        amax_c = C.float().abs().max().item()
+        assert s == (1.0 if phase == 0 else pytest.approx(2 * amax_c / 57344, rel=1e-3))
+        exp = _q5(C, s)
+        diff = (out8.view(torch.uint8).int() - exp.view(torch.uint8).int()).abs()
+        assert diff.max().item() <= 1 and (diff > 0).float().mean().item() < 1e-3   # x·(1/s) vs x/s
+        amax = state[:3].view(torch.int32)[phase].view(torch.float32).item()
+        assert amax == pytest.approx(amax_c, rel=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,H", [(1024, 768), (2048, 1024)])
+def test_ln_bwd_e5m2_output(cuda, T, H):
+    """LayerNorm backward with the e5m2 copy of da for the fp8 dgrad: dz / da equal the plain call bitwise
+    (and so do the parameter gradients), da8 = e5m2(bf16(da) / s) under the delayed scale, amax recorded."""
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(T + H)
+    dy = (torch.randn(T, H, device=cuda, generator=g) * 1e-3).bfloat16()
+    z = torch.randn(T, H, device=cuda, generator=g).bfloat16()
+    gamma = torch.rand(H, device=cuda, generator=g) + 0.5
+    mean = z.float().mean(1)
+    rstd = torch.rsqrt(z.float().var(1, unbiased=False) + 1e-12)
+    grads = [torch.zeros(H, device=cuda) for _ in range(3)]
+    ref = k.ln_bwd(dy, None, z, gamma, mean, rstd, 0.1, 7, 3, *grads, False)
+    grads8 = [torch.zeros(H, device=cuda) for _ in range(3)]
+    state = torch.zeros(4, device=cuda)
+    out = k.ln_bwd(dy, None, z, gamma, mean, rstd, 0.1, 7, 3, *grads8, False, q8=state, phase=0)
+    assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1])
+    for a, b in zip(grads, grads8):
+        assert torch.equal(a, b)
+    da, da8 = out[1].float(), out[2]
+    assert da8.dtype == torch.float8_e5m2 and state[3].item() == 1.0
+    assert torch.equal(da8.view(torch.uint8), _q5(da, 1.0).view(torch.uint8))
+    amax = state[:3].view(torch.int32)[0].view(torch.float32).item()
+    assert amax == da.abs().max().item()
+    out2 = k.ln_bwd(dy, None, z, gamma, mean, rstd, 0.1, 7, 3, *grads8, True, q8=state, phase=1)
+    s = state[3].item()
+    assert s == pytest.approx(2 * amax / 57344, rel=1e-6)
+    diff = (out2[2].view(torch.uint8).int() - _q5(da, s).view(torch.uint8).int()).abs()
+    assert diff.max().item() <= 1 and (diff > 0).float().mean().item() < 1e-3
+
+
+@pytest.mark.gpu
+def test_view_fp8_t_is_the_transposed_forward_copy(cuda):
+    from ml_recipe_distributed_pytorch_amd.models.bert import BertForQuestionAnswering
+    from ml_recipe_distributed_pytorch_amd.models.config import get_config
+    cfg = get_config("bert-base-uncased", num_hidden_layers=1)
+    m = BertForQuestionAnswering(cfg, seed=0, precision="fp8").to(cuda)
+    for name in ("qkv.weight", "intermediate.dense.weight", "output.dense.weight"):
+        key = "transformer.encoder.layer.0." + name
+        w8, s = m.store.view_fp8(key)
+        wt8, st = m.store.view_fp8_t(key)
+        assert wt8.shape == (w8.shape[1], w8.shape[0]) and wt8.is_contiguous()
+        assert torch.equal(wt8.view(torch.uint8), w8.view(torch.uint8).t())
+        assert st.data_ptr() == s.data_ptr()
+
+
+@pytest.mark.gpu
+def test_fp8_dgrad_step_close_to_bf16_dgrad(cuda):
+    """--precision fp8 with the e5m2 dgrads (FFN2 / FFN1 / out-projection) against the same model with bf16
+    dgrads: after the gradient states calibrate (step 3), the parameter gradients agree to fp8 accuracy."""
+    from ml_recipe_distributed_pytorch_amd.models.bert import BertForQuestionAnswering
+    from ml_recipe_distributed_pytorch_amd.models.config import get_config
+    cfg = get_config("bert-base-uncased", num_hidden_layers=2, hidden_dropout_prob=0.0,
+                     attention_probs_dropout_prob=0.0)
+    g = torch.Generator().manual_seed(4)
+    ids = torch.randint(1, cfg.vocab_size, (4, 256), generator=g).to(cuda)
+    grads = {}
+    for dg in (False, True):
+        m = BertForQuestionAnswering(cfg, seed=0, precision="fp8").to(cuda).train()
+        m.fp8_dgrad = dg
+        for _ in range(3):
+            m.zero_grad()
+            out = m(ids)
+            sum((v.float() ** 2).mean() for v in out.values()).backward()
+        torch.cuda.synchronize()
+        if dg:
+            s8 = m.fp8_states(0)
+            assert all(s8[k].calibrated for k in ("dffn2", "dffn1", "dout"))
+        grads[dg] = m.store.grad.clone()
+    assert torch.isfinite(grads[True]).all()
+    for e in m.store.entries:
+        if e.key.startswith("transformer.encoder") and e.key.endswith("weight") and len(e.shape) == 2:
+            a, b = (grads[x][e.offset:e.offset + e.numel] for x in (True, False))
+            rel = ((a - b).norm() / b.norm()).item()
+            assert rel < 0.1, (e.key, rel)
