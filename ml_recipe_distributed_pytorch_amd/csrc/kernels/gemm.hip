@@ -1178,15 +1178,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   }
 }
 
-// Spin kernel for the contention diagnostic (hq_cu_hog): 96 KiB of LDS keeps it alone on its CU, as a
-// GEMM workgroup would need that CU's whole LDS; s_memrealtime is the 100 MHz constant clock.
-__global__ __launch_bounds__(256) void cu_hog_kernel(long ticks) {
-  extern __shared__ char hog_lds[];
-  const long t0 = (long)__builtin_amdgcn_s_memrealtime();
-  while ((long)__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
-  if (threadIdx.x == 1023) hog_lds[0] = 0;   // never true: keeps the LDS allocation
-}
-
 // 0 = auto (v3 for K <= 2304, else v2), 1 = force v1, 2 = force v2, 3 = force v3; HQ_GEMM_VARIANT sets it
 int g_gemm_variant = [] {
   const char* e = getenv("HQ_GEMM_VARIANT");
@@ -1369,15 +1360,6 @@ void hq_gemm_set_sched(int v) {
     std::lock_guard<std::mutex> lock(g_sched_mu);
     (void)sched_pool_locked();
   }
-}
-void hq_cu_hog(int blocks, int usec, hipStream_t s) {
-  constexpr int lds = 96 * 1024;
-  static bool init = [] {
-    (void)hipFuncSetAttribute((const void*)cu_hog_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-    return true;
-  }();
-  (void)init;
-  hipLaunchKernelGGL(cu_hog_kernel, dim3(blocks), dim3(256), lds, s, (long)usec * 100);
 }
 
 // Kernel family for a shape: 256 / 128 = the 256-row kernels with that block width, 1 = vS (128² tiles),

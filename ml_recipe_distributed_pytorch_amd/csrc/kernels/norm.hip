@@ -304,11 +304,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
           float da[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) { da[i] = dz[i] * m[i]; acc[2][c][i] += da[i]; }
-          *reinterpret_cast<uint2*>(da_out + base + col) = hq_pack4(da);
-          if constexpr (Q8) {
+          const uint2 da_bf = hq_pack4(da);
+          *reinterpret_cast<uint2*>(da_out + base + col) = da_bf;
+          if constexpr (Q8) {   // from the bf16-rounded da, exactly what the bf16 copy holds
+            float r[4];
+            hq_unpack4(da_bf, r);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) amax8 = fmaxf(amax8, fabsf(da[i]));
-            *reinterpret_cast<uint32_t*>(da8 + base + col) = hq_pack_bf8x4(da, inv8);
+            for (int i = 0; i < 4; ++i) amax8 = fmaxf(amax8, fabsf(r[i]));
+            *reinterpret_cast<uint32_t*>(da8 + base + col) = hq_pack_bf8x4(r, inv8);
           }
         }
       }

@@ -297,14 +297,17 @@ def test_ln_bwd_e5m2_output(cuda, T, H):
         assert torch.equal(a, b)
     da, da8 = out[1].float(), out[2]
     assert da8.dtype == torch.float8_e5m2 and state[3].item() == 1.0
+
+    def close_codes(got, exp):   # x·(1/s) in the kernel vs x/s here: at most one code apart, rarely
+        diff = (got.view(torch.uint8).int() - exp.view(torch.uint8).int()).abs()
+        assert diff.max().item() <= 1 and (diff > 0).float().mean().item() < 1e-3
     assert torch.equal(da8.view(torch.uint8), _q5(da, 1.0).view(torch.uint8))
     amax = state[:3].view(torch.int32)[0].view(torch.float32).item()
     assert amax == da.abs().max().item()
     out2 = k.ln_bwd(dy, None, z, gamma, mean, rstd, 0.1, 7, 3, *grads8, True, q8=state, phase=1)
     s = state[3].item()
     assert s == pytest.approx(2 * amax / 57344, rel=1e-6)
-    diff = (out2[2].view(torch.uint8).int() - _q5(da, s).view(torch.uint8).int()).abs()
-    assert diff.max().item() <= 1 and (diff > 0).float().mean().item() < 1e-3
+    close_codes(out2[2], _q5(da, s))
 
 
 @pytest.mark.gpu
