@@ -240,15 +240,16 @@ int64_t gemm_fp8_supported(int64_t M, int64_t N, int64_t K) { return hq_gemm_fp8
 
 Tensor gemm_fp8(Tensor A8, Tensor B8, int64_t epi, c10::optional<Tensor> bias, Tensor sa, Tensor sb,
                 c10::optional<Tensor> pre, c10::optional<Tensor> out8, c10::optional<Tensor> state, int64_t phase,
-                c10::optional<Tensor> part) {
+                c10::optional<Tensor> part, c10::optional<Tensor> resid) {
   TORCH_CHECK(A8.is_cuda() && A8.element_size() == 1 && A8.is_contiguous() && B8.is_cuda() && B8.element_size() == 1 &&
               B8.is_contiguous(), "gemm_fp8: A8 / B8 must be contiguous 1-byte (fp8) GPU tensors");
   TORCH_CHECK(A8.dim() == 2 && B8.dim() == 2 && A8.size(1) == B8.size(1), "gemm_fp8: A8[M,K], B8[N,K]");
   TORCH_CHECK(B8.scalar_type() == at::kFloat8_e4m3fn, "gemm_fp8: B8 (weights) must be float8_e4m3fn");
   const int64_t M = A8.size(0), K = A8.size(1), N = B8.size(0);
   TORCH_CHECK(hq_gemm_fp8_supported((int)M, (int)N, (int)K), "gemm_fp8: unsupported shape M=", M, " N=", N, " K=", K);
-  const bool fwd = epi == HQ_EPI_BIAS || epi == HQ_EPI_GELUD, bwd = epi == HQ_EPI_NONE || epi == HQ_EPI_DMUL;
-  TORCH_CHECK(fwd || bwd, "gemm_fp8: epilogue must be BIAS / GELUD (forward) or NONE / DMUL (dgrad)");
+  const bool fwd = epi == HQ_EPI_BIAS || epi == HQ_EPI_GELUD;
+  const bool bwd = epi == HQ_EPI_NONE || epi == HQ_EPI_DMUL || epi == HQ_EPI_RESID;
+  TORCH_CHECK(fwd || bwd, "gemm_fp8: epilogue must be BIAS / GELUD (forward) or NONE / RESID / DMUL (dgrad)");
   TORCH_CHECK(A8.scalar_type() == (fwd ? at::kFloat8_e4m3fn : at::kFloat8_e5m2),
               "gemm_fp8: A8 must be float8_e4m3fn for the forward epilogues, float8_e5m2 for the dgrad ones");
   check(sa, F32, "sa"); check(sb, F32, "sb");
@@ -269,6 +270,12 @@ Tensor gemm_fp8(Tensor A8, Tensor B8, int64_t epi, c10::optional<Tensor> bias, T
     check(*part, F32, "part");
     TORCH_CHECK(part->numel() == (M / 256) * N, "gemm_fp8: part must hold [M/256, N]");
     pp = ptr<float>(*part);
+  }
+  if (epi == HQ_EPI_RESID) {
+    TORCH_CHECK(resid.has_value() && resid->defined(), "gemm_fp8: RESID needs `resid`");
+    check(*resid, BF16, "resid");
+    TORCH_CHECK(resid->size(0) == M && resid->size(1) == N, "gemm_fp8: resid shape");
+    P = ptr<uint16_t>(*resid);
   }
   if (epi == HQ_EPI_GELUD || epi == HQ_EPI_DMUL) {
     TORCH_CHECK(pre.has_value() && pre->defined(), "gemm_fp8: GELUD / DMUL need `pre` (gelu')");
@@ -450,8 +457,10 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor key_bias, int64_t B, int64_t L, 
   return {ctx, lse, mbits};
 }
 
-Tensor attn_bwd(Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, Tensor mbits, int64_t B, int64_t L,
-                int64_t nh, double p, double scale, bool deterministic) {
+// q8 given (--precision fp8): also dQKV as e5m2 under that delayed-scaling state -> [dqkv, dqkv8]
+std::vector<Tensor> attn_bwd_impl(Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, Tensor mbits, int64_t B,
+                                  int64_t L, int64_t nh, double p, double scale, bool deterministic,
+                                  c10::optional<Tensor> q8, int64_t phase) {
   check_attn(qkv, key_bias, B, L, nh);
   check(dctx, BF16, "dctx"); check(ctx, BF16, "ctx"); check(lse, F32, "lse");
   const int64_t H = qkv.size(1) / 3;
@@ -464,10 +473,24 @@ Tensor attn_bwd(Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias
   c10::DeviceGuard g(qkv.device());
   auto dqkv = at::empty_like(qkv);
   auto delta = at::empty({B, nh, L}, lse.options());
+  const bool want8 = q8.has_value() && q8->defined();
+  Tensor dqkv8;
+  if (want8) {
+    check(*q8, F32, "q8");
+    TORCH_CHECK(q8->numel() == 4, "attn_bwd: q8 must be f32[4]");
+    dqkv8 = at::empty(qkv.sizes(), qkv.options().dtype(at::kFloat8_e5m2));
+  }
   hq_attn_bwd(ptr<uint16_t>(dctx), ptr<uint16_t>(qkv), ptr<uint16_t>(ctx), ptr<float>(lse), ptr<float>(key_bias),
               p > 0 ? ptr<uint16_t>(mbits) : nullptr, ptr<uint16_t>(dqkv), ptr<float>(delta), (int)B, (int)L, (int)nh, 64,
-              (float)p, (float)scale, deterministic, cur_stream());
-  return dqkv;
+              (float)p, (float)scale, deterministic, cur_stream(), want8 ? reinterpret_cast<uint8_t*>(dqkv8.data_ptr()) : nullptr,
+              want8 ? ptr<float>(*q8) : nullptr, (int)(phase % 3));
+  if (want8) return {dqkv, dqkv8};
+  return {dqkv};
+}
+
+Tensor attn_bwd(Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, Tensor mbits, int64_t B, int64_t L,
+                int64_t nh, double p, double scale, bool deterministic) {
+  return attn_bwd_impl(dctx, qkv, ctx, lse, key_bias, mbits, B, L, nh, p, scale, deterministic, c10::nullopt, 0)[0];
 }
 
 // ------------------------------------------------------------------------------------ optimizer
@@ -676,7 +699,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("gemm_fp8_supported", &gemm_fp8_supported);
   m.def("gemm_fp8", &gemm_fp8, py::arg("A8"), py::arg("B8"), py::arg("epi"), py::arg("bias"), py::arg("sa"), py::arg("sb"),
         py::arg("pre") = py::none(), py::arg("out8") = py::none(), py::arg("state") = py::none(), py::arg("phase") = 0,
-        py::arg("part") = py::none());
+        py::arg("part") = py::none(), py::arg("resid") = py::none());
   m.def("span_fwd", &span_fwd);
   m.def("span_bwd", &span_bwd);
   m.def("set_dropout_seed", [](c10::optional<Tensor> t) {
@@ -696,6 +719,10 @@ PYBIND11_MODULE(_hq_kernels, m) {
         py::arg("p"), py::arg("seed"), py::arg("opid"), py::arg("scale"), py::arg("q8") = py::none(),
         py::arg("phase") = 0);
   m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd_q8", [](Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, Tensor mbits, int64_t B,
+                          int64_t L, int64_t nh, double p, double scale, bool deterministic, Tensor q8, int64_t phase) {
+    return attn_bwd_impl(dctx, qkv, ctx, lse, key_bias, mbits, B, L, nh, p, scale, deterministic, q8, phase);
+  });
   m.def("grad_norm", &grad_norm);
   m.def("sq_norm_partials", [](Tensor x, int64_t nparts) {
     check(x, F32, "x");

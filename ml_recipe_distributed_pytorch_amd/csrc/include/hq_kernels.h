@@ -49,13 +49,14 @@ void hq_bias_grad(const uint16_t* dy, float* part, HqOuts outs, int T, int N, bo
 // ---- attention.hip ----------------------------------------------------------------------------
 void hq_attn_set_force_slow(int v);          // tests: every ring-forward workgroup takes the slow path
 size_t hq_attn_mask_bytes(int B, int L, int nh);   // dropout keep-bits written by fwd, read by bwd
-// ctx8 / q8 / phase (optional, --precision fp8): ctx also written as e4m3 under the delayed-scaling state q8
+// ctx8 / q8 / phase (optional, --precision fp8): ctx also written as e4m3 under the delayed-scaling state q8;
+// in the backward dqkv8 / q8 / phase: dQKV also as e5m2 (the QKV dgrad's fp8 input)
 void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, float* lse, uint16_t* mbits, int B, int L,
                  int nh, int dh, float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s,
                  uint8_t* ctx8 = nullptr, float* q8 = nullptr, int phase = 0);
 void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx, const float* lse, const float* key_bias,
                  const uint16_t* mbits, uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p, float scale,
-                 bool deterministic, hipStream_t s);
+                 bool deterministic, hipStream_t s, uint8_t* dqkv8 = nullptr, float* q8 = nullptr, int phase = 0);
 
 // ---- optim.hip --------------------------------------------------------------------------------
 struct HqOptChunk {      // one work item of the fused optimizer: <= kOptChunk elements of one segment
@@ -122,8 +123,8 @@ void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, f
                 int S, bool accumulate, hipStream_t s);
 
 // fp8 NT GEMM (gemm_fp8.hip): C = A8·B8ᵀ·sa·sb (+ epilogue), B8 e4m3.  Forward epi ∈ {HQ_EPI_BIAS,
-// HQ_EPI_GELUD} with A8 e4m3; backward epi ∈ {HQ_EPI_NONE, HQ_EPI_DMUL (C ⊙ P, column sums into
-// part[M/256][N])} with A8 e5m2.  C8 != null (GELUD / DMUL): the output also as e4m3 / e5m2 under
+// HQ_EPI_GELUD} with A8 e4m3; backward epi ∈ {HQ_EPI_NONE, HQ_EPI_RESID (C + P), HQ_EPI_DMUL (C ⊙ P,
+// column sums into part[M/256][N])} with A8 e5m2.  C8 != null (GELUD / DMUL): the output also as e4m3 / e5m2 under
 // delayed scaling driven by the 4-float state q8 / phase.
 int hq_gemm_fp8_supported(int M, int N, int K);
 void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, uint16_t* P, const float* sa,

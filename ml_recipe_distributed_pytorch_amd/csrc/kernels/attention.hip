@@ -145,8 +145,10 @@ __device__ __forceinline__ void store_row64(uint16_t* out, const f32x16_t (&a)[2
     }
 }
 
-// store_row64 plus the same 8 bf16-rounded values per lane as e4m3 (x·inv8) at out8 (same element
-// offsets, one byte each); returns this lane's |max| for the delayed-scaling amax.
+// store_row64 plus the same 8 bf16-rounded values per lane as fp8 (x·inv8) at out8 (same element
+// offsets, one byte each): e4m3 (forward ctx) or, E5, e5m2 (backward dQ/dK/dV); returns this lane's |max|
+// for the delayed-scaling amax.
+template <bool E5 = false>
 __device__ __forceinline__ float store_row64_q8(uint16_t* out, uint8_t* out8, const f32x16_t (&a)[2], float mul,
                                                 float inv8, int hh) {
   float amax = 0.f;
@@ -166,7 +168,10 @@ __device__ __forceinline__ float store_row64_q8(uint16_t* out, uint8_t* out8, co
       hq_unpack8(w, f);   // quantise the bf16-rounded ctx, exactly what the bf16 copy holds
 #pragma unroll
       for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(f[e]));
-      *reinterpret_cast<uint2*>(out8 + col) = make_uint2(hq_pack_fp8x4(f, inv8), hq_pack_fp8x4(f + 4, inv8));
+      if constexpr (E5)
+        *reinterpret_cast<uint2*>(out8 + col) = make_uint2(hq_pack_bf8x4(f, inv8), hq_pack_bf8x4(f + 4, inv8));
+      else
+        *reinterpret_cast<uint2*>(out8 + col) = make_uint2(hq_pack_fp8x4(f, inv8), hq_pack_fp8x4(f + 4, inv8));
     }
   return amax;
 }
@@ -615,7 +620,7 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
     const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dctx, const uint16_t* __restrict__ ctx,
     const float* __restrict__ lse, const float* __restrict__ key_bias, const uint16_t* __restrict__ mbits,
     float* __restrict__ delta, uint16_t* __restrict__ dqkv, int L, int nh, int n_qb, float c_scale, float scale,
-    float kscale) {
+    float kscale, uint8_t* __restrict__ dqkv8, const float* __restrict__ q8, float* __restrict__ part8, int phase) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int RNS = RAHEAD + 2;
   const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
@@ -705,6 +710,7 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
       __builtin_amdgcn_s_barrier();
       if (kt + RAHEAD < n32) stage(kt + RAHEAD);
     }
+    if (dqkv8 != nullptr && lane == 0) part8[blockIdx.x * RW + wave] = 0.f;   // its (empty) amax partial
     return;
   }
   LdsOffsets lo_;
@@ -753,7 +759,15 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
       for (int d = 0; d < 2; ++d) dq[d] = mfma32(tr8(tK, 0, lo_, s, d), sb, dq[d]);
     }
   }
-  if (qok) store_row64(dqkv + ((size_t)b * L + qi) * ld + h * D, dq, scale, hh);
+  const size_t orow_q = ((size_t)b * L + qi) * ld + h * D;
+  if (dqkv8 != nullptr) {   // --precision fp8: dQ also as e5m2 for the QKV dgrad (delayed scaling)
+    const float inv8 = 1.f / hq_fp8_delayed_scale(q8, phase, kHqBf8Max);
+    float amax = qok ? store_row64_q8<true>(dqkv + orow_q, dqkv8 + orow_q, dq, scale, inv8, hh) : 0.f;
+    amax = hq_wave_max(amax);
+    if (lane == 0) part8[blockIdx.x * RW + wave] = amax;
+    return;
+  }
+  if (qok) store_row64(dqkv + orow_q, dq, scale, hh);
 }
 
 // dK/dV: keys on the lanes.  Per 32-query tile: S = Q'·Kᵀ (+ aug: −LSE, bias), dP = dO·Vᵀ, then
@@ -762,7 +776,8 @@ template <bool DROP, int NT>
 __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
     const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dctx, const float* __restrict__ lse,
     const float* __restrict__ delta, const float* __restrict__ key_bias, const uint16_t* __restrict__ mbits,
-    uint16_t* __restrict__ dqkv, int L, int nh, int n_kb, float c_scale, float scale, float kscale) {
+    uint16_t* __restrict__ dqkv, int L, int nh, int n_kb, float c_scale, float scale, float kscale,
+    uint8_t* __restrict__ dqkv8, const float* __restrict__ q8, float* __restrict__ part8, int phase) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // slot: Q' [32][64] 4 KB | dO [32][64] 4 KB | A' words [32] uint4 512 B | δ [32] f32 128 B | bits [RW][64] u16
   constexpr int SLOT = 2 * RTILE + 512 + 128 + RW * 128;
@@ -934,8 +949,20 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
       }
     }
   }
+  const size_t orow_k = ((size_t)b * L + kj) * ld + h * D;
+  if (dqkv8 != nullptr) {   // dK, dV also as e5m2; partial slots after the dQ kernel's
+    const float inv8 = 1.f / hq_fp8_delayed_scale(q8, phase, kHqBf8Max);
+    float amax = 0.f;
+    if (active && kok) {
+      amax = store_row64_q8<true>(dqkv + orow_k + 2 * H, dqkv8 + orow_k + 2 * H, dv, 1.f, inv8, hh);
+      amax = fmaxf(amax, store_row64_q8<true>(dqkv + orow_k + H, dqkv8 + orow_k + H, dk, LN2, inv8, hh));
+    }
+    amax = hq_wave_max(amax);
+    if (lane == 0) part8[(gridDim.x + blockIdx.x) * RW + wave] = amax;
+    return;
+  }
   if (active && kok) {
-    uint16_t* out = dqkv + ((size_t)b * L + kj) * ld + h * D;
+    uint16_t* out = dqkv + orow_k;
     store_row64(out + 2 * H, dv, 1.f, hh);
     store_row64(out + H, dk, LN2, hh);                   // Q' = c·Q with c = scale·log2e: dK = Σ dS·Q'/log2e
   }
@@ -1020,7 +1047,7 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
 
 void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx, const float* lse, const float* key_bias,
                  const uint16_t* mbits, uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p,
-                 float scale, bool deterministic, hipStream_t s) {
+                 float scale, bool deterministic, hipStream_t s, uint8_t* dqkv8, float* q8, int phase) {
   set_attn_prio();
   if (dh != D || L > 512) { fprintf(stderr, "hq_attn_bwd: head_dim %d / L %d unsupported\n", dh, L); abort(); }
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
@@ -1033,6 +1060,9 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
     constexpr int AH = 3;
     const size_t lds_dq = (size_t)(AH + 2) * 2 * RTILE + Lp * sizeof(uint4) + (bits ? (size_t)RW * n32 * 128 : 0);
     const size_t lds_kv = 2 * (size_t)(2 * RTILE + 512 + 128 + RW * 128);
+    // dQ and dK/dV grids are the same size: partials [dQ waves | dK/dV waves], one fold after both
+    const int nparts = B * nh * nb * RW;
+    float* part8 = dqkv8 ? hq_fp8_amax_parts((size_t)2 * nparts) : nullptr;
     auto run = [&](auto cn) {
       constexpr int NT = decltype(cn)::value;
       auto launch = [&](auto kdq, auto kkv) {
@@ -1040,9 +1070,9 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
             (hipFuncSetAttribute((const void*)kdq, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess);
         (void)attr;
         hipLaunchKernelGGL(kdq, dim3(B * nh * nb), dim3(RW * 64), lds_dq, s, qkv, dctx, ctx, lse, key_bias, bits, delta,
-                           dqkv, L, nh, nb, scale * LOG2E, scale, ks);
+                           dqkv, L, nh, nb, scale * LOG2E, scale, ks, dqkv8, q8, part8, phase);
         hipLaunchKernelGGL(kkv, dim3(B * nh * nb), dim3(RW * 64), lds_kv, s, qkv, dctx, lse, delta, key_bias, bits, dqkv,
-                           L, nh, nb, scale * LOG2E, scale, ks);
+                           L, nh, nb, scale * LOG2E, scale, ks, dqkv8, q8, part8, phase);
       };
       if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH>, attn_bwd_dkdv_ring_kernel<true, NT>);
       else launch(attn_bwd_dq_ring_kernel<false, NT, AH>, attn_bwd_dkdv_ring_kernel<false, NT>);
@@ -1052,5 +1082,6 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
     else if (L == 256) run(std::integral_constant<int, 8>{});
     else if (L == 128) run(std::integral_constant<int, 4>{});
     else run(std::integral_constant<int, 0>{});
+    if (dqkv8) hq_fp8_amax_fold(part8, 2 * nparts, q8, phase, s, kHqBf8Max);
   }
 }

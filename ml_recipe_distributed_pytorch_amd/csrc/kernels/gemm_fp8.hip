@@ -15,8 +15,8 @@
 //
 // Epilogues, forward (A = e4m3 activations): EPI_BIAS (QKV / out-proj / FFN2) and EPI_GELUD (FFN1:
 // act = gelu(pre), P = gelu'(pre)); Q8 additionally writes act as e4m3 for the next fp8 GEMM.
-// Backward dgrad (A = e5m2 activation gradient, B = e4m3 Wᵀ): EPI_NONE (FFN1 / out-proj dgrad) and
-// EPI_DMUL (FFN2 dgrad: dpre = (dy·W) ⊙ P with P = the stored gelu', plus per-tile column sums of dpre
+// Backward dgrad (A = e5m2 activation gradient, B = e4m3 Wᵀ): EPI_NONE (FFN1 / out-proj dgrad), EPI_RESID
+// (QKV dgrad + the residual gradient, read through P) and EPI_DMUL (FFN2 dgrad: dpre = (dy·W) ⊙ P with P = the stored gelu', plus per-tile column sums of dpre
 // for the FFN1 bias gradient); Q8 on DMUL writes dpre as e5m2 for the FFN1 dgrad.  The e5m2 range
 // (±57344) is what gradients need; the mixed-format MFMA takes the operand formats as immediates.
 // Every Q8 output is under DELAYED scaling: the scale is derived from the previous step's amax (slot
@@ -69,7 +69,7 @@ __device__ __forceinline__ float delayed_scale(const float* st, int phase) {
   return hq_fp8_delayed_scale(st, phase);   // first step: unit scale
 }
 
-constexpr bool grad_epi(int epi) { return epi == HQ_EPI_NONE || epi == HQ_EPI_DMUL; }
+constexpr bool grad_epi(int epi) { return epi == HQ_EPI_NONE || epi == HQ_EPI_DMUL || epi == HQ_EPI_RESID; }
 
 template <int EPI, bool Q8>
 __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
@@ -221,12 +221,16 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
     const int lr = it * ROWS_PER_IT + rsub;
     return m0 + (lr >> 6) * 128 + wm * 64 + (lr & 63);
   };
-  // DMUL's gelu' operand: all 16 pieces of this lane issued at once (one exposed HBM latency, gemm.hip v2)
-  uint4 aux[EPI == HQ_EPI_DMUL ? NIT : 1];
+  // DMUL's gelu' / RESID's residual (both via P): all 16 pieces of this lane issued at once (one exposed
+  // HBM latency, gemm.hip v2)
+  constexpr bool kAux = EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID;
+  uint4 aux[kAux ? NIT : 1];
   float csum[8];
-  if constexpr (EPI == HQ_EPI_DMUL) {
+  if constexpr (kAux) {
 #pragma unroll
     for (int it = 0; it < NIT; ++it) aux[it] = *reinterpret_cast<const uint4*>(P + (size_t)grow_of(it) * ldc + gcol);
+  }
+  if constexpr (EPI == HQ_EPI_DMUL) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[e] = 0.f;
   }
@@ -234,7 +238,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
     const int lr = it * ROWS_PER_IT + rsub;
     uint4 piece = *reinterpret_cast<const uint4*>(wreg + lr * RS + seg * 16);
     const size_t goff = (size_t)grow_of(it) * ldc + gcol;
-    if constexpr (EPI == HQ_EPI_DMUL) {
+    if constexpr (EPI == HQ_EPI_RESID) {
+      float d[8], rr[8];
+      hq_unpack8(piece, d);
+      hq_unpack8(aux[it], rr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) d[e] += rr[e];
+      piece = hq_pack8(d);
+    } else if constexpr (EPI == HQ_EPI_DMUL) {
       float d[8], gd[8];
       hq_unpack8(piece, d);
       hq_unpack8(aux[it], gd);
@@ -270,7 +281,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
     }
     *reinterpret_cast<uint4*>(C + goff) = piece;
   };
-  if constexpr (EPI == HQ_EPI_DMUL) {   // fully unrolled: aux[] must stay in registers
+  if constexpr (kAux) {   // fully unrolled: aux[] must stay in registers
 #pragma unroll
     for (int it = 0; it < NIT; ++it) piece_out(it);
   } else {
@@ -487,6 +498,7 @@ void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* b
       else launch<HQ_EPI_DMUL, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
       break;
     case HQ_EPI_NONE: launch<HQ_EPI_NONE, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s); break;
+    case HQ_EPI_RESID: launch<HQ_EPI_RESID, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s); break;
     default: launch<HQ_EPI_BIAS, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s); break;
   }
 }

@@ -186,8 +186,8 @@ class _LayerFn(torch.autograd.Function):
         # PRODUCERS under delayed scaling: QKV's by the previous layer's second LayerNorm (layer 0: one
         # quantisation pass over the embeddings), the out-projection's by the attention forward's ctx store,
         # FFN1's by this layer's first LayerNorm, FFN2's by FFN1's epilogue — so no standalone quantiser
-        # runs per layer.  In the backward the dgrads of FFN2, FFN1 and the out-projection run in fp8 too
-        # (e5m2 gradients, see backward); weight gradients and the QKV dgrad stay bf16.
+        # runs per layer.  In the backward every dgrad (FFN2, FFN1, out-projection, QKV) runs in fp8 too
+        # (e5m2 gradients, see backward); the weight gradients stay bf16.
         fp8 = fp8 and ops.fp8_gemm_ok(x.shape[0], 3 * cfg.hidden_size, cfg.hidden_size)
         s8 = m.fp8_states(idx) if fp8 else None
         if fp8:
@@ -270,16 +270,17 @@ class _LayerFn(torch.autograd.Function):
                 ops.linear_wgrad(dy, xin, gw, gb, acc)
         Wm = lambda k: st.view(p + k, "master")  # noqa: E731
         dh2 = dh2.contiguous()
-        # --precision fp8: the FFN2 / FFN1 / out-projection dgrads run on the fp8 MFMA kernel with e5m2
+        # --precision fp8: the FFN2 / FFN1 / out-projection / QKV dgrads run on the fp8 MFMA kernel with e5m2
         # gradients (range ±57344; e4m3's ±448 is too narrow for gradients) against the e4m3 Wᵀ copies —
         # each gradient written in e5m2 by its PRODUCER under delayed scaling: da2 and da1 by the LayerNorm
-        # backwards, dpre by the FFN2 dgrad's DMUL epilogue.  A gradient state has no current-scaling seed,
+        # backwards, dpre by the FFN2 dgrad's DMUL epilogue, dQKV by the attention backward.  A gradient state has no current-scaling seed,
         # so its consumer runs in bf16 until one production has recorded an amax (``calibrated``).
         T = dh2.shape[0]
         fp8 = (m.precision == "fp8" and dh2.is_cuda and m.fp8_dgrad and ctx.gelu_deriv
                and ops.fp8_gemm_ok(T, cfg.intermediate_size, cfg.hidden_size)
                and ops.fp8_gemm_ok(T, cfg.hidden_size, cfg.intermediate_size)
-               and ops.fp8_gemm_ok(T, cfg.hidden_size, cfg.hidden_size))
+               and ops.fp8_gemm_ok(T, cfg.hidden_size, cfg.hidden_size)
+               and ops.fp8_gemm_ok(T, cfg.hidden_size, 3 * cfg.hidden_size))
         s8 = m.fp8_states(idx) if fp8 else None
         W8T = lambda k: st.view_fp8_t(p + k)  # noqa: E731  (e4m3 Wᵀ + dequant scale)
 
@@ -316,12 +317,19 @@ class _LayerFn(torch.autograd.Function):
             dctx = ops.linear_dgrad_fp8(da1_8, s8["dout"], W8T("attention.output.dense.weight"))
         else:
             dctx = ops.linear_dgrad(da1, W("attention.output.dense.weight"), wt=WT("attention.output.dense.weight"))
-        dqkv = ops.attn_bwd(dctx, qkv, ctxv, lse, key_bias, ctx.bits, B, L, nh, ctx.pa, info.seed, op0, ctx.scale)
+        if fp8:
+            dqkv, dqkv8 = ops.attn_bwd_q8(dctx, qkv, ctxv, lse, key_bias, ctx.bits, B, L, nh, ctx.pa, ctx.scale,
+                                          s8["dqkv"])
+        else:
+            dqkv = ops.attn_bwd(dctx, qkv, ctxv, lse, key_bias, ctx.bits, B, L, nh, ctx.pa, info.seed, op0, ctx.scale)
         ctx.bits = None
         wgrad(dqkv, x, G("qkv.weight"), G("qkv.bias"))
         if trainable:
             m._group_ready(grp)
-        dx = ops.linear_dgrad_add(dqkv, W("qkv.weight"), dz1, wt=WT("qkv.weight"))
+        if fp8 and s8["dqkv"].calibrated:
+            dx = ops.linear_dgrad_add_fp8(dqkv8, s8["dqkv"], W8T("qkv.weight"), dz1)
+        else:
+            dx = ops.linear_dgrad_add(dqkv, W("qkv.weight"), dz1, wt=WT("qkv.weight"))
         return dx, None, None, None, None
 
 
@@ -457,7 +465,8 @@ class BertForQuestionAnswering(nn.Module):
         if st is None or st["qkv"].buf.device != self.store.device:
             st = {k: ops.Fp8DelayedState(self.store.device) for k in ("qkv", "out", "ffn1", "ffn2")}
             # activation gradients (e5m2): the inputs of the FFN2 / FFN1 / out-projection dgrads
-            st.update({k: ops.Fp8DelayedState(self.store.device, grad=True) for k in ("dffn2", "dffn1", "dout")})
+            st.update({k: ops.Fp8DelayedState(self.store.device, grad=True)
+                       for k in ("dffn2", "dffn1", "dout", "dqkv")})
             self._fp8_states[idx] = st
         return st
 

@@ -112,6 +112,13 @@ def attn_fwd_q8(qkv, key_bias, B, L, nh, p, seed, opid, scale, state: "Fp8Delaye
     return ctx, lse, bits, ctx8
 
 
+def attn_bwd_q8(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, scale, state: "Fp8DelayedState"):
+    """``attn_bwd`` that also writes dQKV in e5m2 under ``state`` — the delayed-scaling state of the fp8 QKV
+    dgrad that consumes it: (dqkv, dqkv8)."""
+    return tuple(_k().attn_bwd_q8(dctx, qkv, ctx, lse, key_bias, bits, int(B), int(L), int(nh), float(p), float(scale),
+                                  deterministic(), state.buf, state.next_phase()))
+
+
 def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale):
     if dctx.is_cuda:
         return _k().attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, int(B), int(L), int(nh), float(p), float(scale),
@@ -249,6 +256,13 @@ def linear_dgrad_fp8(dy8, dy_state: Fp8DelayedState, wt8s):
     ParamStore.view_fp8_t; bf16 out."""
     wt8, sw = wt8s
     return _k().gemm_fp8(dy8, wt8, _EPI_NONE, None, dy_state.scale, sw.reshape(1).float())
+
+
+def linear_dgrad_add_fp8(dy8, dy_state: Fp8DelayedState, wt8s, resid):
+    """resid + dy·W for an e5m2 gradient (the QKV dgrad plus the residual-gradient add, gemm_fp8.hip
+    EPI_RESID) against the e4m3 Wᵀ copy; bf16 out."""
+    wt8, sw = wt8s
+    return _k().gemm_fp8(dy8, wt8, _EPI_RESID, None, dy_state.scale, sw.reshape(1).float(), resid=resid)
 
 
 def linear_dgrad_gelu_fp8(dy8, dy_state: Fp8DelayedState, wt8s, gd, g_bias, accumulate, out_state: Fp8DelayedState):

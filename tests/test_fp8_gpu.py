@@ -327,7 +327,7 @@ def test_view_fp8_t_is_the_transposed_forward_copy(cuda):
 
 @pytest.mark.gpu
 def test_fp8_dgrad_step_close_to_bf16_dgrad(cuda):
-    """--precision fp8 with the e5m2 dgrads (FFN2 / FFN1 / out-projection) against the same model with bf16
+    """--precision fp8 with the e5m2 dgrads (FFN2 / FFN1 / out-projection / QKV) against the same model with bf16
     dgrads: after the gradient states calibrate (step 3), the parameter gradients agree to fp8 accuracy."""
     from ml_recipe_distributed_pytorch_amd.models.bert import BertForQuestionAnswering
     from ml_recipe_distributed_pytorch_amd.models.config import get_config
@@ -346,7 +346,7 @@ def test_fp8_dgrad_step_close_to_bf16_dgrad(cuda):
         torch.cuda.synchronize()
         if dg:
             s8 = m.fp8_states(0)
-            assert all(s8[k].calibrated for k in ("dffn2", "dffn1", "dout"))
+            assert all(s8[k].calibrated for k in ("dffn2", "dffn1", "dout", "dqkv"))
         grads[dg] = m.store.grad.clone()
     assert torch.isfinite(grads[True]).all()
     for e in m.store.entries:
@@ -354,3 +354,47 @@ def test_fp8_dgrad_step_close_to_bf16_dgrad(cuda):
             a, b = (grads[x][e.offset:e.offset + e.numel] for x in (True, False))
             rel = ((a - b).norm() / b.norm()).item()
             assert rel < 0.1, (e.key, rel)
+
+
+@pytest.mark.gpu
+def test_gemm_fp8_dgrad_resid(cuda):
+    """QKV dgrad form: C = bf16(dy8·Wᵀ8·sa·sb) + resid (EPI_RESID, e5m2 A operand)."""
+    k = _native.kernels()
+    M, N, K = 512, 768, 2304
+    g = torch.Generator(device=cuda).manual_seed(31)
+    sa = torch.full((1,), 1e-2 * 4 / 57344, device=cuda)
+    A8 = _q5(torch.randn(M, K, device=cuda, generator=g) * 1e-2, sa)
+    B8, sb = _q((torch.randn(N, K, device=cuda, generator=g) * 0.05).bfloat16())
+    R = (torch.randn(M, N, device=cuda, generator=g) * 1e-3).bfloat16()
+    C = k.gemm_fp8(A8, B8, 4, None, sa, sb, resid=R)
+    mm = ((A8.float() * sa) @ (B8.float() * sb).t()).bfloat16().float()
+    torch.testing.assert_close(C.float(), mm + R.float(), atol=2e-3 * mm.abs().max().item(), rtol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_attn_bwd_e5m2_output(cuda, p):
+    """Attention backward with the e5m2 copy of dQKV for the fp8 QKV dgrad: dqkv equals the plain call
+    bitwise, dqkv8 = e5m2(bf16(dqkv) / s) under the delayed scale, and the amax of BOTH kernels' outputs
+    (dQ from one, dK/dV from the other) lands in the state."""
+    k = _native.kernels()
+    B, L, nh = 2, 384, 12
+    g = torch.Generator(device=cuda).manual_seed(41)
+    qkv = torch.randn(B * L, 3 * nh * 64, device=cuda, generator=g).bfloat16()
+    kb = torch.zeros(B, L, device=cuda)
+    kb[1, 250:] = -10000.0
+    ctx, lse, bits = k.attn_fwd(qkv, kb, B, L, nh, p, 5, 9, 0.125)
+    dctx = (torch.randn(B * L, nh * 64, device=cuda, generator=g) * 1e-2).bfloat16()
+    ref = k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125, False)
+    state = torch.zeros(4, device=cuda)
+    dqkv, dqkv8 = k.attn_bwd_q8(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125, False, state, 0)
+    assert torch.equal(dqkv, ref)
+    assert dqkv8.dtype == torch.float8_e5m2 and state[3].item() == 1.0
+    assert torch.equal(dqkv8.view(torch.uint8), _q5(dqkv, 1.0).view(torch.uint8))
+    amax = state[:3].view(torch.int32)[0].view(torch.float32).item()
+    assert amax == dqkv.float().abs().max().item()
+    _, d8b = k.attn_bwd_q8(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125, False, state, 1)
+    s = state[3].item()
+    assert s == pytest.approx(2 * amax / 57344, rel=1e-6)
+    diff = (d8b.view(torch.uint8).int() - _q5(dqkv, s).view(torch.uint8).int()).abs()
+    assert diff.max().item() <= 1 and (diff > 0).float().mean().item() < 1e-3
