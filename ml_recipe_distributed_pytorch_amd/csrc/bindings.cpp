@@ -232,6 +232,26 @@ void gemm_tn(Tensor dy, Tensor x, Tensor out, bool accumulate, int64_t splits, c
              has_bias ? ptr<float>(*bias_out) : nullptr, (int)T, (int)N, (int)K, S, accumulate, cur_stream());
 }
 
+// fp8 weight gradient: out [N,K] f32 (+)= (dy8ᵀ·x8)·sa·sb, dy8 e5m2 [T,N], x8 e4m3 [T,K] (token-major)
+int64_t gemm_tn8_splits(int64_t T, int64_t N, int64_t K) { return hq_gemm_tn8_splits((int)T, (int)N, (int)K); }
+
+void gemm_tn8(Tensor dy8, Tensor x8, Tensor sa, Tensor sb, Tensor out, bool accumulate) {
+  TORCH_CHECK(dy8.is_cuda() && dy8.scalar_type() == at::kFloat8_e5m2 && dy8.is_contiguous() && dy8.dim() == 2,
+              "gemm_tn8: dy8 must be a contiguous float8_e5m2 [T,N] GPU tensor");
+  TORCH_CHECK(x8.is_cuda() && x8.scalar_type() == at::kFloat8_e4m3fn && x8.is_contiguous() && x8.dim() == 2 &&
+              x8.size(0) == dy8.size(0), "gemm_tn8: x8 must be a contiguous float8_e4m3fn [T,K] GPU tensor");
+  check(out, F32, "out"); check(sa, F32, "sa"); check(sb, F32, "sb");
+  const int64_t T = dy8.size(0), N = dy8.size(1), K = x8.size(1);
+  TORCH_CHECK(out.numel() == N * K, "gemm_tn8: out must hold N*K");
+  const int S = hq_gemm_tn8_splits((int)T, (int)N, (int)K);
+  TORCH_CHECK(S > 0, "gemm_tn8: unsupported shape T=", T, " N=", N, " K=", K, " (need N%128, K%128 == 0)");
+  c10::DeviceGuard g(dy8.device());
+  Tensor part = at::empty({S, N, K}, out.options());
+  hq_gemm_tn8(reinterpret_cast<const uint8_t*>(dy8.data_ptr()), reinterpret_cast<const uint8_t*>(x8.data_ptr()),
+              ptr<float>(sa), ptr<float>(sb), ptr<float>(part), ptr<float>(out), (int)T, (int)N, (int)K, S, accumulate,
+              cur_stream());
+}
+
 // fp8 projection GEMM, C (bf16) = A8·B8ᵀ·sa·sb (+ epilogue), B8 e4m3.  Forward (A8 e4m3): BIAS / GELUD
 // (+ bias f32; GELUD returns act, writes gelu' into `pre` and, with out8/state given, act as e4m3).
 // Backward dgrad (A8 e5m2): NONE / DMUL (C ⊙ pre, column sums into part [M/256, N]; with out8/state,
@@ -697,6 +717,8 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("fp8_quant_delayed_multi", &fp8_quant_delayed_multi);
   m.def("fp8_quant_multi_blocks", &fp8_quant_multi_blocks);
   m.def("gemm_fp8_supported", &gemm_fp8_supported);
+  m.def("gemm_tn8_splits", &gemm_tn8_splits);
+  m.def("gemm_tn8", &gemm_tn8);
   m.def("gemm_fp8", &gemm_fp8, py::arg("A8"), py::arg("B8"), py::arg("epi"), py::arg("bias"), py::arg("sa"), py::arg("sb"),
         py::arg("pre") = py::none(), py::arg("out8") = py::none(), py::arg("state") = py::none(), py::arg("phase") = 0,
         py::arg("part") = py::none(), py::arg("resid") = py::none());

@@ -121,6 +121,11 @@ void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
 int hq_gemm_tn_splits(int T, int N, int K);
 void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, float* bpart, float* bout, int T, int N, int K,
                 int S, bool accumulate, hipStream_t s);
+// fp8 form (--precision fp8): A = dy e5m2, B = x e4m3 (token-major bytes), dequantised by sa[0]·sb[0]; same
+// slabs / reduce, no fused bias.  hq_gemm_tn8_splits: split count, 0 = unsupported.
+int hq_gemm_tn8_splits(int T, int N, int K);
+void hq_gemm_tn8(const uint8_t* A, const uint8_t* B, const float* sa, const float* sb, float* part, float* out, int T,
+                 int N, int K, int S, bool accumulate, hipStream_t s);
 
 // fp8 NT GEMM (gemm_fp8.hip): C = A8·B8ᵀ·sa·sb (+ epilogue), B8 e4m3.  Forward epi ∈ {HQ_EPI_BIAS,
 // HQ_EPI_GELUD} with A8 e4m3; backward epi ∈ {HQ_EPI_NONE, HQ_EPI_RESID (C + P), HQ_EPI_DMUL (C ⊙ P,

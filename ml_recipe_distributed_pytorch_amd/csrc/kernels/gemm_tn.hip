@@ -16,7 +16,14 @@
 // (8 distinct values across the 8 rows → conflict-free).  The DMA image is lane-linear, so the
 // swizzle is applied on the per-lane SOURCE chunk and undone on the read (playbook rule 21).
 //
-// Optional fused bias gradient (BIAS): db[n] = Σ_t dy[t, n] is dyᵀ·1, so the first column-tile's
+// fp8 variant (gemm_tn8_kernel, --precision fp8): dy in e5m2 and x in e4m3, both token-major bytes as their
+// producers wrote them, on v_mfma_scale_f32_16x16x128_f8f6f4.  One MFMA consumes 128 tokens, so a K-tile is
+// 128 tokens and a half-panel [128 tokens][128 columns] = 16 KiB — the same bytes, DMA instructions, phase
+// table and waits as the bf16 kernel; the fragments (32 consecutive tokens of one column per lane) come
+// from four ds_read_b64_tr_b8 per operand (8 tokens each), conflict-free under the row swizzle
+//   f8(t) = ((t >> 1) & 3) | ((t >> 5) & 1) << 2   (16-B chunks of 128-B rows; tools/fp8_lab/tr8_probe.hip).
+//
+// Optional fused bias gradient (bf16 kernel only, BIAS): db[n] = Σ_t dy[t, n] is dyᵀ·1, so the first column-tile's
 // blocks run, in their k-column-0 waves, one extra MFMA per dy fragment against a constant ones
 // fragment (12.5 % more MFMAs in a third of the waves of a third of the blocks) and write fp32 partials
 // [S][N] that the same reduce kernel folds in — replacing a separate 450 MB column-sum pass.
@@ -251,6 +258,176 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const uint16_t* __
   }
 }
 
+// ------------------------------------------------------------------ fp8 (e5m2 dy × e4m3 x)
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+constexpr int BT8 = 128;   // tokens (bytes) per K-tile
+
+__device__ __forceinline__ int tswz8(int t) { return ((t >> 1) & 3) | (((t >> 5) & 1) << 2); }
+
+// w: the x fragment (e4m3, format 0); g: the dy fragment (e5m2, format 1); unit e8m0 block scales
+__device__ __forceinline__ f32x4_t mfma_tn8(const i32x8& w, const i32x8& g, const f32x4_t& c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w, g, c, 0, 1, 0, 127, 0, 127);
+}
+
+// 32 consecutive tokens (32·G … +31, G = lane >> 4) of column cblk·16 + (lane & 15) from a half image at
+// LDS byte address `img`: four transposed reads of 8 tokens each (rows +0, +8, +16, +24 → offsets 1 KiB
+// apart).  `roff` = (32G + q)·128 + 8p and `sw` = f8(32G + q) are lane constants (q = (lane>>1)&7,
+// p = lane&1: lane 2q + p of a 16-lane group addresses row q, bytes 8p … 8p+7 of the column block).
+__device__ __forceinline__ i32x8 trfrag8(uint32_t img, int roff, int sw, int cblk) {
+  const uint32_t a = img + roff + ((cblk ^ sw) << 4);
+  typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+  u32x2 r0, r1, r2, r3;
+  asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(r0) : "v"(a) : "memory");
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:1024" : "=v"(r1) : "v"(a) : "memory");
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:2048" : "=v"(r2) : "v"(a) : "memory");
+  asm volatile("ds_read_b64_tr_b8 %0, %1 offset:3072" : "=v"(r3) : "v"(a) : "memory");
+  i32x8 v;
+  v[0] = (int)r0[0]; v[1] = (int)r0[1]; v[2] = (int)r1[0]; v[3] = (int)r1[1];
+  v[4] = (int)r2[0]; v[5] = (int)r2[1]; v[6] = (int)r3[0]; v[7] = (int)r3[1];
+  return v;
+}
+
+// No fused bias variant: its 40 extra VGPRs (bias accumulators + a ones fragment) spill at 256; the fp8
+// step runs the one wgrad with a bias (QKV) in bf16.
+__global__ __launch_bounds__(kThreads, 1) void gemm_tn8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                               float* __restrict__ part, const float* __restrict__ sa,
+                                                               const float* __restrict__ sb, int T, int N, int K, int S,
+                                                               int tiles_k) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tiles = nwg / S;
+  const int split = id / tiles, tile = id % tiles;
+  const int n0 = (tile / tiles_k) * 256, k0 = (tile % tiles_k) * 256;
+  const int nkt = (T + BT8 - 1) / BT8;
+  const int kt0 = (int)((long)split * nkt / S), kt1 = (int)((long)(split + 1) * nkt / S);
+  const int nt = kt1 - kt0;
+  const int rows = min(nt * BT8, T - kt0 * BT8);
+  HQ_DASSERT(n0 + 128 <= N && k0 + 128 <= K && nt >= 2 && rows > 0);
+
+  const uint8_t* Ab = A + (size_t)kt0 * BT8 * N + n0;
+  const uint8_t* Bb = B + (size_t)kt0 * BT8 * K + k0;
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, rows * N, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, rows * K, 0x00020000);
+
+  // staging: wave w moves rows (2w + i)·8 … +7 of a half (1 KiB per instruction, lane-linear: lane L → row
+  // +L/8, 16-B slot L%8), loading the source chunk that the swizzle places there
+  int voA[2], voB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 8 + (lane >> 3);
+    const int c16 = (lane & 7) ^ tswz8(row);
+    voA[i] = row * N + c16 * 16;
+    voB[i] = row * K + c16 * 16;
+  }
+  auto dma = [&](const __amdgpu_buffer_rsrc_t& rs, const int (&vo)[2], int ld, int half, int t, char* img) {
+    char* dst = img + wave_u * 2048;
+    const int so = half * 128 + t * BT8 * ld;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + i * 1024), 16, vo[i], so, 0, 0);
+  };
+  auto stA = [&](int half, int t) { dma(rA, voA, N, half, t, smem + (t & 1) * STAGE + half * HALF); };
+  auto stB = [&](int half, int t) { dma(rB, voB, K, half, t, smem + (t & 1) * STAGE + (2 + half) * HALF); };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int G = lane >> 4, qq = (lane >> 1) & 7, pp = lane & 1;
+  const int roff = (32 * G + qq) * 128 + 8 * pp;
+  const int sw = tswz8(32 * G + qq);
+  i32x8 af[4], bf0[2], bf1[2];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  auto readA = [&](int t, int mh) {
+    const uint32_t img = lds0 + (t & 1) * STAGE + mh * HALF;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = trfrag8(img, roff, sw, wm * 4 + i);
+  };
+  auto readB = [&](int t, int nh, i32x8 (&bf)[2]) {
+    const uint32_t img = lds0 + (t & 1) * STAGE + (2 + nh) * HALF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bf[j] = trfrag8(img, roff, sw, wn * 2 + j);
+  };
+  auto mma = [&](int mh, int nh, const i32x8 (&bf)[2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[mh * 4 + i][nh * 2 + j] = mfma_tn8(bf[j], af[i], acc[mh * 4 + i][nh * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = []() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // prologue, schedule and waits: identical to gemm_tn_kernel (2 DMA instructions per wave per half)
+  stA(0, 0); stB(0, 0); stB(1, 0); stA(1, 0); stA(0, 1); stB(0, 1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  bar();
+  auto ktile = [&](int t) {
+    const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
+    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    readB(t, 0, bf0);
+    readA(t, 0);
+    if (more1) stB(1, t + 1);
+    bar();
+    mma(0, 0, bf0);
+    bar();
+    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    readB(t, 1, bf1);
+    if (more1) stA(1, t + 1);
+    bar();
+    mma(0, 1, bf1);
+    bar();
+    readA(t, 1);
+    if (more2) stA(0, t + 2);
+    bar();
+    mma(1, 1, bf1);
+    bar();
+    if (more1) {
+      if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    }
+    if (more2) stB(0, t + 2);
+    bar();
+    mma(1, 0, bf0);
+    bar();
+  };
+  if (__builtin_amdgcn_readfirstlane(wm) == 0) {
+    for (int t = 0; t < nt; ++t) ktile(t);
+    bar();
+  } else {
+    bar();
+    for (int t = 0; t < nt; ++t) ktile(t);
+  }
+
+  // epilogue: fp32 slab of the dequantised product
+  const float dq = sa[0] * sb[0];
+  float* out = part + (size_t)split * N * K;
+  const int fr = lane & 15, fq = lane >> 4;
+  const bool n_full = n0 + 256 <= N, k_full = k0 + 256 <= K;
+#pragma unroll
+  for (int I = 0; I < 8; ++I) {
+    const int row = n0 + (I >> 2) * 128 + wm * 64 + (I & 3) * 16 + fr;
+    if (!n_full && (I >> 2) == 1) continue;
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+      if (!k_full && (J >> 1) == 1) continue;
+      const int col = k0 + (J >> 1) * 128 + wn * 32 + (J & 1) * 16 + fq * 4;
+      *reinterpret_cast<float4*>(out + (size_t)row * K + col) =
+          make_float4(acc[I][J][0] * dq, acc[I][J][1] * dq, acc[I][J][2] * dq, acc[I][J][3] * dq);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(const float4* __restrict__ part, int S, size_t n4,
                                                             float4* __restrict__ out, int accumulate) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
@@ -315,4 +492,32 @@ void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, f
   if (bout)
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((N / 4 + 255) / 256), dim3(256), 0, s, (const float4*)bpart, S,
                        (size_t)N / 4, (float4*)bout, accumulate ? 1 : 0);
+}
+
+int hq_gemm_tn8_splits(int T, int N, int K) {
+  if (T <= 0 || N % 128 || K % 128 || N < 128 || K < 128) return 0;
+  if ((size_t)T * N >= (1ull << 31) || (size_t)T * K >= (1ull << 31)) return 0;
+  const int tiles = ((N + 255) / 256) * ((K + 255) / 256);
+  int S = 256 / tiles;
+  if (S < 1) S = 1;
+  const int nkt = (T + BT8 - 1) / BT8;
+  while (S > 1 && nkt / S < 4) --S;
+  if (nkt < 2) return 0;
+  return S;
+}
+
+void hq_gemm_tn8(const uint8_t* A, const uint8_t* B, const float* sa, const float* sb, float* part, float* out, int T,
+                 int N, int K, int S, bool accumulate, hipStream_t s) {
+  constexpr size_t lds = 2 * STAGE;
+  static bool init = [] {
+    (void)hipFuncSetAttribute((const void*)gemm_tn8_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    return true;
+  }();
+  (void)init;
+  const int tiles_k = (K + 255) / 256, tiles = ((N + 255) / 256) * tiles_k;
+  hipLaunchKernelGGL(gemm_tn8_kernel, dim3(tiles * S), dim3(kThreads), lds, s, A, B, part, sa, sb, T, N, K, S, tiles_k);
+  const size_t n4 = (size_t)N * K / 4;
+  const int grid = (int)std::min<size_t>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(grid), dim3(256), 0, s, (const float4*)part, S, n4, (float4*)out,
+                     accumulate ? 1 : 0);
 }

@@ -186,8 +186,9 @@ class _LayerFn(torch.autograd.Function):
         # PRODUCERS under delayed scaling: QKV's by the previous layer's second LayerNorm (layer 0: one
         # quantisation pass over the embeddings), the out-projection's by the attention forward's ctx store,
         # FFN1's by this layer's first LayerNorm, FFN2's by FFN1's epilogue — so no standalone quantiser
-        # runs per layer.  In the backward every dgrad (FFN2, FFN1, out-projection, QKV) runs in fp8 too
-        # (e5m2 gradients, see backward); the weight gradients stay bf16.
+        # runs per layer.  In the backward every dgrad (FFN2, FFN1, out-projection, QKV) and the weight
+        # gradients of the out-projection, FFN1 and FFN2 run in fp8 too (e5m2 gradients, see backward): the
+        # e4m3 inputs written here are kept for those weight gradients.
         fp8 = fp8 and ops.fp8_gemm_ok(x.shape[0], 3 * cfg.hidden_size, cfg.hidden_size)
         s8 = m.fp8_states(idx) if fp8 else None
         if fp8:
@@ -234,6 +235,9 @@ class _LayerFn(torch.autograd.Function):
             h2, z2, m2, r2 = ops.linear_bdr_ln_fwd(act, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), h1,
                                                    kinds[name], *ln2)
         ctx.save_for_backward(x, key_bias, qkv, ctxv, lse, z1, m1, r1, h1, pre, act, z2, m2, r2)
+        # e4m3 inputs of the out-projection / FFN1 / FFN2 GEMMs (their scales stay in the states until the next
+        # forward re-quantises), for the fp8 weight gradients
+        ctx.f8 = (ctx8, h1_8, act8) if (fp8 and act8 is not None and h1_8 is not None) else None
         ctx.bits = bits
         ctx.info, ctx.idx, ctx.ph, ctx.pa, ctx.scale = info, idx, ph, pa, scale
         return h2
@@ -257,17 +261,26 @@ class _LayerFn(torch.autograd.Function):
         WT = lambda k: st.view_t(p + k)  # noqa: E731  (Wᵀ working copy, GPU only)
         side = m.grad_side_stream if dh2.is_cuda else None
 
-        def wgrad(dy, xin, gw, gb):  # dW (+db) — on the side stream when enabled (overlaps the dgrad chain)
+        def wgrad(dy, xin, gw, gb, q=None):  # dW (+db) — on the side stream when enabled (overlaps the dgrads)
+            """q = (dy8, dy_state, x8, x_state): the fp8 form (no bias) once the gradient state is calibrated."""
             if not trainable:
                 return
+            use8 = q is not None and q[0] is not None and q[1].calibrated and ops.fp8_wgrad_ok(
+                dy.shape[0], dy.shape[1], xin.shape[1])
+
+            def run():
+                if use8:
+                    ops.linear_wgrad_fp8(q[0], q[1], q[2], q[3], gw, acc)
+                else:
+                    ops.linear_wgrad(dy, xin, gw, gb, acc)
             if side is None:
-                ops.linear_wgrad(dy, xin, gw, gb, acc)
+                run()
                 return
             side.wait_stream(torch.cuda.current_stream())
-            dy.record_stream(side)
-            xin.record_stream(side)
+            for t in ((dy, xin) + ((q[0], q[2]) if use8 else ())):
+                t.record_stream(side)
             with torch.cuda.stream(side):
-                ops.linear_wgrad(dy, xin, gw, gb, acc)
+                run()
         Wm = lambda k: st.view(p + k, "master")  # noqa: E731
         dh2 = dh2.contiguous()
         # --precision fp8: the FFN2 / FFN1 / out-projection / QKV dgrads run on the fp8 MFMA kernel with e5m2
@@ -283,6 +296,8 @@ class _LayerFn(torch.autograd.Function):
                and ops.fp8_gemm_ok(T, cfg.hidden_size, 3 * cfg.hidden_size))
         s8 = m.fp8_states(idx) if fp8 else None
         W8T = lambda k: st.view_fp8_t(p + k)  # noqa: E731  (e4m3 Wᵀ + dequant scale)
+        f8 = ctx.f8 if fp8 else None          # (ctx8, h1_8, act8): e4m3 forward inputs for the fp8 wgrads
+        ctx.f8 = None
 
         # --- FFN block ------------------------------------------------------------------------
         ln2b = (dh2, None, z2, Wm("output.LayerNorm.weight"), m2, r2, ctx.ph, info.seed, op0 + 2,
@@ -291,7 +306,7 @@ class _LayerFn(torch.autograd.Function):
             dz2, da2, da2_8 = ops.ln_bwd_q8(*ln2b, s8["dffn2"])
         else:
             dz2, da2 = ops.ln_bwd(*ln2b)
-        wgrad(da2, act, G("output.dense.weight"), None)
+        wgrad(da2, act, G("output.dense.weight"), None, (da2_8, s8["dffn2"], f8[2], s8["ffn2"]) if f8 else None)
         dpre8 = None
         if fp8 and s8["dffn2"].calibrated:
             dpre, dpre8 = ops.linear_dgrad_gelu_fp8(da2_8, s8["dffn2"], W8T("output.dense.weight"), pre,
@@ -299,7 +314,7 @@ class _LayerFn(torch.autograd.Function):
         else:
             dpre = ops.linear_dgrad_gelu_d(da2, W("output.dense.weight"), pre, ctx.gelu_deriv,
                                            G("intermediate.dense.bias"), acc, wt=WT("output.dense.weight"))
-        wgrad(dpre, h1, G("intermediate.dense.weight"), None)
+        wgrad(dpre, h1, G("intermediate.dense.weight"), None, (dpre8, s8["dffn1"], f8[1], s8["ffn1"]) if f8 else None)
         if dpre8 is not None and s8["dffn1"].calibrated:
             dh1_ffn = ops.linear_dgrad_fp8(dpre8, s8["dffn1"], W8T("intermediate.dense.weight"))
         else:
@@ -312,7 +327,8 @@ class _LayerFn(torch.autograd.Function):
             dz1, da1, da1_8 = ops.ln_bwd_q8(*ln1b, s8["dout"])
         else:
             dz1, da1 = ops.ln_bwd(*ln1b)
-        wgrad(da1, ctxv, G("attention.output.dense.weight"), None)
+        wgrad(da1, ctxv, G("attention.output.dense.weight"), None,
+              (da1_8, s8["dout"], f8[0], s8["out"]) if f8 else None)
         if fp8 and s8["dout"].calibrated:
             dctx = ops.linear_dgrad_fp8(da1_8, s8["dout"], W8T("attention.output.dense.weight"))
         else:

@@ -280,6 +280,17 @@ def linear_dgrad_gelu_fp8(dy8, dy_state: Fp8DelayedState, wt8s, gd, g_bias, accu
     return dpre, dpre8
 
 
+def fp8_wgrad_ok(T: int, N: int, K: int) -> bool:
+    return _k().gemm_tn8_splits(int(T), int(N), int(K)) > 0
+
+
+def linear_wgrad_fp8(dy8, dy_state: Fp8DelayedState, x8, x_state: Fp8DelayedState, g_w, accumulate):
+    """g_w (fp32 arena view) (+)= dyᵀ·x from the e5m2 gradient and the e4m3 forward input their producers
+    wrote (gemm_tn.hip gemm_tn8_kernel, split-K, dequantised by both states' scales).  No bias: the fp8 step
+    takes its bias gradients from the LayerNorm backward / DMUL column sums (QKV's wgrad stays bf16)."""
+    _k().gemm_tn8(dy8, x8, dy_state.scale, x_state.scale, g_w, bool(accumulate))
+
+
 def linear_gelu_fwd(x, w, b, b32=None):
     """(pre, act) with pre = x·Wᵀ + b, act = gelu(pre) — the CPU oracle form; the GPU uses
     ``linear_gelu_fwd_d`` (derivative stored instead of pre)."""

@@ -328,7 +328,8 @@ def test_view_fp8_t_is_the_transposed_forward_copy(cuda):
 @pytest.mark.gpu
 def test_fp8_dgrad_step_close_to_bf16_dgrad(cuda):
     """--precision fp8 with the e5m2 dgrads (FFN2 / FFN1 / out-projection / QKV) against the same model with bf16
-    dgrads: after the gradient states calibrate (step 3), the parameter gradients agree to fp8 accuracy."""
+    dgrads: after the gradient states calibrate (step 3), the parameter gradients agree to fp8 accuracy
+    (the out-projection / FFN weight gradients run on the fp8 TN kernel from step 2 on)."""
     from ml_recipe_distributed_pytorch_amd.models.bert import BertForQuestionAnswering
     from ml_recipe_distributed_pytorch_amd.models.config import get_config
     cfg = get_config("bert-base-uncased", num_hidden_layers=2, hidden_dropout_prob=0.0,
@@ -398,3 +399,36 @@ def test_attn_bwd_e5m2_output(cuda, p):
     assert s == pytest.approx(2 * amax / 57344, rel=1e-6)
     diff = (d8b.view(torch.uint8).int() - _q5(dqkv, s).view(torch.uint8).int()).abs()
     assert diff.max().item() <= 1 and (diff > 0).float().mean().item() < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,N,K", [(1024, 768, 768), (1024, 3072, 768), (2048, 768, 3072), (1000, 256, 384)])
+def test_gemm_tn8_wgrad(cuda, T, N, K):
+    """fp8 weight gradient (ds_read_b64_tr_b8 fragments, mixed e5m2 × e4m3 MFMA): out (+)= (dy8·sa)ᵀ(x8·sb)
+    against the fp32 product of the dequantised operands; a token tail (T % 128) stages zero rows."""
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(T + N + K)
+    sa = torch.full((1,), 1e-2 * 4 / 57344, device=cuda)
+    dy8 = _q5(torch.randn(T, N, device=cuda, generator=g) * 1e-2, sa)
+    x8, sb = _q(torch.randn(T, K, device=cuda, generator=g).bfloat16())
+    ref = (dy8.float() * sa).t() @ (x8.float() * sb)
+    out = torch.full((N, K), 0.5, device=cuda)
+    k.gemm_tn8(dy8, x8, sa, sb, out, True)
+    torch.testing.assert_close(out, ref + 0.5, atol=1e-4 * ref.abs().max().item() + 1e-6, rtol=1e-4)
+    k.gemm_tn8(dy8, x8, sa, sb, out, False)
+    torch.testing.assert_close(out, ref, atol=1e-4 * ref.abs().max().item(), rtol=1e-4)
+
+
+@pytest.mark.gpu
+def test_gemm_tn8_exact(cuda):
+    """Small integers (exact in e5m2 / e4m3 / fp32): any slip in the transposed-read lane map or the swizzle
+    shows as a wrong integer."""
+    k = _native.kernels()
+    T, N, K = 512, 256, 512
+    t = torch.arange(T, device=cuda)[:, None]
+    dy = ((t * 5 + torch.arange(N, device=cuda)[None, :] * 3) % 7 - 3).float()
+    x = ((t * 3 + torch.arange(K, device=cuda)[None, :] * 11 + 1) % 5 - 2).float()
+    one = torch.ones(1, device=cuda)
+    out = torch.zeros(N, K, device=cuda)
+    k.gemm_tn8(dy.to(torch.float8_e5m2), x.to(torch.float8_e4m3fn), one, one, out, False)
+    assert torch.equal(out, dy.t() @ x)
