@@ -145,10 +145,8 @@ __device__ __forceinline__ void store_row64(uint16_t* out, const f32x16_t (&a)[2
     }
 }
 
-// store_row64 plus the same 8 bf16-rounded values per lane as fp8 (x·inv8) at out8 (same element
-// offsets, one byte each): e4m3 (forward ctx) or, E5, e5m2 (backward dQ/dK/dV); returns this lane's |max|
-// for the delayed-scaling amax.
-template <bool E5 = false>
+// store_row64 plus the same 8 bf16-rounded values per lane as e4m3 (x·inv8) at out8 (same element
+// offsets, one byte each); returns this lane's |max| for the delayed-scaling amax.
 __device__ __forceinline__ float store_row64_q8(uint16_t* out, uint8_t* out8, const f32x16_t (&a)[2], float mul,
                                                 float inv8, int hh) {
   float amax = 0.f;
@@ -168,10 +166,48 @@ __device__ __forceinline__ float store_row64_q8(uint16_t* out, uint8_t* out8, co
       hq_unpack8(w, f);   // quantise the bf16-rounded ctx, exactly what the bf16 copy holds
 #pragma unroll
       for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(f[e]));
-      if constexpr (E5)
-        *reinterpret_cast<uint2*>(out8 + col) = make_uint2(hq_pack_bf8x4(f, inv8), hq_pack_bf8x4(f + 4, inv8));
-      else
-        *reinterpret_cast<uint2*>(out8 + col) = make_uint2(hq_pack_fp8x4(f, inv8), hq_pack_fp8x4(f + 4, inv8));
+      *reinterpret_cast<uint2*>(out8 + col) = make_uint2(hq_pack_fp8x4(f, inv8), hq_pack_fp8x4(f + 4, inv8));
+    }
+  return amax;
+}
+
+// store_row64 plus an e5m2 copy (x·inv8) at out8 for the backward's dQ / dK / dV (the fp8 QKV dgrad's
+// input), quantised from the fp32 values (one rounding; the bf16 copy is rounded separately): the four
+// fp8 bytes of each 4-column half are packed BEFORE the permlane32 swap, so one swap of one dword places
+// them like the bf16 words.  Saturation (only needed when this step's amax outgrew the delayed scale's 2×
+// headroom) runs as a wave-uniform branch.  Returns this lane's |max| for the amax.
+__device__ __forceinline__ uint32_t bf8x4_raw(float a, float b, float c, float d) {
+  const uint32_t w = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
+  return __builtin_amdgcn_cvt_pk_bf8_f32(c, d, w, true);
+}
+__device__ __forceinline__ float store_row64_e5(uint16_t* out, uint8_t* out8, const f32x16_t (&a)[2], float mul,
+                                                float inv8, int hh) {
+  float amax = 0.f;   // of the scaled values (|x·mul| = |x|·|mul|)
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) amax = fmaxf(amax, fmaxf(fabsf(a[d][r]), fabsf(a[d][r + 1])));
+  amax *= fabsf(mul);
+  // rare: this step's amax outgrew the scale's headroom — the fp8 copy saturates to ±57344 (e5m2 would
+  // overflow to inf); the bf16 copy is unaffected
+  const bool sat = __any(amax * inv8 >= kHqBf8Max);
+  const float lim = kHqBf8Max / inv8;
+  auto q = [&](float x) { return (sat ? fminf(fmaxf(x, -lim), lim) : x) * inv8; };
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int g = 0; g < 4; g += 2) {
+      const float va[4] = {a[d][4 * g] * mul, a[d][4 * g + 1] * mul, a[d][4 * g + 2] * mul, a[d][4 * g + 3] * mul};
+      const float vb[4] = {a[d][4 * g + 4] * mul, a[d][4 * g + 5] * mul, a[d][4 * g + 6] * mul, a[d][4 * g + 7] * mul};
+      const uint2 A = hq_pack4(va), B = hq_pack4(vb);
+      const auto r0 = __builtin_amdgcn_permlane32_swap(A.x, B.x, false, false);
+      const auto r1 = __builtin_amdgcn_permlane32_swap(A.y, B.y, false, false);
+      const int col = d * 32 + 8 * g + 8 * hh;
+      *reinterpret_cast<uint4*>(out + col) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+      const uint32_t A8 = bf8x4_raw(q(va[0]), q(va[1]), q(va[2]), q(va[3]));
+      const uint32_t B8 = bf8x4_raw(q(vb[0]), q(vb[1]), q(vb[2]), q(vb[3]));
+      const auto r8 = __builtin_amdgcn_permlane32_swap(A8, B8, false, false);
+      *reinterpret_cast<uint2*>(out8 + col) = make_uint2(r8[0], r8[1]);
     }
   return amax;
 }
@@ -615,7 +651,7 @@ __device__ __forceinline__ void split3(float x, uint16_t& hi, uint16_t& mid, uin
   lo = bf16_rne(r - hq_bf2f(mid));
 }
 
-template <bool DROP, int NT, int RAHEAD>
+template <bool DROP, int NT, int RAHEAD, bool Q8 = false>
 __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
     const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dctx, const uint16_t* __restrict__ ctx,
     const float* __restrict__ lse, const float* __restrict__ key_bias, const uint16_t* __restrict__ mbits,
@@ -710,7 +746,7 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
       __builtin_amdgcn_s_barrier();
       if (kt + RAHEAD < n32) stage(kt + RAHEAD);
     }
-    if (dqkv8 != nullptr && lane == 0) part8[blockIdx.x * RW + wave] = 0.f;   // its (empty) amax partial
+    if (Q8 && lane == 0) part8[blockIdx.x * RW + wave] = 0.f;   // its (empty) amax partial
     return;
   }
   LdsOffsets lo_;
@@ -760,9 +796,9 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
     }
   }
   const size_t orow_q = ((size_t)b * L + qi) * ld + h * D;
-  if (dqkv8 != nullptr) {   // --precision fp8: dQ also as e5m2 for the QKV dgrad (delayed scaling)
+  if constexpr (Q8) {   // --precision fp8: dQ also as e5m2 for the QKV dgrad (delayed scaling)
     const float inv8 = 1.f / hq_fp8_delayed_scale(q8, phase, kHqBf8Max);
-    float amax = qok ? store_row64_q8<true>(dqkv + orow_q, dqkv8 + orow_q, dq, scale, inv8, hh) : 0.f;
+    float amax = qok ? store_row64_e5(dqkv + orow_q, dqkv8 + orow_q, dq, scale, inv8, hh) : 0.f;
     amax = hq_wave_max(amax);
     if (lane == 0) part8[blockIdx.x * RW + wave] = amax;
     return;
@@ -772,7 +808,7 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
 
 // dK/dV: keys on the lanes.  Per 32-query tile: S = Q'·Kᵀ (+ aug: −LSE, bias), dP = dO·Vᵀ, then
 // dVᵀ += dOᵀ·(P∘mask) and dKᵀ += Q'ᵀ·dS with P/dS fed from the accumulators (no LDS round trip).
-template <bool DROP, int NT>
+template <bool DROP, int NT, bool Q8 = false>
 __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
     const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dctx, const float* __restrict__ lse,
     const float* __restrict__ delta, const float* __restrict__ key_bias, const uint16_t* __restrict__ mbits,
@@ -950,12 +986,12 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
     }
   }
   const size_t orow_k = ((size_t)b * L + kj) * ld + h * D;
-  if (dqkv8 != nullptr) {   // dK, dV also as e5m2; partial slots after the dQ kernel's
+  if constexpr (Q8) {   // dK, dV also as e5m2; partial slots after the dQ kernel's
     const float inv8 = 1.f / hq_fp8_delayed_scale(q8, phase, kHqBf8Max);
     float amax = 0.f;
     if (active && kok) {
-      amax = store_row64_q8<true>(dqkv + orow_k + 2 * H, dqkv8 + orow_k + 2 * H, dv, 1.f, inv8, hh);
-      amax = fmaxf(amax, store_row64_q8<true>(dqkv + orow_k + H, dqkv8 + orow_k + H, dk, LN2, inv8, hh));
+      amax = store_row64_e5(dqkv + orow_k + 2 * H, dqkv8 + orow_k + 2 * H, dv, 1.f, inv8, hh);
+      amax = fmaxf(amax, store_row64_e5(dqkv + orow_k + H, dqkv8 + orow_k + H, dk, LN2, inv8, hh));
     }
     amax = hq_wave_max(amax);
     if (lane == 0) part8[(gridDim.x + blockIdx.x) * RW + wave] = amax;
@@ -1074,8 +1110,13 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
         hipLaunchKernelGGL(kkv, dim3(B * nh * nb), dim3(RW * 64), lds_kv, s, qkv, dctx, lse, delta, key_bias, bits, dqkv,
                            L, nh, nb, scale * LOG2E, scale, ks, dqkv8, q8, part8, phase);
       };
-      if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH>, attn_bwd_dkdv_ring_kernel<true, NT>);
-      else launch(attn_bwd_dq_ring_kernel<false, NT, AH>, attn_bwd_dkdv_ring_kernel<false, NT>);
+      if (dqkv8) {   // --precision fp8: the e5m2-writing variants
+        if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH, true>, attn_bwd_dkdv_ring_kernel<true, NT, true>);
+        else launch(attn_bwd_dq_ring_kernel<false, NT, AH, true>, attn_bwd_dkdv_ring_kernel<false, NT, true>);
+      } else {
+        if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH>, attn_bwd_dkdv_ring_kernel<true, NT>);
+        else launch(attn_bwd_dq_ring_kernel<false, NT, AH>, attn_bwd_dkdv_ring_kernel<false, NT>);
+      }
     };
     if (L == 384) run(std::integral_constant<int, 12>{});
     else if (L == 512) run(std::integral_constant<int, 16>{});

@@ -376,8 +376,9 @@ def test_gemm_fp8_dgrad_resid(cuda):
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_attn_bwd_e5m2_output(cuda, p):
     """Attention backward with the e5m2 copy of dQKV for the fp8 QKV dgrad: dqkv equals the plain call
-    bitwise, dqkv8 = e5m2(bf16(dqkv) / s) under the delayed scale, and the amax of BOTH kernels' outputs
-    (dQ from one, dK/dV from the other) lands in the state."""
+    bitwise, dqkv8 = e5m2(dqkv / s) under the delayed scale (quantised from the fp32 values, so within one
+    code of e5m2(bf16(dqkv) / s)), and the amax of BOTH kernels' outputs (dQ from one, dK/dV from the other)
+    lands in the state; an amax beyond the scale's headroom saturates instead of overflowing."""
     k = _native.kernels()
     B, L, nh = 2, 384, 12
     g = torch.Generator(device=cuda).manual_seed(41)
@@ -391,14 +392,23 @@ def test_attn_bwd_e5m2_output(cuda, p):
     dqkv, dqkv8 = k.attn_bwd_q8(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125, False, state, 0)
     assert torch.equal(dqkv, ref)
     assert dqkv8.dtype == torch.float8_e5m2 and state[3].item() == 1.0
-    assert torch.equal(dqkv8.view(torch.uint8), _q5(dqkv, 1.0).view(torch.uint8))
+
+    def close_codes(got, exp, frac):
+        diff = (got.view(torch.uint8).int() - exp.view(torch.uint8).int()).abs()
+        assert diff.max().item() <= 1 and (diff > 0).float().mean().item() < frac
+    close_codes(dqkv8, _q5(dqkv, 1.0), 0.05)   # bf16 vs fp32 source: differs only at bf16 rounding ties
     amax = state[:3].view(torch.int32)[0].view(torch.float32).item()
-    assert amax == dqkv.float().abs().max().item()
+    assert amax == pytest.approx(dqkv.float().abs().max().item(), rel=1e-2)
     _, d8b = k.attn_bwd_q8(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125, False, state, 1)
     s = state[3].item()
     assert s == pytest.approx(2 * amax / 57344, rel=1e-6)
-    diff = (d8b.view(torch.uint8).int() - _q5(dqkv, s).view(torch.uint8).int()).abs()
-    assert diff.max().item() <= 1 and (diff > 0).float().mean().item() < 1e-3
+    close_codes(d8b, _q5(dqkv, s), 0.05)
+    # a state whose previous amax is 1000x too small: every |x| / s far beyond 57344 → saturated, never inf
+    state[:3] = 0.0
+    state[2] = amax * 1e-3
+    _, d8c = k.attn_bwd_q8(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125, False, state, 0)
+    assert torch.isfinite(d8c.float()).all()
+    assert d8c.float().abs().max().item() == 57344.0
 
 
 @pytest.mark.gpu
