@@ -260,7 +260,7 @@ int64_t gemm_fp8_supported(int64_t M, int64_t N, int64_t K) { return hq_gemm_fp8
 
 Tensor gemm_fp8(Tensor A8, Tensor B8, int64_t epi, c10::optional<Tensor> bias, Tensor sa, Tensor sb,
                 c10::optional<Tensor> pre, c10::optional<Tensor> out8, c10::optional<Tensor> state, int64_t phase,
-                c10::optional<Tensor> part, c10::optional<Tensor> resid) {
+                c10::optional<Tensor> part, c10::optional<Tensor> resid, bool write_out) {
   TORCH_CHECK(A8.is_cuda() && A8.element_size() == 1 && A8.is_contiguous() && B8.is_cuda() && B8.element_size() == 1 &&
               B8.is_contiguous(), "gemm_fp8: A8 / B8 must be contiguous 1-byte (fp8) GPU tensors");
   TORCH_CHECK(A8.dim() == 2 && B8.dim() == 2 && A8.size(1) == B8.size(1), "gemm_fp8: A8[M,K], B8[N,K]");
@@ -280,7 +280,10 @@ Tensor gemm_fp8(Tensor A8, Tensor B8, int64_t epi, c10::optional<Tensor> bias, T
     TORCH_CHECK(bias->numel() == N, "gemm_fp8: bias[N]");
   }
   c10::DeviceGuard g(A8.device());
-  Tensor C = at::empty({M, N}, A8.options().dtype(BF16));
+  // write_out = false (GELUD / DMUL with out8): only the fp8 copy (and P / part) — returns an empty tensor
+  TORCH_CHECK(write_out || ((epi == HQ_EPI_GELUD || epi == HQ_EPI_DMUL) && out8.has_value() && out8->defined()),
+              "gemm_fp8: write_out=False needs a GELUD / DMUL epilogue with out8");
+  Tensor C = write_out ? at::empty({M, N}, A8.options().dtype(BF16)) : at::empty({0}, A8.options().dtype(BF16));
   uint16_t* P = nullptr;
   uint8_t* C8 = nullptr;
   float* q8 = nullptr;
@@ -314,7 +317,8 @@ Tensor gemm_fp8(Tensor A8, Tensor B8, int64_t epi, c10::optional<Tensor> bias, T
       q8 = ptr<float>(*state);
     }
   }
-  hq_gemm_fp8(reinterpret_cast<const uint8_t*>(A8.data_ptr()), reinterpret_cast<const uint8_t*>(B8.data_ptr()), ptr<uint16_t>(C),
+  hq_gemm_fp8(reinterpret_cast<const uint8_t*>(A8.data_ptr()), reinterpret_cast<const uint8_t*>(B8.data_ptr()),
+              write_out ? ptr<uint16_t>(C) : nullptr,
               optr<float>(bias), P, ptr<float>(sa), ptr<float>(sb), C8, q8, (int)(phase % 3), (int)M, (int)N, (int)K,
               (int)epi, cur_stream(), pp);
   return C;
@@ -721,7 +725,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("gemm_tn8", &gemm_tn8);
   m.def("gemm_fp8", &gemm_fp8, py::arg("A8"), py::arg("B8"), py::arg("epi"), py::arg("bias"), py::arg("sa"), py::arg("sb"),
         py::arg("pre") = py::none(), py::arg("out8") = py::none(), py::arg("state") = py::none(), py::arg("phase") = 0,
-        py::arg("part") = py::none(), py::arg("resid") = py::none());
+        py::arg("part") = py::none(), py::arg("resid") = py::none(), py::arg("write_out") = true);
   m.def("span_fwd", &span_fwd);
   m.def("span_bwd", &span_bwd);
   m.def("set_dropout_seed", [](c10::optional<Tensor> t) {

@@ -279,7 +279,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
         *reinterpret_cast<uint2*>(C8 + goff) = make_uint2(lo, hi);
       }
     }
-    *reinterpret_cast<uint4*>(C + goff) = piece;
+    // C == null (GELUD / DMUL under --precision fp8 once every consumer reads the fp8 copy): no bf16 output
+    if ((EPI != HQ_EPI_GELUD && EPI != HQ_EPI_DMUL) || C != nullptr) *reinterpret_cast<uint4*>(C + goff) = piece;
   };
   if constexpr (kAux) {   // fully unrolled: aux[] must stay in registers
 #pragma unroll

@@ -214,8 +214,12 @@ class _LayerFn(torch.autograd.Function):
             h1, z1, m1, r1 = ops.linear_bdr_ln_fwd(ctxv, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), x,
                                                    kinds[name], *ln1)
         act8 = None
+        # bf16 act is only read by a bf16 FFN2 weight gradient: skipped (604 MB of stores at b256) when the
+        # backward will run that weight gradient in fp8 from act8 (its gradient state calibrated by then)
+        need_act = not (fp8 and torch.is_grad_enabled() and m.fp8_backward_ok(x.shape[0])
+                        and s8["dffn2"].step >= 1)
         r8 = (ops.linear_gelu_fwd_fp8(h1, W8("intermediate.dense"), Bm("intermediate.dense.bias"), s8["ffn1"],
-                                      s8["ffn2"], x8=h1_8) if fp8 else None)
+                                      s8["ffn2"], x8=h1_8, need_act=need_act) if fp8 else None)
         if r8 is not None:
             pre, act, act8 = r8
             ctx.gelu_deriv = True
@@ -265,8 +269,10 @@ class _LayerFn(torch.autograd.Function):
             """q = (dy8, dy_state, x8, x_state): the fp8 form (no bias) once the gradient state is calibrated."""
             if not trainable:
                 return
-            use8 = q is not None and q[0] is not None and q[1].calibrated and ops.fp8_wgrad_ok(
-                dy.shape[0], dy.shape[1], xin.shape[1])
+            use8 = (q is not None and q[0] is not None and q[2] is not None and q[1].calibrated
+                    and ops.fp8_wgrad_ok(q[0].shape[0], q[0].shape[1], q[2].shape[1]))
+            # the forward / DMUL skip a bf16 operand only when this fp8 form is certain to run
+            assert use8 or (dy is not None and xin is not None), "bf16 weight-gradient operand was not kept"
 
             def run():
                 if use8:
@@ -277,7 +283,7 @@ class _LayerFn(torch.autograd.Function):
                 run()
                 return
             side.wait_stream(torch.cuda.current_stream())
-            for t in ((dy, xin) + ((q[0], q[2]) if use8 else ())):
+            for t in ((q[0], q[2]) if use8 else (dy, xin)):
                 t.record_stream(side)
             with torch.cuda.stream(side):
                 run()
@@ -288,12 +294,7 @@ class _LayerFn(torch.autograd.Function):
         # each gradient written in e5m2 by its PRODUCER under delayed scaling: da2 and da1 by the LayerNorm
         # backwards, dpre by the FFN2 dgrad's DMUL epilogue, dQKV by the attention backward.  A gradient state has no current-scaling seed,
         # so its consumer runs in bf16 until one production has recorded an amax (``calibrated``).
-        T = dh2.shape[0]
-        fp8 = (m.precision == "fp8" and dh2.is_cuda and m.fp8_dgrad and ctx.gelu_deriv
-               and ops.fp8_gemm_ok(T, cfg.intermediate_size, cfg.hidden_size)
-               and ops.fp8_gemm_ok(T, cfg.hidden_size, cfg.intermediate_size)
-               and ops.fp8_gemm_ok(T, cfg.hidden_size, cfg.hidden_size)
-               and ops.fp8_gemm_ok(T, cfg.hidden_size, 3 * cfg.hidden_size))
+        fp8 = m.precision == "fp8" and dh2.is_cuda and ctx.gelu_deriv and m.fp8_backward_ok(dh2.shape[0])
         s8 = m.fp8_states(idx) if fp8 else None
         W8T = lambda k: st.view_fp8_t(p + k)  # noqa: E731  (e4m3 Wᵀ + dequant scale)
         f8 = ctx.f8 if fp8 else None          # (ctx8, h1_8, act8): e4m3 forward inputs for the fp8 wgrads
@@ -309,8 +310,11 @@ class _LayerFn(torch.autograd.Function):
         wgrad(da2, act, G("output.dense.weight"), None, (da2_8, s8["dffn2"], f8[2], s8["ffn2"]) if f8 else None)
         dpre8 = None
         if fp8 and s8["dffn2"].calibrated:
+            # bf16 dpre only if a consumer still needs it: the FFN1 dgrad and weight gradient read dpre8 once
+            # its state is calibrated (after this production), the latter only with the e4m3 h1 kept
+            need_dpre = not (s8["dffn1"].step >= 1 and (f8 is not None or not trainable))
             dpre, dpre8 = ops.linear_dgrad_gelu_fp8(da2_8, s8["dffn2"], W8T("output.dense.weight"), pre,
-                                                    G("intermediate.dense.bias"), acc, s8["dffn1"])
+                                                    G("intermediate.dense.bias"), acc, s8["dffn1"], need_dpre)
         else:
             dpre = ops.linear_dgrad_gelu_d(da2, W("output.dense.weight"), pre, ctx.gelu_deriv,
                                            G("intermediate.dense.bias"), acc, wt=WT("output.dense.weight"))
@@ -390,7 +394,7 @@ class BertForQuestionAnswering(nn.Module):
         super().__init__()
         self.config = config
         self.precision = precision
-        self.fp8_dgrad = True   # --precision fp8: run the FFN / out-projection dgrads in fp8 as well
+        self.fp8_dgrad = True   # --precision fp8: run the backward GEMMs (dgrads, most wgrads) in fp8 as well
         gen = torch.Generator().manual_seed(seed) if seed is not None else None
         self.store = ParamStore(build_entries(config))
         _init_store(self.store, config, gen)
@@ -472,6 +476,15 @@ class BertForQuestionAnswering(nn.Module):
         if torch.device(device).type != "cuda":
             return torch.float32
         return {"bf16": torch.bfloat16, "fp32": torch.float32, "fp8": torch.bfloat16}[self.precision]
+
+    def fp8_backward_ok(self, T: int) -> bool:
+        """The fp8 backward (e5m2 dgrads and weight gradients) runs for T tokens: enabled and every GEMM
+        shape tiles on gemm_fp8 / gemm_tn8 (BERT / RoBERTa base and large at T % 256 == 0)."""
+        c = self.config
+        H, F = c.hidden_size, c.intermediate_size
+        return (self.fp8_dgrad and ops.fp8_gemm_ok(T, F, H) and ops.fp8_gemm_ok(T, H, F) and ops.fp8_gemm_ok(T, H, H)
+                and ops.fp8_gemm_ok(T, H, 3 * H) and ops.fp8_wgrad_ok(T, H, F) and ops.fp8_wgrad_ok(T, F, H)
+                and ops.fp8_wgrad_ok(T, H, H))
 
     def fp8_states(self, idx: int):
         """Delayed-scaling states of layer ``idx``'s fp8 GEMM inputs (created on first use)."""

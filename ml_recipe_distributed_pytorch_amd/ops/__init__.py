@@ -232,11 +232,13 @@ def linear_fwd_fp8_own(x8, x_state: Fp8DelayedState, w8s, b32):
     return _k().gemm_fp8(x8, w8, _EPI_BIAS, b32, x_state.scale, sw.reshape(1).float())
 
 
-def linear_gelu_fwd_fp8(x, w8s, b32, in_state: Fp8DelayedState, out_state: Fp8DelayedState, x8=None):
+def linear_gelu_fwd_fp8(x, w8s, b32, in_state: Fp8DelayedState, out_state: Fp8DelayedState, x8=None,
+                        need_act: bool = True):
     """FFN1 in fp8 on the own block-scaled MFMA kernel (gemm_fp8.hip): returns (gelu'(pre), act, act8)
-    — act in bf16 (saved for the FFN2 weight gradient) and in e4m3 under ``out_state``'s delayed scale
-    for the FFN2 fp8 GEMM; None when the shape does not tile (caller falls back).  ``x8``: the input
-    already in e4m3 under ``in_state`` (LN forward's fp8 output), else it is quantised here."""
+    — act in bf16 (for a bf16 FFN2 weight gradient; ``need_act=False`` skips it and returns None when the
+    fp8 weight gradient will read act8) and in e4m3 under ``out_state``'s delayed scale for the FFN2 fp8
+    GEMM; None when the shape does not tile (caller falls back).  ``x8``: the input already in e4m3 under
+    ``in_state`` (LN forward's fp8 output), else it is quantised here."""
     M, K, N = x.shape[0], x.shape[1], w8s[0].shape[0]
     if not _k().gemm_fp8_supported(M, N, K):
         return None
@@ -246,8 +248,8 @@ def linear_gelu_fwd_fp8(x, w8s, b32, in_state: Fp8DelayedState, out_state: Fp8De
     gd = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
     act8 = torch.empty(M, N, dtype=torch.float8_e4m3fn, device=x.device)
     act = _k().gemm_fp8(x8, w8, _EPI_GELUD, b32, in_state.scale, sw.reshape(1).float(), pre=gd, out8=act8,
-                        state=out_state.buf, phase=out_state.next_phase())
-    return gd, act, act8
+                        state=out_state.buf, phase=out_state.next_phase(), write_out=bool(need_act))
+    return gd, (act if need_act else None), act8
 
 
 def linear_dgrad_fp8(dy8, dy_state: Fp8DelayedState, wt8s):
@@ -265,19 +267,20 @@ def linear_dgrad_add_fp8(dy8, dy_state: Fp8DelayedState, wt8s, resid):
     return _k().gemm_fp8(dy8, wt8, _EPI_RESID, None, dy_state.scale, sw.reshape(1).float(), resid=resid)
 
 
-def linear_dgrad_gelu_fp8(dy8, dy_state: Fp8DelayedState, wt8s, gd, g_bias, accumulate, out_state: Fp8DelayedState):
+def linear_dgrad_gelu_fp8(dy8, dy_state: Fp8DelayedState, wt8s, gd, g_bias, accumulate, out_state: Fp8DelayedState,
+                          need_bf16: bool = True):
     """FFN2 dgrad in fp8: dpre = (dy·W) ⊙ gelu'(pre) (``gd``: the gelu' stored by the forward), the FFN1 bias
     gradient from the epilogue's column sums, and dpre also in e5m2 under ``out_state`` for the FFN1 dgrad:
-    (dpre, dpre8)."""
+    (dpre, dpre8); ``need_bf16=False`` (every consumer reads dpre8) skips the bf16 dpre (returned as None)."""
     wt8, sw = wt8s
     M, N = dy8.shape[0], wt8.shape[0]
     part = torch.empty(M // 256, N, dtype=torch.float32, device=dy8.device)
     dpre8 = torch.empty(M, N, dtype=torch.float8_e5m2, device=dy8.device)
     dpre = _k().gemm_fp8(dy8, wt8, _EPI_DMUL, None, dy_state.scale, sw.reshape(1).float(), pre=gd, out8=dpre8,
-                         state=out_state.buf, phase=out_state.next_phase(), part=part)
+                         state=out_state.buf, phase=out_state.next_phase(), part=part, write_out=bool(need_bf16))
     if g_bias is not None:
         _k().colsum_into(part, g_bias, bool(accumulate))
-    return dpre, dpre8
+    return (dpre if need_bf16 else None), dpre8
 
 
 def fp8_wgrad_ok(T: int, N: int, K: int) -> bool:
