@@ -124,7 +124,8 @@ std::vector<Tensor> ln_fwd(Tensor a, c10::optional<Tensor> resid_opt, Tensor gam
 // q8 (f32[4] delayed-scaling state of the fp8 dgrad GEMM that consumes da): also returns da as e5m2
 std::vector<Tensor> ln_bwd(Tensor dy, c10::optional<Tensor> dy2, Tensor z, Tensor gamma, Tensor mean, Tensor rstd, double p,
                            int64_t seed, int64_t opid, c10::optional<Tensor> g_gamma, c10::optional<Tensor> g_beta,
-                           c10::optional<Tensor> g_bias, bool accumulate, c10::optional<Tensor> q8, int64_t phase) {
+                           c10::optional<Tensor> g_bias, bool accumulate, c10::optional<Tensor> q8, int64_t phase,
+                           bool write_da) {
   check(dy, BF16, "dy"); check_opt(dy2, BF16, "dy2"); check(z, BF16, "z"); check(gamma, F32, "gamma");
   check(mean, F32, "mean"); check(rstd, F32, "rstd");
   check_opt(g_gamma, F32, "g_gamma"); check_opt(g_beta, F32, "g_beta"); check_opt(g_bias, F32, "g_bias");
@@ -133,7 +134,9 @@ std::vector<Tensor> ln_bwd(Tensor dy, c10::optional<Tensor> dy2, Tensor z, Tenso
   const int64_t T = dy.size(0), H = dy.size(1);
   TORCH_CHECK(gamma.numel() == H && mean.numel() == T && rstd.numel() == T, "stat shapes");
   c10::DeviceGuard g(dy.device());
-  auto dz = at::empty_like(dy), da = at::empty_like(dy);
+  // write_da = false (with q8): da only as e5m2 — the bf16 da comes back empty
+  TORCH_CHECK(write_da || (q8.has_value() && q8->defined()), "ln_bwd: write_da=False needs q8");
+  auto dz = at::empty_like(dy), da = write_da ? at::empty_like(dy) : at::empty({0}, dy.options());
   const int nb = hq_ln_bwd_partials((int)T);
   auto part = at::empty({nb, 3 * H}, gamma.options());
   const bool want8 = q8.has_value() && q8->defined();
@@ -145,7 +148,7 @@ std::vector<Tensor> ln_bwd(Tensor dy, c10::optional<Tensor> dy2, Tensor z, Tenso
     da8 = at::empty(dy.sizes(), dy.options().dtype(at::kFloat8_e5m2));
   }
   hq_ln_bwd(ptr<uint16_t>(dy), optr<uint16_t>(dy2), ptr<uint16_t>(z), ptr<float>(gamma), ptr<float>(mean), ptr<float>(rstd),
-            ptr<uint16_t>(dz), ptr<uint16_t>(da), ptr<float>(part),
+            ptr<uint16_t>(dz), write_da ? ptr<uint16_t>(da) : nullptr, ptr<float>(part),
             outs4(optr<float>(g_gamma), optr<float>(g_beta), optr<float>(g_bias)), (int)T, (int)H, (float)p, u32(seed),
             u32(opid), accumulate, cur_stream(), want8 ? reinterpret_cast<uint8_t*>(da8.data_ptr()) : nullptr,
             want8 ? ptr<float>(*q8) : nullptr, (int)(phase % 3));
@@ -694,7 +697,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
         py::arg("seed"), py::arg("opid"), py::arg("q8") = py::none(), py::arg("phase") = 0);
   m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("dy2"), py::arg("z"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
         py::arg("p"), py::arg("seed"), py::arg("opid"), py::arg("g_gamma"), py::arg("g_beta"), py::arg("g_bias"),
-        py::arg("accumulate"), py::arg("q8") = py::none(), py::arg("phase") = 0);
+        py::arg("accumulate"), py::arg("q8") = py::none(), py::arg("phase") = 0, py::arg("write_da") = true);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("epi"), py::arg("bias") = py::none(),
         py::arg("pre") = py::none(), py::arg("resid") = py::none(), py::arg("part") = py::none(),

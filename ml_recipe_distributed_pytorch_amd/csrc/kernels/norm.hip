@@ -305,7 +305,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
 #pragma unroll
           for (int i = 0; i < 4; ++i) { da[i] = dz[i] * m[i]; acc[2][c][i] += da[i]; }
           const uint2 da_bf = hq_pack4(da);
-          *reinterpret_cast<uint2*>(da_out + base + col) = da_bf;
+          // da_out == null (Q8 only, --precision fp8 once every consumer reads da8): no bf16 da
+          if (!Q8 || da_out != nullptr) *reinterpret_cast<uint2*>(da_out + base + col) = da_bf;
           if constexpr (Q8) {   // from the bf16-rounded da, exactly what the bf16 copy holds
             float r[4];
             hq_unpack4(da_bf, r);

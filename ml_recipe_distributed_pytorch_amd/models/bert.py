@@ -303,8 +303,9 @@ class _LayerFn(torch.autograd.Function):
         # --- FFN block ------------------------------------------------------------------------
         ln2b = (dh2, None, z2, Wm("output.LayerNorm.weight"), m2, r2, ctx.ph, info.seed, op0 + 2,
                 G("output.LayerNorm.weight"), G("output.LayerNorm.bias"), G("output.dense.bias"), acc)
-        if fp8:
-            dz2, da2, da2_8 = ops.ln_bwd_q8(*ln2b, s8["dffn2"])
+        if fp8:   # bf16 da2 only while its fp8 consumers (FFN2 dgrad + weight gradient) still fall back
+            need = not (s8["dffn2"].step >= 1 and (f8 is not None or not trainable))
+            dz2, da2, da2_8 = ops.ln_bwd_q8(*ln2b, s8["dffn2"], need)
         else:
             dz2, da2 = ops.ln_bwd(*ln2b)
         wgrad(da2, act, G("output.dense.weight"), None, (da2_8, s8["dffn2"], f8[2], s8["ffn2"]) if f8 else None)
@@ -327,8 +328,9 @@ class _LayerFn(torch.autograd.Function):
         ln1b = (dz2, dh1_ffn, z1, Wm("attention.output.LayerNorm.weight"), m1, r1, ctx.ph, info.seed, op0 + 1,
                 G("attention.output.LayerNorm.weight"), G("attention.output.LayerNorm.bias"),
                 G("attention.output.dense.bias"), acc)
-        if fp8:
-            dz1, da1, da1_8 = ops.ln_bwd_q8(*ln1b, s8["dout"])
+        if fp8:   # likewise for the out-projection dgrad + weight gradient
+            need = not (s8["dout"].step >= 1 and (f8 is not None or not trainable))
+            dz1, da1, da1_8 = ops.ln_bwd_q8(*ln1b, s8["dout"], need)
         else:
             dz1, da1 = ops.ln_bwd(*ln1b)
         wgrad(da1, ctxv, G("attention.output.dense.weight"), None,

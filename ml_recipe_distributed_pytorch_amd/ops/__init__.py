@@ -64,11 +64,13 @@ def ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias
 
 
 def ln_bwd_q8(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate,
-              state: "Fp8DelayedState"):
+              state: "Fp8DelayedState", need_da: bool = True):
     """``ln_bwd`` that also writes da in e5m2 under ``state`` — the delayed-scaling state of the fp8 dgrad
-    GEMM that consumes da: (dz, da, da8)."""
-    return tuple(_k().ln_bwd(dy, dy2, z, gamma, mean, rstd, float(p), int(seed), int(opid), g_gamma, g_beta, g_bias,
-                             bool(accumulate), q8=state.buf, phase=state.next_phase()))
+    GEMM that consumes da: (dz, da, da8); ``need_da=False`` (every consumer reads da8) skips the bf16 da
+    (returned as None)."""
+    dz, da, da8 = _k().ln_bwd(dy, dy2, z, gamma, mean, rstd, float(p), int(seed), int(opid), g_gamma, g_beta, g_bias,
+                              bool(accumulate), q8=state.buf, phase=state.next_phase(), write_da=bool(need_da))
+    return dz, (da if need_da else None), da8
 
 
 # ------------------------------------------------------------------------------------------ GELU
