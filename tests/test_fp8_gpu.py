@@ -295,7 +295,7 @@ def test_ln_bwd_e5m2_output(cuda, T, H):
     out = k.ln_bwd(dy, None, z, gamma, mean, rstd, 0.1, 7, 3, *grads8, False, q8=state, phase=0)
     assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1])
     for a, b in zip(grads, grads8):   # the variants may contract a·m + acc differently: last-bit differences
-        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-9)
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5 * a.abs().max().item())
     da, da8 = out[1].float(), out[2]
     assert da8.dtype == torch.float8_e5m2 and state[3].item() == 1.0
 
