@@ -724,6 +724,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("fp8_quant_delayed_multi", &fp8_quant_delayed_multi);
   m.def("fp8_quant_multi_blocks", &fp8_quant_multi_blocks);
   m.def("gemm_fp8_supported", &gemm_fp8_supported);
+  m.def("gemm_fp8_set_variant", [](int64_t v) { hq_gemm_fp8_set_variant((int)v); });
   m.def("gemm_tn8_splits", &gemm_tn8_splits);
   m.def("gemm_tn8", &gemm_tn8);
   m.def("gemm_fp8", &gemm_fp8, py::arg("A8"), py::arg("B8"), py::arg("epi"), py::arg("bias"), py::arg("sa"), py::arg("sb"),

@@ -71,7 +71,54 @@ __device__ __forceinline__ float delayed_scale(const float* st, int phase) {
 
 constexpr bool grad_epi(int epi) { return epi == HQ_EPI_NONE || epi == HQ_EPI_DMUL || epi == HQ_EPI_RESID; }
 
-template <int EPI, bool Q8>
+// One 8-column bf16 piece of the dequantised (+bias) tile through the epilogue `EPI` and out to global
+// memory at element offset goff: RESID adds the residual, DMUL multiplies by gelu' (column sums into csum)
+// and with Q8 writes the e5m2 copy, GELUD writes gelu' to P and act (Q8: also e4m3).  `aux` is the piece of
+// P (DMUL: gelu', RESID: residual) loaded ahead.  WC = false skips the bf16 output (GELUD / DMUL with Q8, once
+// every consumer reads the fp8 copy) — a template flag: a runtime test around the 16 unrolled stores made hipcc
+// spill the DMUL epilogue.
+template <int EPI, bool Q8, bool WC>
+__device__ __forceinline__ void epi_piece(uint4 piece, const uint4& aux, size_t goff, uint16_t* __restrict__ C,
+                                          uint16_t* __restrict__ P, uint8_t* __restrict__ C8, float inv8, float& amax,
+                                          float (&csum)[8]) {
+  if constexpr (EPI == HQ_EPI_RESID) {
+    float d[8], rr[8];
+    hq_unpack8(piece, d);
+    hq_unpack8(aux, rr);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) d[e] += rr[e];
+    piece = hq_pack8(d);
+  } else if constexpr (EPI == HQ_EPI_DMUL) {
+    float d[8], gd[8];
+    hq_unpack8(piece, d);
+    hq_unpack8(aux, gd);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { d[e] *= gd[e]; csum[e] += d[e]; }
+    piece = hq_pack8(d);
+    if constexpr (Q8) {   // e5m2 dpre for the FFN1 dgrad, from the bf16-rounded values the bf16 copy holds
+      hq_unpack8(piece, d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(d[e]));
+      *reinterpret_cast<uint2*>(C8 + goff) = make_uint2(hq_pack_bf8x4(d, inv8), hq_pack_bf8x4(d + 4, inv8));
+    }
+  } else if constexpr (EPI == HQ_EPI_GELUD) {
+    float x[8], g[8];
+    hq_unpack8(piece, x);
+    hq_gelu_grad8(x, g);   // g = gelu'(x), x = gelu(x)
+    *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
+    piece = hq_pack8(x);
+    if constexpr (Q8) {
+      float f[8];
+      hq_unpack8(piece, f);   // quantise the bf16-rounded act, exactly what the bf16 copy holds
+#pragma unroll
+      for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(f[e]));
+      *reinterpret_cast<uint2*>(C8 + goff) = make_uint2(hq_pack_fp8x4(f, inv8), hq_pack_fp8x4(f + 4, inv8));
+    }
+  }
+  if constexpr (WC) *reinterpret_cast<uint4*>(C + goff) = piece;
+}
+
+template <int EPI, bool Q8, bool WC>
 __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                                uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                                uint16_t* __restrict__ P, const float* __restrict__ sa,
@@ -236,51 +283,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
   }
   auto piece_out = [&](int it) {
     const int lr = it * ROWS_PER_IT + rsub;
-    uint4 piece = *reinterpret_cast<const uint4*>(wreg + lr * RS + seg * 16);
-    const size_t goff = (size_t)grow_of(it) * ldc + gcol;
-    if constexpr (EPI == HQ_EPI_RESID) {
-      float d[8], rr[8];
-      hq_unpack8(piece, d);
-      hq_unpack8(aux[it], rr);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) d[e] += rr[e];
-      piece = hq_pack8(d);
-    } else if constexpr (EPI == HQ_EPI_DMUL) {
-      float d[8], gd[8];
-      hq_unpack8(piece, d);
-      hq_unpack8(aux[it], gd);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) { d[e] *= gd[e]; csum[e] += d[e]; }
-      piece = hq_pack8(d);
-      if constexpr (Q8) {   // e5m2 dpre for the FFN1 dgrad, from the bf16-rounded values the bf16 copy holds
-        hq_unpack8(piece, d);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(d[e]));
-        *reinterpret_cast<uint2*>(C8 + goff) = make_uint2(hq_pack_bf8x4(d, inv8), hq_pack_bf8x4(d + 4, inv8));
-      }
-    } else if constexpr (EPI == HQ_EPI_GELUD) {
-      float x[8], g[8];
-      hq_unpack8(piece, x);
-      hq_gelu_grad8(x, g);   // g = gelu'(x), x = gelu(x)
-      *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
-      piece = hq_pack8(x);
-      if constexpr (Q8) {
-        float f[8];
-        hq_unpack8(piece, f);   // quantise the bf16-rounded act, exactly what the bf16 copy holds
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          amax = fmaxf(amax, fabsf(f[e]));
-          f[e] = fminf(fmaxf(f[e] * inv8, -kFp8Max), kFp8Max);
-        }
-        uint32_t lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
-        lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
-        uint32_t hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
-        hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
-        *reinterpret_cast<uint2*>(C8 + goff) = make_uint2(lo, hi);
-      }
-    }
-    // C == null (GELUD / DMUL under --precision fp8 once every consumer reads the fp8 copy): no bf16 output
-    if ((EPI != HQ_EPI_GELUD && EPI != HQ_EPI_DMUL) || C != nullptr) *reinterpret_cast<uint4*>(C + goff) = piece;
+    const uint4 piece = *reinterpret_cast<const uint4*>(wreg + lr * RS + seg * 16);
+    epi_piece<EPI, Q8, WC>(piece, aux[kAux ? it : 0], (size_t)grow_of(it) * ldc + gcol, C, P, C8, inv8, amax, csum);
   };
   if constexpr (kAux) {   // fully unrolled: aux[] must stay in registers
 #pragma unroll
@@ -308,24 +312,302 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
   }
 }
 
+// ------------------------------------------------------------------ persistent form (gemm.hip v3)
+// At K = 768 a 256² fp8 tile is only 6 K-tiles, so v2's per-tile fixed cost (workgroup launch, the
+// prologue's first HBM round trip, the epilogue's drain) is about half of it.  This form keeps ONE workgroup
+// per CU walking tiles (tile = id, id + grid, …) and runs the LDS-DMA pipeline across the tile seam exactly
+// as gemm.hip's gemm_nt3_kernel (same LDS plan, phase table and counted waits — the fp8 K-tile has the bf16
+// one's byte geometry): the next tile's K-tile 0 is staged during this tile's last two K-tiles, its K-tile-1
+// first halves after the epilogue, which borrows the last K-tile's buffer (two 64-row rounds per wave).
+// The epilogue's vm ops per lane (E) are counted into the next tile's first waits.  Amax partials: one per
+// wave, accumulated over the wave's tiles and written at the end.
+template <int EPI, bool Q8, bool WC>
+struct P8Epi {   // vm ops per lane per tile: C (WC), P (GELUD), C8 (Q8) stores, aux loads (DMUL / RESID)
+  static constexpr bool kAux = EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID;
+  static constexpr int kStores = (WC ? 16 : 0) + (EPI == HQ_EPI_GELUD ? 16 : 0) + (Q8 ? 16 : 0);
+  static constexpr int E = kStores + (kAux ? 16 : 0);
+  static_assert(6 + E <= 63, "vmcnt field");
+};
+
+template <int EPI, bool Q8, bool WC>
+__global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
+                                                                uint16_t* __restrict__ C, const float* __restrict__ bias,
+                                                                uint16_t* __restrict__ P, const float* __restrict__ sa,
+                                                                const float* __restrict__ sb, uint8_t* __restrict__ C8,
+                                                                const float* __restrict__ q8, float* __restrict__ part8,
+                                                                float* __restrict__ part, int phase, int M, int N, int K) {
+  constexpr int FX = grad_epi(EPI) ? 1 : 0;
+  constexpr int PANEL = 256 * 128, STAGE = 2 * PANEL;
+  constexpr int WN = 64, RS = WN * 2 + 16;
+  constexpr int REGION = 64 * RS;            // one wave's 64-row staging round (9216 B)
+  constexpr int SPARE = 2 * STAGE;           // past both stage buffers: wave 7's region, then csum scratch
+  constexpr int E = P8Epi<EPI, Q8, WC>::E;
+  constexpr bool kAux = P8Epi<EPI, Q8, WC>::kAux;
+  static_assert(7 * REGION <= STAGE && SPARE + REGION + 2 * BN * 4 <= 160 * 1024, "LDS plan");
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int tiles_n = N / BN, ntiles = (M / BM) * tiles_n;
+  const int nt = K / BK;
+  const int lda = K, ldb = K, ldc = N;
+  HQ_DASSERT(K % BK == 0 && nt >= 2 && N % BN == 0 && M % BM == 0);
+
+  int voA[2], voB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = wave * 16 + i * 8 + (lane >> 3);
+    const int src_slot = (lane & 7) ^ ((row >> 1) & 7);
+    voA[i] = row * lda + src_slot * 16;
+    voB[i] = row * ldb + src_slot * 16;
+  }
+  auto rsrc_a = [&](int tile) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)(tile / tiles_n) * BM * lda), (short)0, BM * lda, 0x00020000);
+  };
+  auto rsrc_b = [&](int tile) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(B + (size_t)(tile % tiles_n) * BN * ldb), (short)0, BN * ldb, 0x00020000);
+  };
+  auto stA = [&](__amdgpu_buffer_rsrc_t rs, int half, int kt, int buf) {
+    char* dst = smem + buf * STAGE + (half * 128 + wave_u * 16) * 128;
+    const int so = half * 128 * lda + kt * BK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + i * 8 * 128), 16, voA[i], so, 0, 0);
+  };
+  auto stB = [&](__amdgpu_buffer_rsrc_t rs, int half, int kt, int buf) {
+    char* dst = smem + buf * STAGE + PANEL + (half * 128 + wave_u * 16) * 128;
+    const int so = half * 128 * ldb + kt * BK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + i * 8 * 128), 16, voB[i], so, 0, 0);
+  };
+
+  f32x4_t acc[8][4];
+  const int fr = lane & 15, fq = lane >> 4;
+  i32x8 af[4], bf0[2], bf1[2];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  auto readA = [&](int buf, int mh) {
+    const uint32_t pa = lds0 + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = frag32(pa, mh * 128 + wm * 64 + i * 16 + fr, fq);
+  };
+  auto readB = [&](int buf, int nh, i32x8 (&bf)[2]) {
+    const uint32_t pb = lds0 + buf * STAGE + PANEL;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bf[j] = frag32(pb, nh * 128 + wn * 32 + j * 16 + fr, fq);
+  };
+  auto mma = [&](int mh, int nh, const i32x8 (&bf)[2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[mh * 4 + i][nh * 2 + j] = mfma_fp8<FX>(bf[j], af[i], acc[mh * 4 + i][nh * 2 + j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto bar = []() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  const float dq = sa[0] * sb[0];
+  float inv8 = 1.f, amax = 0.f;
+  if constexpr (Q8) inv8 = 1.f / hq_fp8_delayed_scale(q8, phase, EPI == HQ_EPI_DMUL ? kHqBf8Max : kHqFp8Max);
+
+  int tile = id;
+  HQ_DASSERT(tile < ntiles);   // the host launches min(tiles, CUs) workgroups
+  int next = tile + nwg;
+  __amdgpu_buffer_rsrc_t ca = rsrc_a(tile), cb = rsrc_b(tile);
+  int p0 = 0;
+  stA(ca, 0, 0, 0); stB(cb, 0, 0, 0); stB(cb, 1, 0, 0); stA(ca, 1, 0, 0);
+  stA(ca, 0, 1, 1); stB(cb, 0, 1, 1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  bar();
+  bool first = true;
+
+  for (;;) {
+    const bool last = next >= ntiles;
+    const __amdgpu_buffer_rsrc_t na = rsrc_a(last ? tile : next), nb = rsrc_b(last ? tile : next);
+    const int tm = tile / tiles_n, tn = tile % tiles_n;
+    const int m0 = tm * BM, n0 = tn * BN;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    // phase / stage / wait table: gemm.hip gemm_nt3_kernel
+    auto ktile = [&](int t) {
+      const bool more1 = t + 1 < nt || !last;
+      const bool more2 = t + 2 < nt || (t + 2 == nt && !last);
+      const int b0 = (p0 + t) & 1, b1 = b0 ^ 1;
+      const bool x1 = t + 1 >= nt, x2 = t + 2 >= nt;
+      const __amdgpu_buffer_rsrc_t a1 = x1 ? na : ca, b1r = x1 ? nb : cb;
+      const __amdgpu_buffer_rsrc_t a2 = x2 ? na : ca, b2r = x2 ? nb : cb;
+      const int k1 = x1 ? t + 1 - nt : t + 1, k2 = x2 ? t + 2 - nt : t + 2;
+      if (t == 0 && !first) {
+        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E) : "memory");
+      } else if (more1) {
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      }
+      readB(b0, 0, bf0);
+      readA(b0, 0);
+      if (more1) stB(b1r, 1, k1, b1);
+      bar();
+      mma(0, 0, bf0);
+      bar();
+      if (t == 0 && !first) {
+        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E) : "memory");
+      } else if (more1) {
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      readB(b0, 1, bf1);
+      if (more1) stA(a1, 1, k1, b1);
+      bar();
+      mma(0, 1, bf1);
+      bar();
+      readA(b0, 1);
+      if (more2) stA(a2, 0, k2, b0);
+      bar();
+      mma(1, 1, bf1);
+      bar();
+      if (more1) {
+        if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      }
+      if (more2) stB(b2r, 0, k2, b0);
+      bar();
+      mma(1, 0, bf0);
+      bar();
+    };
+    if (__builtin_amdgcn_readfirstlane(wm) == 0) {
+      for (int t = 0; t < nt; ++t) ktile(t);
+      bar();
+    } else {
+      bar();
+      for (int t = 0; t < nt; ++t) ktile(t);
+    }
+    const int bl = (p0 + nt - 1) & 1;
+    char* wreg = wave < 7 ? smem + bl * STAGE + wave * REGION : smem + SPARE;
+
+    // ---- epilogue, 64 local rows per round (acc · sa·sb (+bias) -> bf16 staging -> epi_piece)
+    constexpr int SEGS = WN / 8, ROWS_PER_IT = 64 / SEGS;
+    constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELUD;
+    const int seg = lane % SEGS, rsub = lane / SEGS;
+    const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;
+    float csum[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+#pragma unroll
+    for (int rnd = 0; rnd < 2; ++rnd) {
+#pragma unroll
+      for (int J = 0; J < 4; ++J) {
+        const int nh = J >> 1, j = J & 1;
+        const int lc = nh * 32 + j * 16 + fq * 4;
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
+#pragma unroll
+        for (int I = 0; I < 4; ++I) {
+          const f32x4_t& a = acc[rnd * 4 + I][J];
+          float v[4] = {fmaf(a[0], dq, bv.x), fmaf(a[1], dq, bv.y), fmaf(a[2], dq, bv.z), fmaf(a[3], dq, bv.w)};
+          *reinterpret_cast<uint2*>(wreg + (I * 16 + fr) * RS + lc * 2) = hq_pack4(v);
+        }
+      }
+      auto goff_of = [&](int it) {   // it: 0..7 within this round
+        const int lr = it * ROWS_PER_IT + rsub;
+        return (size_t)(m0 + rnd * 128 + wm * 64 + lr) * ldc + gcol;
+      };
+      // aux pieces in batches of AB: all 8 at once (one exposed latency) spills the Q8 DMUL epilogue here
+      constexpr int AB = (EPI == HQ_EPI_DMUL && Q8) ? 4 : 8;
+#pragma unroll
+      for (int h = 0; h < 8; h += AB) {
+        uint4 aux[kAux ? AB : 1];
+        if constexpr (kAux) {
+#pragma unroll
+          for (int it = 0; it < AB; ++it) aux[it] = *reinterpret_cast<const uint4*>(P + goff_of(h + it));
+        }
+#pragma unroll
+        for (int it = 0; it < AB; ++it) {
+          const int lr = (h + it) * ROWS_PER_IT + rsub;
+          const uint4 piece = *reinterpret_cast<const uint4*>(wreg + lr * RS + seg * 16);
+          epi_piece<EPI, Q8, WC>(piece, aux[kAux ? it : 0], goff_of(h + it), C, P, C8, inv8, amax, csum);
+        }
+      }
+    }
+    if constexpr (EPI == HQ_EPI_DMUL) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        for (int o = SEGS; o < 64; o <<= 1) csum[e] += __shfl_xor(csum[e], o, 64);
+      float* red = reinterpret_cast<float*>(smem + SPARE + REGION);  // [2][BN], by tile column
+      if (rsub == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[wm * BN + (gcol - n0) + e] = csum[e];
+      }
+      bar();
+      for (int c = tid; c < BN; c += kThreads) part[(size_t)tm * N + n0 + c] = red[c] + red[BN + c];
+    }
+    if (last) break;
+    // every wave has read its staging rounds out of buffer bl: stage the next tile's K-tile-1 halves there
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    stA(na, 0, 1, bl); stB(nb, 0, 1, bl);
+    tile = next;
+    next = tile + nwg;
+    ca = na;
+    cb = nb;
+    p0 = (p0 + nt) & 1;
+    first = false;
+  }
+  if constexpr (Q8) {   // this wave's amax over all its tiles -> its partial slot
+    amax = hq_wave_max(amax);
+    if (lane == 0) part8[blockIdx.x * (kThreads / 64) + wave] = amax;
+  }
+}
+
 constexpr size_t lds_bytes() {
   const size_t stage = 2 * (size_t)(2 * 256 * 128);
   const size_t epi = 8 * 128 * (size_t)(64 * 2 + 16);
   return stage > epi ? stage : epi;
 }
 
-template <int EPI, bool Q8>
+// 0 = auto (persistent for K <= kPersistMaxK, v2 above), 2 = always v2, 3 = always persistent (A/B, tests)
+int g_fp8_variant = 0;
+constexpr int kPersistMaxK = 2304;
+
+template <int EPI, bool Q8, bool WC = true>
 void launch(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, uint16_t* P, const float* sa,
             const float* sb, uint8_t* C8, float* q8, float* part, int phase, int M, int N, int K, hipStream_t s) {
+  const bool persist = g_fp8_variant == 3 || (g_fp8_variant == 0 && K <= kPersistMaxK);
+  if (persist) {
+    constexpr size_t lds = 2 * (size_t)(2 * 256 * 128) + 64 * (64 * 2 + 16) + 2 * BN * 4;
+    static int ncu = [] {
+      int dev = 0, n = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      (void)hipFuncSetAttribute((const void*)gemm_fp8p_kernel<EPI, Q8, WC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      return n > 0 ? n : 256;
+    }();
+    const int tiles = (M / BM) * (N / BN);
+    const int nwg = std::min(tiles, ncu);   // every workgroup has at least one tile
+    float* part8 = Q8 ? hq_fp8_amax_parts((size_t)nwg * (kThreads / 64)) : nullptr;
+    hipLaunchKernelGGL((gemm_fp8p_kernel<EPI, Q8, WC>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, sa, sb, C8, q8,
+                       part8, part, phase, M, N, K);
+    if (Q8) hq_fp8_amax_fold(part8, nwg * (kThreads / 64), q8, phase, s, EPI == HQ_EPI_DMUL ? kHqBf8Max : kHqFp8Max);
+    return;
+  }
   constexpr size_t lds = lds_bytes();
   static bool init = [] {
-    (void)hipFuncSetAttribute((const void*)gemm_fp8_kernel<EPI, Q8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm_fp8_kernel<EPI, Q8, WC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     return true;
   }();
   (void)init;
   const int grid = (M / BM) * (N / BN);
   float* part8 = Q8 ? hq_fp8_amax_parts((size_t)grid * (kThreads / 64)) : nullptr;
-  hipLaunchKernelGGL((gemm_fp8_kernel<EPI, Q8>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, sa, sb,
+  hipLaunchKernelGGL((gemm_fp8_kernel<EPI, Q8, WC>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, sa, sb,
                      C8, q8, part8, part, phase, M, N, K, K, K, N);
   if (Q8) hq_fp8_amax_fold(part8, grid * (kThreads / 64), q8, phase, s, EPI == HQ_EPI_DMUL ? kHqBf8Max : kHqFp8Max);
 }
@@ -481,6 +763,8 @@ void hq_fp8_amax_fold(const float* part, int n, float* q8, int phase, hipStream_
   hipLaunchKernelGGL(amax_fold_kernel, dim3(1), dim3(1024), 0, s, part, nullptr, 1, 0LL, n, q8, phase, fmax);
 }
 
+void hq_gemm_fp8_set_variant(int v) { g_fp8_variant = v; }
+
 int hq_gemm_fp8_supported(int M, int N, int K) {
   return (M % BM == 0 && N % BN == 0 && K % BK == 0 && K >= 2 * BK && (size_t)BM * K < (1ull << 31) &&
           (size_t)BN * K < (1ull << 31)) ? 1 : 0;
@@ -491,11 +775,13 @@ void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* b
                  float* part) {
   switch (epi) {
     case HQ_EPI_GELUD:
-      if (C8) launch<HQ_EPI_GELUD, true>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
+      if (C8 && C) launch<HQ_EPI_GELUD, true>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
+      else if (C8) launch<HQ_EPI_GELUD, true, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
       else launch<HQ_EPI_GELUD, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
       break;
     case HQ_EPI_DMUL:
-      if (C8) launch<HQ_EPI_DMUL, true>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
+      if (C8 && C) launch<HQ_EPI_DMUL, true>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
+      else if (C8) launch<HQ_EPI_DMUL, true, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
       else launch<HQ_EPI_DMUL, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
       break;
     case HQ_EPI_NONE: launch<HQ_EPI_NONE, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s); break;

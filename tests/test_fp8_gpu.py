@@ -8,6 +8,15 @@ from ml_recipe_distributed_pytorch_amd import _native
 EPI_BIAS, EPI_GELUD = 1, 5
 
 
+@pytest.fixture(params=[2, 3], ids=["v2", "persistent"])
+def variant(request):
+    """Run an fp8 GEMM test on both kernel forms (per-tile v2 and persistent), restoring auto afterwards."""
+    k = _native.kernels()
+    k.gemm_fp8_set_variant(request.param)
+    yield request.param
+    k.gemm_fp8_set_variant(0)
+
+
 def _q(x):
     k = _native.kernels()
     x8, s = k.fp8_quantize(x)
@@ -16,7 +25,7 @@ def _q(x):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(256, 256, 256), (512, 768, 768), (768, 2304, 768), (256, 768, 3072)])
-def test_gemm_fp8_bias(cuda, M, N, K):
+def test_gemm_fp8_bias(cuda, variant, M, N, K):
     k = _native.kernels()
     g = torch.Generator(device=cuda).manual_seed(M + N + K)
     A = torch.randn(M, K, device=cuda, generator=g).bfloat16()
@@ -32,7 +41,7 @@ def test_gemm_fp8_bias(cuda, M, N, K):
 
 
 @pytest.mark.gpu
-def test_gemm_fp8_asymmetric_exact(cuda):
+def test_gemm_fp8_asymmetric_exact(cuda, variant):
     """Small-integer operands (exact in e4m3 and in the fp32 accumulator): catches any lane-map slip."""
     k = _native.kernels()
     M, N, K = 256, 512, 256
@@ -48,7 +57,7 @@ def test_gemm_fp8_asymmetric_exact(cuda):
 
 
 @pytest.mark.gpu
-def test_gemm_fp8_gelud_delayed_q8(cuda):
+def test_gemm_fp8_gelud_delayed_q8(cuda, variant):
     """FFN1 epilogue: act = gelu(pre), gelu'(pre), and act in e4m3 under delayed scaling (unit scale
     on the first step, 2·amax_prev/448 after; amax tracked in the 3-slot state)."""
     k = _native.kernels()
@@ -215,7 +224,7 @@ def _q5(x, s):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K", [(256, 768, 768), (512, 3072, 768), (512, 768, 3072)])
-def test_gemm_fp8_dgrad_e5m2(cuda, M, N, K):
+def test_gemm_fp8_dgrad_e5m2(cuda, variant, M, N, K):
     """dgrad form: A = e5m2 gradient (mixed-format MFMA, blgp = e5m2), B = e4m3 Wᵀ, no epilogue."""
     k = _native.kernels()
     g = torch.Generator(device=cuda).manual_seed(M * 3 + N + K)
@@ -230,7 +239,7 @@ def test_gemm_fp8_dgrad_e5m2(cuda, M, N, K):
 
 
 @pytest.mark.gpu
-def test_gemm_fp8_dgrad_exact(cuda):
+def test_gemm_fp8_dgrad_exact(cuda, variant):
     """Small integers (exact in e5m2, e4m3 and fp32): the e5m2 operand's lane map and format code."""
     k = _native.kernels()
     M, N, K = 256, 512, 256
@@ -245,7 +254,7 @@ def test_gemm_fp8_dgrad_exact(cuda):
 
 
 @pytest.mark.gpu
-def test_gemm_fp8_dmul_colsum_q8(cuda):
+def test_gemm_fp8_dmul_colsum_q8(cuda, variant):
     """FFN2 dgrad epilogue: dpre = bf16(dy·W) ⊙ gelu', per-256-row column sums (FFN1 bias gradient) and
     dpre in e5m2 under the gradient's delayed scale (2·amax_prev/57344), over three phases."""
     k = _native.kernels()
@@ -362,7 +371,7 @@ def test_fp8_dgrad_step_close_to_bf16_dgrad(cuda):
 
 
 @pytest.mark.gpu
-def test_gemm_fp8_dgrad_resid(cuda):
+def test_gemm_fp8_dgrad_resid(cuda, variant):
     """QKV dgrad form: C = bf16(dy8·Wᵀ8·sa·sb) + resid (EPI_RESID, e5m2 A operand)."""
     k = _native.kernels()
     M, N, K = 512, 768, 2304
@@ -446,3 +455,45 @@ def test_gemm_tn8_exact(cuda):
     out = torch.zeros(N, K, device=cuda)
     k.gemm_tn8(dy.to(torch.float8_e5m2), x.to(torch.float8_e4m3fn), one, one, out, False)
     assert torch.equal(out, dy.t() @ x)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("epi,q8", [(1, False), (5, True), (5, False), (6, True), (0, False), (4, False)])
+def test_gemm_fp8_persistent_matches_per_tile(cuda, epi, q8):
+    """The persistent form (one workgroup per CU walking 4.5 tiles each, DMA pipelined across tile seams) against
+    the per-tile v2 kernel at M = 24576, N = 3072, K = 768: bitwise equal outputs, gelu', fp8 copies, column
+    partials and delayed-scaling state (same K order, same epilogue math per tile)."""
+    k = _native.kernels()
+    M, N, K = 24576, 3072, 768
+    g = torch.Generator(device=cuda).manual_seed(epi * 10 + int(q8))
+    grad = epi in (0, 4, 6)
+    sa = torch.full((1,), 4e-2 / 57344 if grad else 1.0, device=cuda)
+    A8 = _q5(torch.randn(M, K, device=cuda, generator=g) * 1e-2, sa) if grad else \
+        torch.randn(M, K, device=cuda, generator=g).clamp(-8, 8).to(torch.float8_e4m3fn)
+    B8, sb = _q((torch.randn(N, K, device=cuda, generator=g) * 0.05).bfloat16())
+    bias = torch.randn(N, device=cuda, generator=g) * 0.1
+    aux = (torch.rand(M, N, device=cuda, generator=g) * 1.2 - 0.1).bfloat16()
+    outs = []
+    for v in (2, 3):
+        k.gemm_fp8_set_variant(v)
+        kw = {}
+        if epi in (5, 6):
+            kw["pre"] = aux.clone() if epi == 6 else torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+        if epi == 4:
+            kw["resid"] = aux
+        if epi == 6:
+            kw["part"] = torch.empty(M // 256, N, device=cuda)
+        if q8:
+            kw["out8"] = torch.empty(M, N, device=cuda, dtype=torch.float8_e5m2 if epi == 6 else torch.float8_e4m3fn)
+            kw["state"] = torch.tensor([0.0, 0.0, 3.0, 0.0], device=cuda)
+            kw["phase"] = 0
+        C = k.gemm_fp8(A8, B8, epi, None if grad else bias, sa, sb, **kw)
+        torch.cuda.synchronize()
+        outs.append((C, kw))
+    k.gemm_fp8_set_variant(0)
+    (c2, kw2), (c3, kw3) = outs
+    assert torch.equal(c2, c3)
+    for key in ("pre", "part", "out8", "state"):
+        if key in kw2:
+            assert torch.equal(kw2[key].view(torch.uint8) if kw2[key].element_size() == 1 else kw2[key],
+                               kw3[key].view(torch.uint8) if kw3[key].element_size() == 1 else kw3[key]), key
