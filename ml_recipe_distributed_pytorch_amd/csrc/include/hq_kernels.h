@@ -132,7 +132,7 @@ void hq_gemm_tn8(const uint8_t* A, const uint8_t* B, const float* sa, const floa
 // column sums into part[M/256][N])} with A8 e5m2.  C8 != null (GELUD / DMUL): the output also as e4m3 / e5m2 under
 // delayed scaling driven by the 4-float state q8 / phase.
 int hq_gemm_fp8_supported(int M, int N, int K);
-void hq_gemm_fp8_set_variant(int v);   // 0 auto (persistent for K <= 2304), 2 = per-tile v2, 3 = persistent
+void hq_gemm_fp8_set_variant(int v);   // 0 auto (persistent but the Q8 DMUL), 2 = per-tile v2, 3 = persistent
 void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, uint16_t* P, const float* sa,
                  const float* sb, uint8_t* C8, float* q8, int phase, int M, int N, int K, int epi, hipStream_t s,
                  float* part = nullptr);

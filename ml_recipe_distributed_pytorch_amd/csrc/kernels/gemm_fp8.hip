@@ -574,14 +574,16 @@ constexpr size_t lds_bytes() {
   return stage > epi ? stage : epi;
 }
 
-// 0 = auto (persistent for K <= kPersistMaxK, v2 above), 2 = always v2, 3 = always persistent (A/B, tests)
+// 0 = auto, 2 = always v2, 3 = always persistent (A/B, tests).  Auto = persistent, except the Q8 DMUL
+// epilogue, whose e5m2 copy pushes the persistent kernel past 256 VGPRs (spills: 486 vs 408 µs as v2);
+// persistent elsewhere measured 1.01-1.15x v2 on the b256 step shapes (tools/fp8_lab/fp8_variant_bench.py,
+// profiles/r3_fp8_bwd).
 int g_fp8_variant = 0;
-constexpr int kPersistMaxK = 2304;
 
 template <int EPI, bool Q8, bool WC = true>
 void launch(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, uint16_t* P, const float* sa,
             const float* sb, uint8_t* C8, float* q8, float* part, int phase, int M, int N, int K, hipStream_t s) {
-  const bool persist = g_fp8_variant == 3 || (g_fp8_variant == 0 && K <= kPersistMaxK);
+  const bool persist = g_fp8_variant == 3 || (g_fp8_variant == 0 && !(EPI == HQ_EPI_DMUL && Q8));
   if (persist) {
     constexpr size_t lds = 2 * (size_t)(2 * 256 * 128) + 64 * (64 * 2 + 16) + 2 * BN * 4;
     static int ncu = [] {
