@@ -484,10 +484,12 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor key_bias, int64_t B, int64_t L, 
   return {ctx, lse, mbits};
 }
 
-// q8 given (--precision fp8): also dQKV as e5m2 under that delayed-scaling state -> [dqkv, dqkv8]
+// q8 given (--precision fp8): also dQKV as e5m2 under that delayed-scaling state -> [dqkv, dqkv8]; with
+// write_bf16 = false: [empty, dqkv8, bpart] — no bf16 dQKV, the QKV bias-gradient column partials
+// bpart [B·ceil(L/32), 3H] instead (colsum_into reduces them)
 std::vector<Tensor> attn_bwd_impl(Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, Tensor mbits, int64_t B,
                                   int64_t L, int64_t nh, double p, double scale, bool deterministic,
-                                  c10::optional<Tensor> q8, int64_t phase) {
+                                  c10::optional<Tensor> q8, int64_t phase, bool write_bf16 = true) {
   check_attn(qkv, key_bias, B, L, nh);
   check(dctx, BF16, "dctx"); check(ctx, BF16, "ctx"); check(lse, F32, "lse");
   const int64_t H = qkv.size(1) / 3;
@@ -498,9 +500,11 @@ std::vector<Tensor> attn_bwd_impl(Tensor dctx, Tensor qkv, Tensor ctx, Tensor ls
     TORCH_CHECK(mbits.numel() * 2 == (int64_t)hq_attn_mask_bytes((int)B, (int)L, (int)nh), "dropout mask size");
   }
   c10::DeviceGuard g(qkv.device());
-  auto dqkv = at::empty_like(qkv);
-  auto delta = at::empty({B, nh, L}, lse.options());
   const bool want8 = q8.has_value() && q8->defined();
+  TORCH_CHECK(write_bf16 || want8, "attn_bwd: write_bf16=False needs q8");
+  auto dqkv = write_bf16 ? at::empty_like(qkv) : at::empty({0}, qkv.options());
+  auto delta = at::empty({B, nh, L}, lse.options());
+  Tensor bpart = write_bf16 ? Tensor() : at::empty({B * ((L + 31) / 32), qkv.size(1)}, lse.options());
   Tensor dqkv8;
   if (want8) {
     check(*q8, F32, "q8");
@@ -508,9 +512,11 @@ std::vector<Tensor> attn_bwd_impl(Tensor dctx, Tensor qkv, Tensor ctx, Tensor ls
     dqkv8 = at::empty(qkv.sizes(), qkv.options().dtype(at::kFloat8_e5m2));
   }
   hq_attn_bwd(ptr<uint16_t>(dctx), ptr<uint16_t>(qkv), ptr<uint16_t>(ctx), ptr<float>(lse), ptr<float>(key_bias),
-              p > 0 ? ptr<uint16_t>(mbits) : nullptr, ptr<uint16_t>(dqkv), ptr<float>(delta), (int)B, (int)L, (int)nh, 64,
-              (float)p, (float)scale, deterministic, cur_stream(), want8 ? reinterpret_cast<uint8_t*>(dqkv8.data_ptr()) : nullptr,
-              want8 ? ptr<float>(*q8) : nullptr, (int)(phase % 3));
+              p > 0 ? ptr<uint16_t>(mbits) : nullptr, write_bf16 ? ptr<uint16_t>(dqkv) : nullptr, ptr<float>(delta), (int)B,
+              (int)L, (int)nh, 64, (float)p, (float)scale, deterministic, cur_stream(),
+              want8 ? reinterpret_cast<uint8_t*>(dqkv8.data_ptr()) : nullptr, want8 ? ptr<float>(*q8) : nullptr,
+              (int)(phase % 3), write_bf16 ? nullptr : ptr<float>(bpart));
+  if (!write_bf16) return {dqkv, dqkv8, bpart};
   if (want8) return {dqkv, dqkv8};
   return {dqkv};
 }
@@ -750,9 +756,12 @@ PYBIND11_MODULE(_hq_kernels, m) {
         py::arg("phase") = 0);
   m.def("attn_bwd", &attn_bwd);
   m.def("attn_bwd_q8", [](Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, Tensor mbits, int64_t B,
-                          int64_t L, int64_t nh, double p, double scale, bool deterministic, Tensor q8, int64_t phase) {
-    return attn_bwd_impl(dctx, qkv, ctx, lse, key_bias, mbits, B, L, nh, p, scale, deterministic, q8, phase);
-  });
+                          int64_t L, int64_t nh, double p, double scale, bool deterministic, Tensor q8, int64_t phase,
+                          bool write_bf16) {
+    return attn_bwd_impl(dctx, qkv, ctx, lse, key_bias, mbits, B, L, nh, p, scale, deterministic, q8, phase, write_bf16);
+  }, py::arg("dctx"), py::arg("qkv"), py::arg("ctx"), py::arg("lse"), py::arg("key_bias"), py::arg("mbits"), py::arg("B"),
+     py::arg("L"), py::arg("nh"), py::arg("p"), py::arg("scale"), py::arg("deterministic"), py::arg("q8"), py::arg("phase"),
+     py::arg("write_bf16") = true);
   m.def("grad_norm", &grad_norm);
   m.def("sq_norm_partials", [](Tensor x, int64_t nparts) {
     check(x, F32, "x");

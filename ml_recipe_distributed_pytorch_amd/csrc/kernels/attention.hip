@@ -180,6 +180,7 @@ __device__ __forceinline__ uint32_t bf8x4_raw(float a, float b, float c, float d
   const uint32_t w = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
   return __builtin_amdgcn_cvt_pk_bf8_f32(c, d, w, true);
 }
+template <bool WB = true>   // WB = false: the e5m2 copy only (no bf16 output)
 __device__ __forceinline__ float store_row64_e5(uint16_t* out, uint8_t* out8, const f32x16_t (&a)[2], float mul,
                                                 float inv8, int hh) {
   float amax = 0.f;   // of the scaled values (|x·mul| = |x|·|mul|)
@@ -199,17 +200,52 @@ __device__ __forceinline__ float store_row64_e5(uint16_t* out, uint8_t* out8, co
     for (int g = 0; g < 4; g += 2) {
       const float va[4] = {a[d][4 * g] * mul, a[d][4 * g + 1] * mul, a[d][4 * g + 2] * mul, a[d][4 * g + 3] * mul};
       const float vb[4] = {a[d][4 * g + 4] * mul, a[d][4 * g + 5] * mul, a[d][4 * g + 6] * mul, a[d][4 * g + 7] * mul};
-      const uint2 A = hq_pack4(va), B = hq_pack4(vb);
-      const auto r0 = __builtin_amdgcn_permlane32_swap(A.x, B.x, false, false);
-      const auto r1 = __builtin_amdgcn_permlane32_swap(A.y, B.y, false, false);
       const int col = d * 32 + 8 * g + 8 * hh;
-      *reinterpret_cast<uint4*>(out + col) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+      if constexpr (WB) {
+        const uint2 A = hq_pack4(va), B = hq_pack4(vb);
+        const auto r0 = __builtin_amdgcn_permlane32_swap(A.x, B.x, false, false);
+        const auto r1 = __builtin_amdgcn_permlane32_swap(A.y, B.y, false, false);
+        *reinterpret_cast<uint4*>(out + col) = make_uint4(r0[0], r1[0], r0[1], r1[1]);
+      }
       const uint32_t A8 = bf8x4_raw(q(va[0]), q(va[1]), q(va[2]), q(va[3]));
       const uint32_t B8 = bf8x4_raw(q(vb[0]), q(vb[1]), q(vb[2]), q(vb[3]));
       const auto r8 = __builtin_amdgcn_permlane32_swap(A8, B8, false, false);
       *reinterpret_cast<uint2*>(out8 + col) = make_uint2(r8[0], r8[1]);
     }
   return amax;
+}
+
+// --precision fp8, calibrated: the QKV bias gradient Σ_t dQKV[t, :] as per-wave column partials (the
+// fp8 QKV weight gradient has no fused bias).  Column sums of one 32-column half `d` of a transposed 32x32
+// accumulator over the 32 lanes of each wave half (the wave's 32 tokens): a reduce-scatter butterfly over
+// lane masks 16, 8, 4, 2 then one plain exchange — 4·(8+4+2+1)+1 ops instead of 5·16.  Lanes l and l^1 end
+// with the sum of accumulator row r = (l >> 1) & 15 (value order: level m keeps the lower half of the list
+// when lane bit m is 0).  Invalid lanes (tokens past L) contribute 0.
+__device__ __forceinline__ float colsum16(const f32x16_t& a, float mul, bool valid, int lane) {
+  float v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = valid ? a[r] * mul : 0.f;
+#pragma unroll
+  for (int lvl = 0; lvl < 4; ++lvl) {
+    const int m = 16 >> lvl, k = 8 >> lvl;
+    const bool up = (lane & m) != 0;
+#pragma unroll
+    for (int i = 0; i < k; ++i) {
+      const float send = up ? v[i] : v[i + k];
+      const float keep = up ? v[i + k] : v[i];
+      v[i] = keep + __shfl_xor(send, m, 64);
+    }
+  }
+  return v[0] + __shfl_xor(v[0], 1, 64);
+}
+// both halves of a row-of-64 accumulator pair -> row `dst` (64 floats: column d·32 + acc_row(r, hh))
+__device__ __forceinline__ void colsum_row64(float* dst, const f32x16_t (&a)[2], float mul, bool valid, int lane,
+                                             int hh) {
+#pragma unroll
+  for (int d = 0; d < 2; ++d) {
+    const float sum = colsum16(a[d], mul, valid, lane);
+    if ((lane & 1) == 0) dst[d * 32 + acc_row((lane >> 1) & 15, hh)] = sum;
+  }
 }
 
 // Static issue priority of a workgroup's waves for the whole main loop (MI355X_MICROARCH "Two waves per
@@ -651,12 +687,16 @@ __device__ __forceinline__ void split3(float x, uint16_t& hi, uint16_t& mid, uin
   lo = bf16_rne(r - hq_bf2f(mid));
 }
 
-template <bool DROP, int NT, int RAHEAD, bool Q8 = false>
+// MODE 0: bf16 dQKV; 1: bf16 + e5m2 copy (fp8 backward, calibrating); 2: e5m2 only + column partials of the
+// QKV bias gradient into bpart [B·n32][3H] (fp8 backward, calibrated: every consumer reads the e5m2 copy)
+template <bool DROP, int NT, int RAHEAD, int MODE = 0>
 __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
     const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dctx, const uint16_t* __restrict__ ctx,
     const float* __restrict__ lse, const float* __restrict__ key_bias, const uint16_t* __restrict__ mbits,
     float* __restrict__ delta, uint16_t* __restrict__ dqkv, int L, int nh, int n_qb, float c_scale, float scale,
-    float kscale, uint8_t* __restrict__ dqkv8, const float* __restrict__ q8, float* __restrict__ part8, int phase) {
+    float kscale, uint8_t* __restrict__ dqkv8, const float* __restrict__ q8, float* __restrict__ part8, int phase,
+    float* __restrict__ bpart) {
+  constexpr bool Q8 = MODE > 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int RNS = RAHEAD + 2;
   const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
@@ -798,9 +838,10 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
   const size_t orow_q = ((size_t)b * L + qi) * ld + h * D;
   if constexpr (Q8) {   // --precision fp8: dQ also as e5m2 for the QKV dgrad (delayed scaling)
     const float inv8 = 1.f / hq_fp8_delayed_scale(q8, phase, kHqBf8Max);
-    float amax = qok ? store_row64_e5(dqkv + orow_q, dqkv8 + orow_q, dq, scale, inv8, hh) : 0.f;
+    float amax = qok ? store_row64_e5<MODE == 1>(dqkv + orow_q, dqkv8 + orow_q, dq, scale, inv8, hh) : 0.f;
     amax = hq_wave_max(amax);
     if (lane == 0) part8[blockIdx.x * RW + wave] = amax;
+    if constexpr (MODE == 2) colsum_row64(bpart + ((size_t)b * n32 + qs) * 3 * H + h * D, dq, scale, qok, lane, hh);
     return;
   }
   if (qok) store_row64(dqkv + orow_q, dq, scale, hh);
@@ -808,12 +849,14 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
 
 // dK/dV: keys on the lanes.  Per 32-query tile: S = Q'·Kᵀ (+ aug: −LSE, bias), dP = dO·Vᵀ, then
 // dVᵀ += dOᵀ·(P∘mask) and dKᵀ += Q'ᵀ·dS with P/dS fed from the accumulators (no LDS round trip).
-template <bool DROP, int NT, bool Q8 = false>
+template <bool DROP, int NT, int MODE = 0>   // MODE: as attn_bwd_dq_ring_kernel
 __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
     const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dctx, const float* __restrict__ lse,
     const float* __restrict__ delta, const float* __restrict__ key_bias, const uint16_t* __restrict__ mbits,
     uint16_t* __restrict__ dqkv, int L, int nh, int n_kb, float c_scale, float scale, float kscale,
-    uint8_t* __restrict__ dqkv8, const float* __restrict__ q8, float* __restrict__ part8, int phase) {
+    uint8_t* __restrict__ dqkv8, const float* __restrict__ q8, float* __restrict__ part8, int phase,
+    float* __restrict__ bpart) {
+  constexpr bool Q8 = MODE > 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // slot: Q' [32][64] 4 KB | dO [32][64] 4 KB | A' words [32] uint4 512 B | δ [32] f32 128 B | bits [RW][64] u16
   constexpr int SLOT = 2 * RTILE + 512 + 128 + RW * 128;
@@ -990,11 +1033,18 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
     const float inv8 = 1.f / hq_fp8_delayed_scale(q8, phase, kHqBf8Max);
     float amax = 0.f;
     if (active && kok) {
-      amax = store_row64_e5(dqkv + orow_k + 2 * H, dqkv8 + orow_k + 2 * H, dv, 1.f, inv8, hh);
-      amax = fmaxf(amax, store_row64_e5(dqkv + orow_k + H, dqkv8 + orow_k + H, dk, LN2, inv8, hh));
+      amax = store_row64_e5<MODE == 1>(dqkv + orow_k + 2 * H, dqkv8 + orow_k + 2 * H, dv, 1.f, inv8, hh);
+      amax = fmaxf(amax, store_row64_e5<MODE == 1>(dqkv + orow_k + H, dqkv8 + orow_k + H, dk, LN2, inv8, hh));
     }
     amax = hq_wave_max(amax);
     if (lane == 0) part8[(gridDim.x + blockIdx.x) * RW + wave] = amax;
+    if constexpr (MODE == 2) {
+      if (active) {   // every key subtile < n32 is active (L ≤ 32·n32): each partial row is written once
+        float* row = bpart + ((size_t)b * n32 + ks_idx) * 3 * H + h * D;
+        colsum_row64(row + 2 * H, dv, 1.f, kok, lane, hh);
+        colsum_row64(row + H, dk, LN2, kok, lane, hh);
+      }
+    }
     return;
   }
   if (active && kok) {
@@ -1083,7 +1133,7 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
 
 void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx, const float* lse, const float* key_bias,
                  const uint16_t* mbits, uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p,
-                 float scale, bool deterministic, hipStream_t s, uint8_t* dqkv8, float* q8, int phase) {
+                 float scale, bool deterministic, hipStream_t s, uint8_t* dqkv8, float* q8, int phase, float* bpart) {
   set_attn_prio();
   if (dh != D || L > 512) { fprintf(stderr, "hq_attn_bwd: head_dim %d / L %d unsupported\n", dh, L); abort(); }
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
@@ -1106,13 +1156,16 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
             (hipFuncSetAttribute((const void*)kdq, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024) == hipSuccess);
         (void)attr;
         hipLaunchKernelGGL(kdq, dim3(B * nh * nb), dim3(RW * 64), lds_dq, s, qkv, dctx, ctx, lse, key_bias, bits, delta,
-                           dqkv, L, nh, nb, scale * LOG2E, scale, ks, dqkv8, q8, part8, phase);
+                           dqkv, L, nh, nb, scale * LOG2E, scale, ks, dqkv8, q8, part8, phase, bpart);
         hipLaunchKernelGGL(kkv, dim3(B * nh * nb), dim3(RW * 64), lds_kv, s, qkv, dctx, lse, delta, key_bias, bits, dqkv,
-                           L, nh, nb, scale * LOG2E, scale, ks, dqkv8, q8, part8, phase);
+                           L, nh, nb, scale * LOG2E, scale, ks, dqkv8, q8, part8, phase, bpart);
       };
-      if (dqkv8) {   // --precision fp8: the e5m2-writing variants
-        if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH, true>, attn_bwd_dkdv_ring_kernel<true, NT, true>);
-        else launch(attn_bwd_dq_ring_kernel<false, NT, AH, true>, attn_bwd_dkdv_ring_kernel<false, NT, true>);
+      if (dqkv8 && bpart) {   // --precision fp8, calibrated: e5m2 + bias partials, no bf16
+        if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH, 2>, attn_bwd_dkdv_ring_kernel<true, NT, 2>);
+        else launch(attn_bwd_dq_ring_kernel<false, NT, AH, 2>, attn_bwd_dkdv_ring_kernel<false, NT, 2>);
+      } else if (dqkv8) {   // --precision fp8: the e5m2-writing variants
+        if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH, 1>, attn_bwd_dkdv_ring_kernel<true, NT, 1>);
+        else launch(attn_bwd_dq_ring_kernel<false, NT, AH, 1>, attn_bwd_dkdv_ring_kernel<false, NT, 1>);
       } else {
         if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH>, attn_bwd_dkdv_ring_kernel<true, NT>);
         else launch(attn_bwd_dq_ring_kernel<false, NT, AH>, attn_bwd_dkdv_ring_kernel<false, NT>);

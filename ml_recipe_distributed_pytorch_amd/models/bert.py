@@ -241,7 +241,7 @@ class _LayerFn(torch.autograd.Function):
         ctx.save_for_backward(x, key_bias, qkv, ctxv, lse, z1, m1, r1, h1, pre, act, z2, m2, r2)
         # e4m3 inputs of the out-projection / FFN1 / FFN2 GEMMs (their scales stay in the states until the next
         # forward re-quantises), for the fp8 weight gradients
-        ctx.f8 = (ctx8, h1_8, act8) if (fp8 and act8 is not None and h1_8 is not None) else None
+        ctx.f8 = (ctx8, h1_8, act8, x8) if (fp8 and act8 is not None and h1_8 is not None) else None
         ctx.bits = bits
         ctx.info, ctx.idx, ctx.ph, ctx.pa, ctx.scale = info, idx, ph, pa, scale
         return h2
@@ -297,7 +297,7 @@ class _LayerFn(torch.autograd.Function):
         fp8 = m.precision == "fp8" and dh2.is_cuda and ctx.gelu_deriv and m.fp8_backward_ok(dh2.shape[0])
         s8 = m.fp8_states(idx) if fp8 else None
         W8T = lambda k: st.view_fp8_t(p + k)  # noqa: E731  (e4m3 Wᵀ + dequant scale)
-        f8 = ctx.f8 if fp8 else None          # (ctx8, h1_8, act8): e4m3 forward inputs for the fp8 wgrads
+        f8 = ctx.f8 if fp8 else None          # (ctx8, h1_8, act8, x8): e4m3 forward inputs for the fp8 wgrads
         ctx.f8 = None
 
         # --- FFN block ------------------------------------------------------------------------
@@ -339,13 +339,20 @@ class _LayerFn(torch.autograd.Function):
             dctx = ops.linear_dgrad_fp8(da1_8, s8["dout"], W8T("attention.output.dense.weight"))
         else:
             dctx = ops.linear_dgrad(da1, W("attention.output.dense.weight"), wt=WT("attention.output.dense.weight"))
-        if fp8:
-            dqkv, dqkv8 = ops.attn_bwd_q8(dctx, qkv, ctxv, lse, key_bias, ctx.bits, B, L, nh, ctx.pa, ctx.scale,
-                                          s8["dqkv"])
+        bpart = None
+        if fp8:   # calibrated: e5m2 dQKV only (+ QKV bias-gradient partials), the fp8 QKV wgrad reads it with x8
+            need = not (s8["dqkv"].step >= 1 and (f8 is not None or not trainable))
+            dqkv, dqkv8, bpart = ops.attn_bwd_q8(dctx, qkv, ctxv, lse, key_bias, ctx.bits, B, L, nh, ctx.pa, ctx.scale,
+                                                 s8["dqkv"], need)
         else:
             dqkv = ops.attn_bwd(dctx, qkv, ctxv, lse, key_bias, ctx.bits, B, L, nh, ctx.pa, info.seed, op0, ctx.scale)
         ctx.bits = None
-        wgrad(dqkv, x, G("qkv.weight"), G("qkv.bias"))
+        if bpart is not None:
+            wgrad(None, None, G("qkv.weight"), None, (dqkv8, s8["dqkv"], f8[3], s8["qkv"]))
+            if trainable:
+                ops.colsum_into(bpart, G("qkv.bias"), acc)
+        else:
+            wgrad(dqkv, x, G("qkv.weight"), G("qkv.bias"))
         if trainable:
             m._group_ready(grp)
         if fp8 and s8["dqkv"].calibrated:
@@ -486,7 +493,7 @@ class BertForQuestionAnswering(nn.Module):
         H, F = c.hidden_size, c.intermediate_size
         return (self.fp8_dgrad and ops.fp8_gemm_ok(T, F, H) and ops.fp8_gemm_ok(T, H, F) and ops.fp8_gemm_ok(T, H, H)
                 and ops.fp8_gemm_ok(T, H, 3 * H) and ops.fp8_wgrad_ok(T, H, F) and ops.fp8_wgrad_ok(T, F, H)
-                and ops.fp8_wgrad_ok(T, H, H))
+                and ops.fp8_wgrad_ok(T, H, H) and ops.fp8_wgrad_ok(T, 3 * H, H))
 
     def fp8_states(self, idx: int):
         """Delayed-scaling states of layer ``idx``'s fp8 GEMM inputs (created on first use)."""

@@ -114,11 +114,15 @@ def attn_fwd_q8(qkv, key_bias, B, L, nh, p, seed, opid, scale, state: "Fp8Delaye
     return ctx, lse, bits, ctx8
 
 
-def attn_bwd_q8(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, scale, state: "Fp8DelayedState"):
+def attn_bwd_q8(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, scale, state: "Fp8DelayedState",
+                need_bf16: bool = True):
     """``attn_bwd`` that also writes dQKV in e5m2 under ``state`` — the delayed-scaling state of the fp8 QKV
-    dgrad that consumes it: (dqkv, dqkv8)."""
-    return tuple(_k().attn_bwd_q8(dctx, qkv, ctx, lse, key_bias, bits, int(B), int(L), int(nh), float(p), float(scale),
-                                  deterministic(), state.buf, state.next_phase()))
+    dgrad that consumes it: (dqkv, dqkv8, None).  ``need_bf16=False`` (the QKV dgrad and weight gradient
+    both read dqkv8): (None, dqkv8, bpart) — no bf16 dQKV; bpart holds column partials of the QKV bias
+    gradient (``colsum_into``)."""
+    r = _k().attn_bwd_q8(dctx, qkv, ctx, lse, key_bias, bits, int(B), int(L), int(nh), float(p), float(scale),
+                         deterministic(), state.buf, state.next_phase(), bool(need_bf16))
+    return (r[0], r[1], None) if need_bf16 else (None, r[1], r[2])
 
 
 def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale):
@@ -384,6 +388,11 @@ def linear_wgrad(dy, x, g_w, g_b, accumulate):
             _k().bias_grad(dy, g_b, bool(accumulate))
         return
     ref.linear_wgrad(dy, x, g_w, g_b, accumulate)
+
+
+def colsum_into(part, out, accumulate):
+    """out (+)= Σ_rows part (fp32 column partials, e.g. the QKV bias gradient of the fp8 backward)."""
+    _k().colsum_into(part, out, bool(accumulate))
 
 
 def bias_grad(dy, g_b, accumulate):

@@ -416,6 +416,15 @@ def test_attn_bwd_e5m2_output(cuda, p):
     s = state[3].item()
     assert s == pytest.approx(2 * amax / 57344, rel=1e-6)
     close_codes(d8b, _q5(dqkv, s), 0.05)
+    # calibrated mode: no bf16 dQKV, the same e5m2 bytes, and the QKV bias-gradient column partials
+    st2 = state.clone()
+    r2 = k.attn_bwd_q8(dctx, qkv, ctx, lse, kb, bits, B, L, nh, p, 0.125, False, st2, 1, write_bf16=False)
+    assert r2[0].numel() == 0 and torch.equal(r2[1].view(torch.uint8), d8b.view(torch.uint8))
+    bpart = r2[2]
+    assert bpart.shape == (B * ((L + 31) // 32), 3 * nh * 64)
+    colsum = bpart.sum(0)
+    ref_sum = dqkv.float().sum(0)
+    torch.testing.assert_close(colsum, ref_sum, rtol=2e-2, atol=2e-2 * ref_sum.abs().max().item())
     # a state whose previous amax is 1000x too small: every |x| / s far beyond 57344 → saturated, never inf
     state[:3] = 0.0
     state[2] = amax * 1e-3
