@@ -216,27 +216,46 @@ __device__ __forceinline__ float store_row64_e5(uint16_t* out, uint8_t* out8, co
 }
 
 // --precision fp8, calibrated: the QKV bias gradient Σ_t dQKV[t, :] as per-wave column partials (the
-// fp8 QKV weight gradient has no fused bias).  Column sums of one 32-column half `d` of a transposed 32x32
-// accumulator over the 32 lanes of each wave half (the wave's 32 tokens): a reduce-scatter butterfly over
-// lane masks 16, 8, 4, 2 then one plain exchange — 4·(8+4+2+1)+1 ops instead of 5·16.  Lanes l and l^1 end
-// with the sum of accumulator row r = (l >> 1) & 15 (value order: level m keeps the lower half of the list
-// when lane bit m is 0).  Invalid lanes (tokens past L) contribute 0.
+// fp8 QKV weight gradient has no fused bias).  Column sums of one 32-column half of a transposed 32x32
+// accumulator over the 32 lanes of each wave half (the wave's 32 tokens), as a reduce-scatter butterfly on
+// VALU lane exchanges only (no LDS): lane bit 4 with v_permlane16_swap (one swap hands each 16-lane row the
+// other row's half, so keep + partner = both results summed), then DPP row_ror:8 (bit 3), row_half_mirror
+// (lane ^ 7: decides bit 2), quad_perm (lane ^ 2), and a final lane ^ 1 add.  Lanes l and l^1 end with the
+// sum of accumulator row r = (l >> 1) & 15.  Invalid lanes (tokens past L) contribute 0.
+__device__ __forceinline__ float dpp_f(float x, int ctrl_sel) {
+  const int v = __float_as_int(x);
+  int r;
+  switch (ctrl_sel) {   // compile-time after inlining
+    case 0: r = __builtin_amdgcn_update_dpp(0, v, 0x128, 0xf, 0xf, false); break;   // row_ror:8  (lane ^ 8)
+    case 1: r = __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false); break;   // row_half_mirror (^ 7)
+    case 2: r = __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false); break;    // quad_perm 2,3,0,1 (^ 2)
+    default: r = __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false); break;   // quad_perm 1,0,3,2 (^ 1)
+  }
+  return __int_as_float(r);
+}
 __device__ __forceinline__ float colsum16(const f32x16_t& a, float mul, bool valid, int lane) {
   float v[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = valid ? a[r] * mul : 0.f;
+  // bit 4: rows 0/1 (and 2/3) of 16 lanes trade halves; afterwards both hold keep + partner's
 #pragma unroll
-  for (int lvl = 0; lvl < 4; ++lvl) {
-    const int m = 16 >> lvl, k = 8 >> lvl;
-    const bool up = (lane & m) != 0;
+  for (int i = 0; i < 8; ++i) {
+    const auto t = __builtin_amdgcn_permlane16_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 8]), false, false);
+    v[i] = __uint_as_float(t[0]) + __uint_as_float(t[1]);
+  }
+  // bits 3, 2, 1: keep the half selected by the lane bit, add the partner's copy of it
+#pragma unroll
+  for (int lvl = 0; lvl < 3; ++lvl) {
+    const int k = 4 >> lvl, bit = 8 >> lvl;
+    const bool up = (lane & bit) != 0;
 #pragma unroll
     for (int i = 0; i < k; ++i) {
       const float send = up ? v[i] : v[i + k];
       const float keep = up ? v[i + k] : v[i];
-      v[i] = keep + __shfl_xor(send, m, 64);
+      v[i] = keep + dpp_f(send, lvl);
     }
   }
-  return v[0] + __shfl_xor(v[0], 1, 64);
+  return v[0] + dpp_f(v[0], 3);
 }
 // both halves of a row-of-64 accumulator pair -> row `dst` (64 floats: column d·32 + acc_row(r, hh))
 __device__ __forceinline__ void colsum_row64(float* dst, const f32x16_t (&a)[2], float mul, bool valid, int lane,
