@@ -489,8 +489,7 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor key_bias, int64_t B, int64_t L, 
 // bpart [B·ceil(L/32), 3H] instead (colsum_into reduces them)
 std::vector<Tensor> attn_bwd_impl(Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, Tensor mbits, int64_t B,
                                   int64_t L, int64_t nh, double p, double scale, bool deterministic,
-                                  c10::optional<Tensor> q8, int64_t phase, bool write_bf16 = true,
-                                  bool bias_part = false) {
+                                  c10::optional<Tensor> q8, int64_t phase, bool write_bf16 = true) {
   check_attn(qkv, key_bias, B, L, nh);
   check(dctx, BF16, "dctx"); check(ctx, BF16, "ctx"); check(lse, F32, "lse");
   const int64_t H = qkv.size(1) / 3;
@@ -505,8 +504,7 @@ std::vector<Tensor> attn_bwd_impl(Tensor dctx, Tensor qkv, Tensor ctx, Tensor ls
   TORCH_CHECK(write_bf16 || want8, "attn_bwd: write_bf16=False needs q8");
   auto dqkv = write_bf16 ? at::empty_like(qkv) : at::empty({0}, qkv.options());
   auto delta = at::empty({B, nh, L}, lse.options());
-  const bool want_bp = !write_bf16 || bias_part;
-  Tensor bpart = want_bp ? at::empty({B * ((L + 31) / 32), qkv.size(1)}, lse.options()) : Tensor();
+  Tensor bpart = write_bf16 ? Tensor() : at::empty({B * ((L + 31) / 32), qkv.size(1)}, lse.options());
   Tensor dqkv8;
   if (want8) {
     check(*q8, F32, "q8");
@@ -517,9 +515,8 @@ std::vector<Tensor> attn_bwd_impl(Tensor dctx, Tensor qkv, Tensor ctx, Tensor ls
               p > 0 ? ptr<uint16_t>(mbits) : nullptr, write_bf16 ? ptr<uint16_t>(dqkv) : nullptr, ptr<float>(delta), (int)B,
               (int)L, (int)nh, 64, (float)p, (float)scale, deterministic, cur_stream(),
               want8 ? reinterpret_cast<uint8_t*>(dqkv8.data_ptr()) : nullptr, want8 ? ptr<float>(*q8) : nullptr,
-              (int)(phase % 3), want_bp ? ptr<float>(bpart) : nullptr);
+              (int)(phase % 3), write_bf16 ? nullptr : ptr<float>(bpart));
   if (!write_bf16) return {dqkv, dqkv8, bpart};
-  if (bias_part && !want8) return {dqkv, bpart};
   if (want8) return {dqkv, dqkv8};
   return {dqkv};
 }
@@ -758,12 +755,6 @@ PYBIND11_MODULE(_hq_kernels, m) {
         py::arg("p"), py::arg("seed"), py::arg("opid"), py::arg("scale"), py::arg("q8") = py::none(),
         py::arg("phase") = 0);
   m.def("attn_bwd", &attn_bwd);
-  // bf16 dQKV + QKV bias-gradient column partials [B·ceil(L/32), 3H] -> [dqkv, bpart]
-  m.def("attn_bwd_bpart", [](Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, Tensor mbits, int64_t B,
-                             int64_t L, int64_t nh, double p, double scale, bool deterministic) {
-    return attn_bwd_impl(dctx, qkv, ctx, lse, key_bias, mbits, B, L, nh, p, scale, deterministic, c10::nullopt, 0, true,
-                         true);
-  });
   m.def("attn_bwd_q8", [](Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, Tensor mbits, int64_t B,
                           int64_t L, int64_t nh, double p, double scale, bool deterministic, Tensor q8, int64_t phase,
                           bool write_bf16) {

@@ -58,8 +58,8 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
                  const uint16_t* mbits, uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p, float scale,
                  bool deterministic, hipStream_t s, uint8_t* dqkv8 = nullptr, float* q8 = nullptr, int phase = 0,
                  float* bpart = nullptr);
-// bpart != null: the QKV bias-gradient column partials bpart[B·ceil(L/32)][3H] (sum over rows = Σ_t dQKV[t, :])
-// for a weight gradient without fused bias; with dqkv8 as well, dqkv (bf16) is NOT written (fp8 backward).
+// bpart != null (with dqkv8): dqkv (bf16) is NOT written; instead the QKV bias-gradient column partials
+// bpart[B·ceil(L/32)][3H] (sum over rows = Σ_t dQKV[t, :]) for the fp8 weight gradient.
 
 // ---- optim.hip --------------------------------------------------------------------------------
 struct HqOptChunk {      // one work item of the fused optimizer: <= kOptChunk elements of one segment

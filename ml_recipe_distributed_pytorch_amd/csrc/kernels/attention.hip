@@ -706,8 +706,7 @@ __device__ __forceinline__ void split3(float x, uint16_t& hi, uint16_t& mid, uin
   lo = bf16_rne(r - hq_bf2f(mid));
 }
 
-// MODE 0: bf16 dQKV; 3: bf16 + column partials of the QKV bias gradient into bpart (its weight gradient then
-// runs without a fused bias); 1: bf16 + e5m2 copy (fp8 backward, calibrating); 2: e5m2 only + column partials of the
+// MODE 0: bf16 dQKV; 1: bf16 + e5m2 copy (fp8 backward, calibrating); 2: e5m2 only + column partials of the
 // QKV bias gradient into bpart [B·n32][3H] (fp8 backward, calibrated: every consumer reads the e5m2 copy)
 template <bool DROP, int NT, int RAHEAD, int MODE = 0>
 __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
@@ -716,7 +715,7 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
     float* __restrict__ delta, uint16_t* __restrict__ dqkv, int L, int nh, int n_qb, float c_scale, float scale,
     float kscale, uint8_t* __restrict__ dqkv8, const float* __restrict__ q8, float* __restrict__ part8, int phase,
     float* __restrict__ bpart) {
-  constexpr bool Q8 = MODE == 1 || MODE == 2;
+  constexpr bool Q8 = MODE > 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int RNS = RAHEAD + 2;
   const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
@@ -865,7 +864,6 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
     return;
   }
   if (qok) store_row64(dqkv + orow_q, dq, scale, hh);
-  if constexpr (MODE == 3) colsum_row64(bpart + ((size_t)b * n32 + qs) * 3 * H + h * D, dq, scale, qok, lane, hh);
 }
 
 // dK/dV: keys on the lanes.  Per 32-query tile: S = Q'·Kᵀ (+ aug: −LSE, bias), dP = dO·Vᵀ, then
@@ -877,7 +875,7 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
     uint16_t* __restrict__ dqkv, int L, int nh, int n_kb, float c_scale, float scale, float kscale,
     uint8_t* __restrict__ dqkv8, const float* __restrict__ q8, float* __restrict__ part8, int phase,
     float* __restrict__ bpart) {
-  constexpr bool Q8 = MODE == 1 || MODE == 2;
+  constexpr bool Q8 = MODE > 0;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // slot: Q' [32][64] 4 KB | dO [32][64] 4 KB | A' words [32] uint4 512 B | δ [32] f32 128 B | bits [RW][64] u16
   constexpr int SLOT = 2 * RTILE + 512 + 128 + RW * 128;
@@ -1073,13 +1071,6 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
     store_row64(out + 2 * H, dv, 1.f, hh);
     store_row64(out + H, dk, LN2, hh);                   // Q' = c·Q with c = scale·log2e: dK = Σ dS·Q'/log2e
   }
-  if constexpr (MODE == 3) {
-    if (active) {
-      float* row = bpart + ((size_t)b * n32 + ks_idx) * 3 * H + h * D;
-      colsum_row64(row + 2 * H, dv, 1.f, kok, lane, hh);
-      colsum_row64(row + H, dk, LN2, kok, lane, hh);
-    }
-  }
 }
 
 }  // namespace
@@ -1194,9 +1185,6 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
       } else if (dqkv8) {   // --precision fp8: the e5m2-writing variants
         if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH, 1>, attn_bwd_dkdv_ring_kernel<true, NT, 1>);
         else launch(attn_bwd_dq_ring_kernel<false, NT, AH, 1>, attn_bwd_dkdv_ring_kernel<false, NT, 1>);
-      } else if (bpart) {   // bf16 + QKV bias partials
-        if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH, 3>, attn_bwd_dkdv_ring_kernel<true, NT, 3>);
-        else launch(attn_bwd_dq_ring_kernel<false, NT, AH, 3>, attn_bwd_dkdv_ring_kernel<false, NT, 3>);
       } else {
         if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH>, attn_bwd_dkdv_ring_kernel<true, NT>);
         else launch(attn_bwd_dq_ring_kernel<false, NT, AH>, attn_bwd_dkdv_ring_kernel<false, NT>);

@@ -344,16 +344,11 @@ class _LayerFn(torch.autograd.Function):
             need = not (s8["dqkv"].step >= 1 and (f8 is not None or not trainable))
             dqkv, dqkv8, bpart = ops.attn_bwd_q8(dctx, qkv, ctxv, lse, key_bias, ctx.bits, B, L, nh, ctx.pa, ctx.scale,
                                                  s8["dqkv"], need)
-        elif dh2.is_cuda:   # the QKV bias gradient from in-kernel column partials: its wgrad runs bias-free
-            dqkv, bpart = ops.attn_bwd_bpart(dctx, qkv, ctxv, lse, key_bias, ctx.bits, B, L, nh, ctx.pa, ctx.scale)
         else:
             dqkv = ops.attn_bwd(dctx, qkv, ctxv, lse, key_bias, ctx.bits, B, L, nh, ctx.pa, info.seed, op0, ctx.scale)
         ctx.bits = None
         if bpart is not None:
-            if dqkv is None:   # fp8, calibrated: e5m2 dQKV × the e4m3 QKV input
-                wgrad(None, None, G("qkv.weight"), None, (dqkv8, s8["dqkv"], f8[3], s8["qkv"]))
-            else:              # bf16
-                wgrad(dqkv, x, G("qkv.weight"), None)
+            wgrad(None, None, G("qkv.weight"), None, (dqkv8, s8["dqkv"], f8[3], s8["qkv"]))
             if trainable:
                 ops.colsum_into(bpart, G("qkv.bias"), acc)
         else:

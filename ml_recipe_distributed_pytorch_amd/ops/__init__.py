@@ -125,13 +125,6 @@ def attn_bwd_q8(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, scale, state: 
     return (r[0], r[1], None) if need_bf16 else (None, r[1], r[2])
 
 
-def attn_bwd_bpart(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, scale):
-    """GPU ``attn_bwd`` that also returns column partials of the QKV bias gradient (fp32, summed over each
-    wave's 32 tokens in-kernel): (dqkv, bpart) — so the QKV weight gradient runs without a fused bias."""
-    return tuple(_k().attn_bwd_bpart(dctx, qkv, ctx, lse, key_bias, bits, int(B), int(L), int(nh), float(p),
-                                     float(scale), deterministic()))
-
-
 def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale):
     if dctx.is_cuda:
         return _k().attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, int(B), int(L), int(nh), float(p), float(scale),

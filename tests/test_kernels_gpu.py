@@ -150,27 +150,6 @@ def test_attention_bwd_deterministic_mode_repeatable(cuda):
         assert torch.equal(k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125, det), d0)
 
 
-@pytest.mark.parametrize("L", [384, 100])
-def test_attention_bwd_bias_partials(cuda, L):
-    """attn_bwd_bpart: bitwise the same dQKV as attn_bwd, plus per-32-token column partials whose sum is the QKV
-    bias gradient Σ_t dQKV[t, :] (fp32 in-kernel sums over the transposed accumulators; ragged L included)."""
-    k = _native.kernels()
-    torch.manual_seed(6)
-    B, nh = 3, 12
-    H = nh * 64
-    qkv = _bf(torch.randn(B * L, 3 * H)).to(cuda)
-    kb = torch.zeros(B, L, device=cuda)
-    kb[1, L // 2:] = -10000.0
-    ctx, lse, bits = k.attn_fwd(qkv, kb, B, L, nh, 0.1, 7, 1, 0.125)
-    dctx = _bf(torch.randn(B * L, H)).to(cuda)
-    d0 = k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125, True)
-    d1, bpart = k.attn_bwd_bpart(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125, True)
-    assert torch.equal(d0, d1)
-    assert bpart.shape == (B * ((L + 31) // 32), 3 * H)
-    ref = d0.float().sum(0)
-    torch.testing.assert_close(bpart.sum(0), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
-
-
 def test_attention_bert_base_shape(cuda):
     _attn_case(cuda, 2, 384, 12, 0.1, masked=False)
 
