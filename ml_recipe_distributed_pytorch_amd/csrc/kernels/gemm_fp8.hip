@@ -47,11 +47,21 @@ __device__ __forceinline__ f32x4_t mfma_fp8(const i32x8& w, const i32x8& x, cons
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(w, x, c, 0, FX, 0, 127, 0, 127);
 }
 
+// 16-B chunk swizzle of the 128-B LDS rows: chunk ^= f8row(row).  With the bf16 kernels' (row >> 1) & 7 the
+// fragment reads below were 2-way bank-conflicted (PMC: SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE = 0.50): in
+// each 16-lane group of a ds_read_b128 (lanes {0–3,12–15,20–27}, {4–11,16–19,28–31}, …) rows 2j / 2j+1 of
+// fq = 0 and rows of fq = 1 land on the same chunks.  j ^ ((j & 2) << 1), j = (row >> 1) & 7, gives the
+// eight rows of each parity in a group eight distinct chunks for every slot pair (2fq, 2fq+1).
+__device__ __forceinline__ int f8row(int row) {
+  const int j = (row >> 1) & 7;
+  return j ^ ((j & 2) << 1);
+}
+
 // 32-byte fragment (k = 32·fq … +31) of LDS row `row`: slots 2fq and 2fq+1, source swizzle undone.
 // Inline asm: with plain loads hipcc (ROCm 7.2) drained vmcnt(0) before these reads in this kernel (it
 // could not rule out aliasing with the in-flight LDS-DMA); mma() waits lgkmcnt(0) + sched_barrier.
 __device__ __forceinline__ i32x8 frag32(uint32_t panel, int row, int fq) {
-  const int sw = (row >> 1) & 7;
+  const int sw = f8row(row);
   const uint32_t a0 = panel + row * 128 + (((2 * fq) ^ sw) << 4);
   const uint32_t a1 = panel + row * 128 + (((2 * fq + 1) ^ sw) << 4);
   typedef __attribute__((ext_vector_type(4))) int i32x4;
@@ -150,7 +160,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = wave * 16 + i * 8 + (lane >> 3);
-    const int src_slot = (lane & 7) ^ ((row >> 1) & 7);
+    const int src_slot = (lane & 7) ^ f8row(row);
     voA[i] = row * lda + src_slot * 16;
     voB[i] = row * ldb + src_slot * 16;
   }
@@ -360,7 +370,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* _
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = wave * 16 + i * 8 + (lane >> 3);
-    const int src_slot = (lane & 7) ^ ((row >> 1) & 7);
+    const int src_slot = (lane & 7) ^ f8row(row);
     voA[i] = row * lda + src_slot * 16;
     voB[i] = row * ldb + src_slot * 16;
   }
