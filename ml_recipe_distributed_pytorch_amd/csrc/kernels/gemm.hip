@@ -45,9 +45,6 @@ typedef __attribute__((address_space(1))) void g_void;
 __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, const f32x4_t& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-__device__ __forceinline__ f32x16_t mfma32(const bf16x8_t& a, const bf16x8_t& b, const f32x16_t& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
 
 __device__ __forceinline__ float gelu_erf(float x) { return hq_gelu(x); }
 __device__ __forceinline__ float gelu_grad(float x) { return hq_gelu_grad(x); }
@@ -836,10 +833,7 @@ struct NT3Epi {
   static constexpr int E = kStores + kLoads;   // vm ops per lane (the part store of waves 0-3 is not counted: a
 };                                             // smaller count only waits longer)
 
-// M32: the same phase table on v_mfma_f32_32x32x16_bf16 (a quadrant = 2 × 1 32² tiles × 4 k-steps = 8
-// MFMAs instead of 4 × 2 16² tiles × 2 k-steps = 16); operands swapped as in the 16² form, so a lane holds
-// m = lane & 31 and n = 8·(r >> 2) + 4·(lane >> 5) + (r & 3) of accumulator register r.
-template <int EPI, bool M32 = false>
+template <int EPI>
 __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                                uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                                uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
@@ -904,55 +898,32 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   };
 
   f32x4_t acc[8][4];
-  f32x16_t acc32[4][2];   // M32: [mh·2 + i][nh]
   const int fr = lane & 15, fq = lane >> 4;
-  const int r32 = lane & 31, h32 = lane >> 5;
-  // 16² form: [ks][i] / [ks][j]; M32 form: flat index ks·2 + i of 8 A fragments, ks of 4 B fragments
   bf16x8_t af[2][4];
   bf16x8_t bf0[2][2], bf1[2][2];
   auto readA = [&](int buf, int mh) {
     const char* pa = smem + buf * STAGE;
-    if constexpr (M32) {
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) af[ks >> 1][(ks & 1) * 2 + i] = frag(pa, mh * 128 + wm * 64 + i * 32 + r32, ks * 2 + h32);
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) af[ks][i] = frag(pa, mh * 128 + wm * 64 + i * 16 + fr, ks * 4 + fq);
-    }
+      for (int i = 0; i < 4; ++i) af[ks][i] = frag(pa, mh * 128 + wm * 64 + i * 16 + fr, ks * 4 + fq);
   };
   auto readB = [&](int buf, int nh, bf16x8_t (&bf)[2][2]) {
     const char* pb = smem + buf * STAGE + PANEL;
-    if constexpr (M32) {
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks) bf[ks >> 1][ks & 1] = frag(pb, nh * 128 + wn * 32 + r32, ks * 2 + h32);
-    } else {
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) bf[ks][j] = frag(pb, nh * 128 + wn * 32 + j * 16 + fr, ks * 4 + fq);
-    }
+      for (int j = 0; j < 2; ++j) bf[ks][j] = frag(pb, nh * 128 + wn * 32 + j * 16 + fr, ks * 4 + fq);
   };
   auto mma = [&](int mh, int nh, const bf16x8_t (&bf)[2][2]) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
-    if constexpr (M32) {
 #pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-          acc32[mh * 2 + i][nh] = mfma32(bf[ks >> 1][ks & 1], af[ks >> 1][(ks & 1) * 2 + i], acc32[mh * 2 + i][nh]);
-    } else {
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[mh * 4 + i][nh * 2 + j] = mfma16(bf[ks][j], af[ks][i], acc[mh * 4 + i][nh * 2 + j]);
-    }
+        for (int j = 0; j < 2; ++j) acc[mh * 4 + i][nh * 2 + j] = mfma16(bf[ks][j], af[ks][i], acc[mh * 4 + i][nh * 2 + j]);
     __builtin_amdgcn_s_setprio(0);
   };
   auto bar = []() {
@@ -1011,17 +982,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     const __amdgpu_buffer_rsrc_t na = rsrc_a(last ? tile : next), nb = rsrc_b(last ? tile : next);
     const int tm = tile / tiles_n, tn = tile % tiles_n;
     const int m0 = tm * BM, n0 = tn * BN;
-    if constexpr (M32) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc32[i][j] = f32x16_t{};
-    } else {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    }
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
     // One K-tile = 4 phases (v2's table); "t+1" / "t+2" halves past this tile's end come from the next
     // tile's K-tile 0 (t+1 == nt, t+2 == nt); the next tile's K-tile 1 (t+2 == nt+1) is held back.
@@ -1100,36 +1064,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     for (int e = 0; e < 8; ++e) csum[e] = 0.f;
 #pragma unroll
     for (int rnd = 0; rnd < 2; ++rnd) {
-      if constexpr (M32) {
 #pragma unroll
-        for (int nh = 0; nh < 2; ++nh)
+      for (int J = 0; J < 4; ++J) {
+        const int nh = J >> 1, j = J & 1;
+        const int lc = nh * 32 + j * 16 + fq * 4;
+        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int lc = nh * 32 + g * 8 + h32 * 4;
-            float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-            if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + g * 8 + h32 * 4);
-#pragma unroll
-            for (int i = 0; i < 2; ++i) {
-              const f32x16_t& a = acc32[rnd * 2 + i][nh];
-              float v[4] = {a[4 * g], a[4 * g + 1], a[4 * g + 2], a[4 * g + 3]};
-              if constexpr (kBias) { v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w; }
-              *reinterpret_cast<uint2*>(wreg + (i * 32 + r32) * RS + lc * 2) = hq_pack4(v);
-            }
-          }
-      } else {
-#pragma unroll
-        for (int J = 0; J < 4; ++J) {
-          const int nh = J >> 1, j = J & 1;
-          const int lc = nh * 32 + j * 16 + fq * 4;
-          float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-          if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
-#pragma unroll
-          for (int I = 0; I < 4; ++I) {
-            const f32x4_t& a = acc[rnd * 4 + I][J];
-            float v[4] = {a[0], a[1], a[2], a[3]};
-            if constexpr (kBias) { v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w; }
-            *reinterpret_cast<uint2*>(wreg + (I * 16 + fr) * RS + lc * 2) = hq_pack4(v);
-          }
+        for (int I = 0; I < 4; ++I) {
+          const f32x4_t& a = acc[rnd * 4 + I][J];
+          float v[4] = {a[0], a[1], a[2], a[3]};
+          if constexpr (kBias) { v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w; }
+          *reinterpret_cast<uint2*>(wreg + (I * 16 + fr) * RS + lc * 2) = hq_pack4(v);
         }
       }
       uint4 aux[kReadsAux ? 8 : 1];
@@ -1239,13 +1185,10 @@ int g_gemm_variant = [] {
 }();
 // v3 start offset of odd workgroups per XCD, in units of s_sleep(127) (HQ_GEMM_STAGGER, bits 0-7) and
 // the epilogue A/B knobs (HQ_GEMM_EPIFLAGS, bits 8-15); both 0 in production
-// bit 16 (kMfma32): the v3 kernel's 32x32x16 MFMA form (HQ_GEMM_MFMA32)
-constexpr int kMfma32 = 1 << 16;
 int g_gemm_stagger = [] {
   const char* e = getenv("HQ_GEMM_STAGGER");
   const char* f = getenv("HQ_GEMM_EPIFLAGS");
-  const char* m = getenv("HQ_GEMM_MFMA32");
-  return (e ? atoi(e) & 0xFF : 0) | ((f ? atoi(f) & 0xFF : 0) << 8) | (m && atoi(m) ? kMfma32 : 0);
+  return (e ? atoi(e) & 0xFF : 0) | ((f ? atoi(f) & 0xFF : 0) << 8);
 }();
 
 // default static: uncontended the dynamic schedule costs ~0.9 % of the step (profiles/r2_sched); GradReducer
@@ -1362,18 +1305,13 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
       int dev = 0, n = 0;
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-      (void)hipFuncSetAttribute((const void*)gemm_nt3_kernel<EPI, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      (void)hipFuncSetAttribute((const void*)gemm_nt3_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (void)hipFuncSetAttribute((const void*)gemm_nt3_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       return n > 0 ? n : 256;
     }();
     const int nwg = std::min(grid, ncu);
     unsigned* sched = (g_gemm_sched && grid > 2 * nwg) ? nt3_sched_slot(s) : nullptr;
-    if (g_gemm_stagger & kMfma32)
-      hipLaunchKernelGGL((gemm_nt3_kernel<EPI, true>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, R, part,
-                         M, N, K, lda, ldb, ldc, g_gemm_stagger & 0xFFFF, sched, dr);
-    else
-      hipLaunchKernelGGL((gemm_nt3_kernel<EPI, false>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, R, part,
-                         M, N, K, lda, ldb, ldc, g_gemm_stagger & 0xFFFF, sched, dr);
+    hipLaunchKernelGGL((gemm_nt3_kernel<EPI>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, R, part,
+                       M, N, K, lda, ldb, ldc, g_gemm_stagger, sched, dr);
   } else if (bn == 256 && (g_gemm_variant == 0 || g_gemm_variant == 2 || g_gemm_variant == 3) && K >= 2 * BK && srd_ok) {
     // production v2: buffer_load…lds staging (+8-12 % over global_load_lds on the BERT shapes,
     // tools/gemm_lab); grouped 8-row-panel tile order only for wide N (+15 % at 8192², neutral at
