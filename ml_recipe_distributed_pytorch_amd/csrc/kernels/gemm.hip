@@ -851,7 +851,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   constexpr int E = NT3Epi<EPI>::E;
   constexpr int TICKET = SPARE + REGION + 2 * BN * 4;   // LDS word: the tile after `next` (dynamic schedule)
   static_assert(7 * REGION <= STAGE && TICKET + 16 <= 160 * 1024, "LDS plan");
-  const int epi_flags = stagger >> 8;   // HQ_GEMM_EPIFLAGS (A/B knobs; 0 in production)
+  const bool ht_on = (stagger >> 16) & 1;   // kHalfTail
+  const int epi_flags = (stagger >> 8) & 0xFF;   // HQ_GEMM_EPIFLAGS (A/B knobs; 0 in production)
   stagger &= 0xFF;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
 
@@ -865,6 +866,22 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   const int tiles_n = N / BN, ntiles = (M / BM) * tiles_n;
   const int nt = K / BK;
   HQ_DASSERT(K % BK == 0 && nt >= 2 && N % BN == 0 && M % BM == 0);
+  // Half-tile tail: when the last wave of tiles is at most half full (rtail = ntiles % nwg tiles on nwg
+  // workgroups), its rtail tiles run as 2·rtail 128-row "half tiles", one per workgroup, so that wave costs about
+  // half a tile's time instead of a whole one (at B = 256 every N = 768 GEMM has 4.5 waves of tiles).  Work
+  // units: 0 … F-1 the full tiles, F … F+2·rtail-1 the halves (unit F + 2h + e = rows e·128 … of tile F + h).  A
+  // half tile keeps the full tile's load / barrier / wait sequence (its second 128 A rows are staged and
+  // never read) and skips the m-half-1 MFMA phases, fragment reads and epilogue round.  Column partials
+  // (DGELU / DMUL) are per 256-row block, so those epilogues never split.
+  constexpr bool kHalfOK = !(EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL);
+  const int rtail = ntiles % nwg;
+  const bool halftail = kHalfOK && ht_on && rtail > 0 && 2 * rtail <= nwg;
+  const int F = halftail ? ntiles - rtail : ntiles;
+  const int nunits = halftail ? F + 2 * rtail : ntiles;
+  auto unit_m0 = [&](int u) {
+    return u < F ? (u / tiles_n) * BM : ((F + ((u - F) >> 1)) / tiles_n) * BM + ((u - F) & 1) * 128;
+  };
+  auto unit_n0 = [&](int u) { return (u < F ? u : F + ((u - F) >> 1)) % tiles_n * BN; };
 
   int voA[2], voB[2];
 #pragma unroll
@@ -874,14 +891,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     voA[i] = (row * lda + src_slot * 8) * 2;
     voB[i] = (row * ldb + src_slot * 8) * 2;
   }
-  // buffer descriptors over a tile's A row panel / B column panel
-  auto rsrc_a = [&](int tile) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)(tile / tiles_n) * BM * lda), (short)0, BM * lda * 2,
+  // buffer descriptors over a unit's A row panel / B column panel (a last half tile's panel ends at row M:
+  // its unread second 128 rows load as zeros)
+  auto rsrc_a = [&](int u) {
+    const int m0 = unit_m0(u);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * lda), (short)0, min(BM, M - m0) * lda * 2,
                                              0x00020000);
   };
-  auto rsrc_b = [&](int tile) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(B + (size_t)(tile % tiles_n) * BN * ldb), (short)0, BN * ldb * 2,
-                                             0x00020000);
+  auto rsrc_b = [&](int u) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(B + (size_t)unit_n0(u) * ldb), (short)0, BN * ldb * 2, 0x00020000);
   };
   // one 16 KiB half (128 rows × 64 bf16) of K-tile `kt` into LDS buffer `buf`
   auto stA = [&](__amdgpu_buffer_rsrc_t rs, int half, int kt, int buf) {
@@ -945,9 +963,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   // the spot — out of it) and published through LDS after the K-loop, where hipcc drains vmcnt anyway.
   // Every workgroup bumps sched[256] on exit; the last one zeroes the counters for the next launch on this
   // stream (stream order: the next launch starts after this one has drained, graph replays included).
-  int tile = id;
-  HQ_DASSERT(tile < ntiles);     // the host launches min(tiles, CUs) workgroups, so every one has a tile
-  if (tile >= ntiles) return;   // (unreachable; an early exit would skip the exit count that re-zeroes sched)
+  int tile = id;                // a work unit (see the half-tile tail above)
+  HQ_DASSERT(tile < nunits);     // the host launches min(tiles, CUs) workgroups, so every one has a tile
+  if (tile >= nunits) return;   // (unreachable; an early exit would skip the exit count that re-zeroes sched)
   int next = tile + nwg;
   const int cnt_x = q + (xcd < r ? 1 : 0), base_x = id - (bid >> 3);
   unsigned* tix = sched ? sched + 32 * xcd : nullptr;
@@ -964,9 +982,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   bar();
   bool first = true;
+  bool prev_half = false;       // the previous unit was a half tile: its epilogue issued E / 2 vm ops
 
   for (;;) {
-    const bool last = next >= ntiles;
+    const bool last = next >= nunits;
+    const bool half = __builtin_amdgcn_readfirstlane(tile >= F ? 1 : 0) != 0;
     unsigned ticket = 0;
     const bool draw = sched && !last;
     // drawn in phase P1 of K-tile 0, after that phase's stage: the counted vmcnt(6) of K-tile 1's P1 (6 newer
@@ -980,8 +1000,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       }
     };
     const __amdgpu_buffer_rsrc_t na = rsrc_a(last ? tile : next), nb = rsrc_b(last ? tile : next);
-    const int tm = tile / tiles_n, tn = tile % tiles_n;
-    const int m0 = tm * BM, n0 = tn * BN;
+    const int m0 = unit_m0(tile), n0 = unit_n0(tile);
+    const int tm = m0 / BM;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -999,7 +1019,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       const int k1 = x1 ? t + 1 - nt : t + 1, k2 = x2 ? t + 2 - nt : t + 2;
       // P0 (0,0)
       if (t == 0 && !first) {
-        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E) : "memory");
+        if (prev_half) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E / 2) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E) : "memory");
       } else if (more1) {
         asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       } else {
@@ -1013,7 +1034,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       bar();
       // P1 (0,1)
       if (t == 0 && !first) {
-        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E) : "memory");
+        if (prev_half) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E / 2) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E) : "memory");
       } else if (more1) {
         asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       } else {
@@ -1026,10 +1048,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       mma(0, 1, bf1);
       bar();
       // P2 (1,1)
-      readA(b0, 1);
+      if (!half) readA(b0, 1);
       if (more2) stA(a2, 0, k2, b0);
       bar();
-      mma(1, 1, bf1);
+      if (!half) mma(1, 1, bf1);
       bar();
       // P3 (1,0)
       if (more1) {
@@ -1037,7 +1059,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       }
       if (more2) stB(b2r, 0, k2, b0);
       bar();
-      mma(1, 0, bf0);
+      if (!half) mma(1, 0, bf0);
       bar();
     };
     if (__builtin_amdgcn_readfirstlane(wm) == 0) {
@@ -1064,6 +1086,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     for (int e = 0; e < 8; ++e) csum[e] = 0.f;
 #pragma unroll
     for (int rnd = 0; rnd < 2; ++rnd) {
+      if (rnd == 1 && half) break;
 #pragma unroll
       for (int J = 0; J < 4; ++J) {
         const int nh = J >> 1, j = J & 1;
@@ -1161,8 +1184,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     if (sched) {
       const unsigned sx = *reinterpret_cast<const unsigned*>(smem + TICKET);
       const long t = (long)(sx / (unsigned)cnt_x) * nwg + base_x + (long)(sx % (unsigned)cnt_x);
-      after = t < ntiles ? (int)t : ntiles;
+      after = t < nunits ? (int)t : nunits;
     }
+    prev_half = half;
     tile = next;
     next = __builtin_amdgcn_readfirstlane(after);
     ca = na;
@@ -1185,10 +1209,14 @@ int g_gemm_variant = [] {
 }();
 // v3 start offset of odd workgroups per XCD, in units of s_sleep(127) (HQ_GEMM_STAGGER, bits 0-7) and
 // the epilogue A/B knobs (HQ_GEMM_EPIFLAGS, bits 8-15); both 0 in production
+// bit 16 (kHalfTail): v3 runs a last, at most half-full wave of tiles as 128-row half tiles (on by default;
+// HQ_GEMM_HALFTAIL=0 turns it off for A/B)
+constexpr int kHalfTail = 1 << 16;
 int g_gemm_stagger = [] {
   const char* e = getenv("HQ_GEMM_STAGGER");
   const char* f = getenv("HQ_GEMM_EPIFLAGS");
-  return (e ? atoi(e) & 0xFF : 0) | ((f ? atoi(f) & 0xFF : 0) << 8);
+  const char* h = getenv("HQ_GEMM_HALFTAIL");
+  return (e ? atoi(e) & 0xFF : 0) | ((f ? atoi(f) & 0xFF : 0) << 8) | (h && !atoi(h) ? 0 : kHalfTail);
 }();
 
 // default static: uncontended the dynamic schedule costs ~0.9 % of the step (profiles/r2_sched); GradReducer

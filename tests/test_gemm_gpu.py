@@ -258,3 +258,54 @@ def test_gemm_nt_split_k_low_fill(cuda, M, N, K, variant):
         assert torch.equal(k.gemm_nt(A, B, EPI_NONE), c0)
     resid = torch.randn(M, N, device=cuda, generator=g).bfloat16()
     _close(k.gemm_nt(A, B, EPI_RESID, resid=resid), ref + resid.float())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(25600, 768, 768), (25600, 768, 2304), (98304, 768, 768)])
+def test_gemm_nt_half_tile_tail(cuda, M, N, K, variant):
+    """v3's half-tile tail (a last wave of tiles at most half full runs as 128-row half tiles): 300 or 1152
+    256² tiles on 256 CUs.  Every epilogue must be bitwise equal with the tail split on and off (a half tile
+    accumulates its rows in the same order) and match the fp32 reference; DGELU / DMUL never split."""
+    if variant not in (0, 3):
+        pytest.skip("the half-tile tail is a v3 schedule")
+    EPI_GELUD, EPI_DMUL, EPI_BDR = 5, 6, 7
+    HT = 1 << 16
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(M + K)
+    A = (torch.randn(M, K, device=cuda, generator=g) * 0.5).bfloat16()
+    B = (torch.randn(N, K, device=cuda, generator=g) * 0.1).bfloat16()
+    bias = torch.randn(N, device=cuda, generator=g) * 0.1
+    resid = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+    gd = torch.rand(M, N, device=cuda, generator=g).bfloat16()
+    rows = torch.cat([torch.arange(0, 1024), torch.arange(M - 2048, M)]).to(cuda)
+    ref = _ref(A[rows], B)
+
+    def run(epi, **kw):
+        outs = []
+        for w in (0, HT):
+            k.gemm_set_stagger(w)
+            try:
+                kk = {n: (v.clone() if torch.is_tensor(v) and n in ("pre",) and epi in (EPI_GELU, EPI_GELUD) else v)
+                      for n, v in kw.items()}
+                o = k.gemm_nt(A, B, epi, **kk)
+                outs.append((o, kk.get("pre")))
+            finally:
+                k.gemm_set_stagger(HT)
+        assert torch.equal(outs[0][0], outs[1][0]), f"epi {epi}: half-tile tail changed the output"
+        if outs[0][1] is not None and epi in (EPI_GELU, EPI_GELUD):
+            assert torch.equal(outs[0][1], outs[1][1]), f"epi {epi}: half-tile tail changed P"
+        return outs[1]
+
+    _close(run(EPI_NONE)[0][rows], ref)
+    _close(run(EPI_BIAS, bias=bias)[0][rows], ref + bias)
+    _close(run(EPI_RESID, resid=resid)[0][rows], ref + resid[rows].float())
+    o, p = run(EPI_GELU, bias=bias, pre=torch.empty(M, N, device=cuda, dtype=torch.bfloat16))
+    _close(p[rows], ref + bias)
+    _close(o[rows], torch.nn.functional.gelu(p[rows].float()))
+    o, _ = run(EPI_GELUD, bias=bias, pre=torch.empty(M, N, device=cuda, dtype=torch.bfloat16))
+    _close(o[rows], torch.nn.functional.gelu(ref + bias))
+    part = torch.empty(k.gemm_nt_part_rows(M, N, K), N, device=cuda)
+    _close(run(EPI_DMUL, pre=gd, part=part)[0][rows], ref.bfloat16().float() * gd[rows].float())
+    o, _ = run(EPI_BDR, bias=bias, resid=resid, p=0.0, seed=1, opid=2)
+    _close(o[rows], ref + bias + resid[rows].float())
+    run(EPI_BDR, bias=bias, resid=resid, p=0.1, seed=3, opid=5)   # dropout keyed by the global index: bitwise
