@@ -8,8 +8,9 @@ import torch
 from ml_recipe_distributed_pytorch_amd import _native
 
 EPI_BIAS, EPI_RESID, EPI_GELUD, EPI_DMUL = 1, 4, 5, 6
-# grids above 2 x 256 workgroups (the dynamic schedule's range): 768 and 555 tiles of 256²
-SHAPES = [(16384, 3072, 768), (9472, 3840, 256), (65536, 768, 1536)]
+# grids above 2 x 256 workgroups (the dynamic schedule's range): 768, 555 and 1152 tiles of 256² (555 and 1152 end in a
+# half-full wave: the half-tile tail, whose units a workgroup may draw back to back under the hog)
+SHAPES = [(16384, 3072, 768), (9472, 3840, 256), (65536, 768, 1536), (98304, 768, 768)]
 
 
 def _operands(dev, M, N, K, epi, seed):
