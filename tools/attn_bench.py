@@ -9,7 +9,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.environ.get("HQ_PKG_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ml_recipe_distributed_pytorch_amd._native import kernels  # noqa: E402
 
 
