@@ -547,9 +547,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
 
   const int nwg = gridDim.x;
   const int bid = blockIdx.x;
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int tile = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   const int tiles_n = N / BN;
+  // Half-tile tail (as v3's; production buffer-load form, ungrouped order only): the host launches rt blocks
+  // more than there are tiles when the last wave of tiles would be at most half full; blocks F … nwg-1,
+  // dispatched last, run the last rt tiles as 2·rt 128-row halves.
+  constexpr bool kHalfOK = !(EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL) && (ABL & 8) != 0 && (ABL & 16) == 0;
+  const int ntiles = (M / BM) * tiles_n;
+  const int rt = kHalfOK ? nwg - ntiles : 0;
+  const int F = nwg - 2 * rt;                    // full-tile blocks (= ntiles - rt)
+  const bool half = rt > 0 && bid >= F;
+  const int nfull = rt > 0 ? F : nwg;
+  const int xcd = bid & 7, q = nfull >> 3, r = nfull & 7;
+  const int tile = half ? F + ((bid - F) >> 1) : (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   int tm = tile / tiles_n, tn = tile % tiles_n;
   if constexpr ((ABL & 16) != 0) {
     constexpr int GM = 8;
@@ -558,8 +567,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
     tm = first + in % gsz;
     tn = in / gsz;
   }
-  const int m0 = tm * BM, n0 = tn * BN;
-  HQ_DASSERT(m0 + BM <= M && n0 + BN <= N && K % BK == 0 && K >= 2 * BK);
+  const int m0 = tm * BM + (half ? ((bid - F) & 1) * 128 : 0), n0 = tn * BN;
+  HQ_DASSERT(m0 + (half ? 128 : BM) <= M && n0 + BN <= N && K % BK == 0 && K >= 2 * BK);
 
   const uint16_t* Ab = A + (size_t)m0 * lda;
   const uint16_t* Bb = B + (size_t)n0 * ldb;
@@ -573,7 +582,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
   // 8-row pieces a wave stages are the same for every half and K-tile (the swizzle depends on row
   // bits 1..3 only), so the K-tile and half advance lives in the scalar soffset.
   const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, BM * lda * 2, 0x00020000);
+  // (a last half tile's panel ends at row M: its unread second 128 rows load as zeros)
+  __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, min(BM, M - m0) * lda * 2, 0x00020000);
   __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, BN * ldb * 2, 0x00020000);
   int voA[2], voB[2];
 #pragma unroll
@@ -643,10 +653,18 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
     asm volatile("" ::: "memory");
   };
 
-  // prologue: tile 0 (A0 B0 B1 A1) and the first two halves of tile 1; retire A0(0), B0(0)
-  stage_half(Ab, lda, 0, 0, smem); stage_half(Bb, ldb, 0, 0, smem + PANEL);
-  stage_half(Bb, ldb, 1, 0, smem + PANEL); stage_half(Ab, lda, 1, 0, smem);
-  stage_half(Ab, lda, 0, 1, smem + STAGE); stage_half(Bb, ldb, 0, 1, smem + STAGE + PANEL);
+  // prologue: tile 0 (A0 B0 B1 A1) and the first two halves of tile 1; retire A0(0), B0(0).  Always real
+  // loads (also in the no-load ablation); the buffer form reads a last half tile's panel end as zeros.
+  auto proA = [&](int half, int t) {
+    if constexpr ((ABL & 8) != 0) buf_half(rA, voA, lda, half, t, smem + (t & 1) * STAGE);
+    else stage_half(Ab, lda, half, t, smem + (t & 1) * STAGE);
+  };
+  auto proB = [&](int half, int t) {
+    if constexpr ((ABL & 8) != 0) buf_half(rB, voB, ldb, half, t, smem + (t & 1) * STAGE + PANEL);
+    else stage_half(Bb, ldb, half, t, smem + (t & 1) * STAGE + PANEL);
+  };
+  proA(0, 0); proB(0, 0); proB(1, 0); proA(1, 0);
+  proA(0, 1); proB(0, 1);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   bar();
 
@@ -669,10 +687,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
     mma(0, 1, bf1);
     bar();
     // P2 (1,1)
-    readA(t, 1);
+    if (!half) readA(t, 1);
     if (more2) stA(0, t + 2);
     bar();
-    mma(1, 1, bf1);
+    if (!half) mma(1, 1, bf1);
     bar();
     // P3 (1,0)
     if (more1) {
@@ -680,7 +698,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
     }
     if (more2) stB(0, t + 2);
     bar();
-    mma(1, 0, bf0);
+    if (!half) mma(1, 0, bf0);
     bar();
   };
   if (ABL & 4) {
@@ -727,11 +745,15 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
   // pieces of this lane at once so ONE load latency is exposed instead of one per few pieces inside the
   // store loop (64 VGPRs; the accumulators are dead now).  Issued after the staging writes: hipcc
   // drains vmcnt(0) before the first LDS write (the main loop's LDS-DMA shares the counter).
+  // a half tile has local rows 0..63 only (it < NIT / 2)
   uint4 aux[kReadsAux ? NIT : 1];
   if constexpr (kReadsAux) {
     const uint16_t* src = (EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR) ? R : P;
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) aux[it] = *reinterpret_cast<const uint4*>(src + (size_t)grow_of(it) * ldc + gcol);
+    for (int it = 0; it < NIT; ++it) {   // a half tile re-reads its rows for the unused pieces (no per-load branch)
+      const int itl = half ? (it & (NIT / 2 - 1)) : it;
+      aux[it] = *reinterpret_cast<const uint4*>(src + (size_t)grow_of(itl) * ldc + gcol);
+    }
   }
   float csum[8];
   if constexpr (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL) {
@@ -740,6 +762,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
   }
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
+    if (half && it >= NIT / 2) continue;
     const int lr = it * ROWS_PER_IT + rsub;
     uint4 piece = *reinterpret_cast<const uint4*>(wreg + lr * RS + seg * 16);
     const size_t goff = (size_t)grow_of(it) * ldc + gcol;
@@ -1326,7 +1349,12 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
   const bool srd_ok = (size_t)BM * lda * 2 < (1ull << 31) && (size_t)256 * ldb * 2 < (1ull << 31);
   // v3 (persistent, pipelined across tiles) where the per-tile fixed cost matters: K <= 2304 (+2-6 % at
   // K = 768 / 2304 on the b256 shapes, -1-3 % at K = 3072: tools/gemm_nt3_check.py, profiles/s3_gemm_v3)
-  const bool v3_auto = g_gemm_variant == 0 && K <= 2304;
+  // (and at any K when the half-tile tail applies: at K = 3072 v3 + tail beat v2 + tail by 0.2-2.8 % on two
+  // boxes, profiles/r3_halftail)
+  const int ncu_t = nts_num_cus(), rt_t = grid % ncu_t;
+  const bool tail_t = (g_gemm_stagger & kHalfTail) && EPI != HQ_EPI_DGELU && EPI != HQ_EPI_DMUL && rt_t > 0 &&
+                      2 * rt_t <= ncu_t && grid > ncu_t;
+  const bool v3_auto = g_gemm_variant == 0 && (K <= 2304 || tail_t);
   if (bn == 256 && (g_gemm_variant == 3 || v3_auto) && K >= 2 * BK && srd_ok) {
     constexpr size_t lds = 2 * 2 * 256 * 128 + 64 * 144 + 2 * 256 * 4 + 16;
     static int ncu = [] {
@@ -1351,12 +1379,17 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
       return true;
     }();
     (void)init;
-    if (N / 256 >= 16)
+    if (N / 256 >= 16) {
       hipLaunchKernelGGL((gemm_nt2_kernel<EPI, 24>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, R, part, M, N, K,
                          lda, ldb, ldc, dr);
-    else
-      hipLaunchKernelGGL((gemm_nt2_kernel<EPI, 8>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, R, part, M, N, K,
-                         lda, ldb, ldc, dr);
+    } else {
+      // half-tile tail: rt more blocks, the last 2·rt of them halves of the last rt tiles
+      const int ncu = nts_num_cus(), rt = grid % ncu;
+      const bool ht = (g_gemm_stagger & kHalfTail) && EPI != HQ_EPI_DGELU && EPI != HQ_EPI_DMUL && rt > 0 &&
+                      2 * rt <= ncu && grid > ncu;
+      hipLaunchKernelGGL((gemm_nt2_kernel<EPI, 8>), dim3(ht ? grid + rt : grid), dim3(kThreads), lds, s, A, B, C, bias, P,
+                         R, part, M, N, K, lda, ldb, ldc, dr);
+    }
   } else if (bn == 256) {
     constexpr size_t lds = epi_lds(256);
     static bool init = [] {

@@ -261,13 +261,14 @@ def test_gemm_nt_split_k_low_fill(cuda, M, N, K, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,N,K", [(25600, 768, 768), (25600, 768, 2304), (98304, 768, 768)])
+@pytest.mark.parametrize("M,N,K", [(25600, 768, 768), (25600, 768, 2304), (98304, 768, 768), (25600, 768, 3072),
+                                   (98304, 768, 3072)])
 def test_gemm_nt_half_tile_tail(cuda, M, N, K, variant):
-    """v3's half-tile tail (a last wave of tiles at most half full runs as 128-row half tiles): 300 or 1152
-    256² tiles on 256 CUs.  Every epilogue must be bitwise equal with the tail split on and off (a half tile
-    accumulates its rows in the same order) and match the fp32 reference; DGELU / DMUL never split."""
-    if variant not in (0, 3):
-        pytest.skip("the half-tile tail is a v3 schedule")
+    """The v3 / v2 half-tile tail (a last wave of tiles at most half full runs as 128-row half tiles): 300 or
+    1152 256² tiles on 256 CUs.  Every epilogue must be bitwise equal with the tail split on and off (a half
+    tile accumulates its rows in the same order) and match the fp32 reference; DGELU / DMUL never split."""
+    if variant not in (0, 2, 3):
+        pytest.skip("the half-tile tail is a v2 / v3 schedule")
     EPI_GELUD, EPI_DMUL, EPI_BDR = 5, 6, 7
     HT = 1 << 16
     k = _native.kernels()

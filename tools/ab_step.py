@@ -4,7 +4,7 @@ per-step differences are not swamped by box-to-box variance.  Rounds alternate A
 median ms/step of each.
 
     python tools/ab_step.py --toggle gelu_deriv [--batch 256] [--rounds 4] [--steps 8]
-toggles: gemm_v1 (NT kernel v2 vs v1),
+toggles: gemm_v1 (NT kernel v2 vs v1), halftail (GEMM half-tile tail on / off),
          input_pipeline (on: bench.py's per-step host synthesis + pinned H2D; off: one resident batch)
 """
 import argparse
@@ -41,6 +41,8 @@ def set_toggle(name, on):
         _native.kernels().gemm_set_variant(1 if on else 0)
     elif name == "gemm_v2":   # on: per-tile v2 everywhere; off: auto (persistent v3 for K <= 2304)
         _native.kernels().gemm_set_variant(2 if on else 0)
+    elif name == "halftail":   # on: v2 / v3 half-tile tail (+ v3 at K = 3072 when it applies); off: neither
+        _native.kernels().gemm_set_stagger((1 << 16) if on else 0)
     elif name == "input_pipeline":
         pass
     else:

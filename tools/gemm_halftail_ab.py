@@ -46,7 +46,7 @@ def main():
             kw["resid"] = torch.randn(M, N, device=dev).bfloat16()
         arms = [("v3", 3, 0), ("v3+halftail", 3, HT)]
         if K > 2304:
-            arms.insert(0, ("v2", 2, 0))
+            arms = [("v2", 2, 0), ("v2+halftail", 2, HT)] + arms
         # rows checked: the first 2048 and the last 4096 (the half tiles live in the last wave)
         rows = torch.cat([torch.arange(0, 2048), torch.arange(M - 4096, M)]).to(dev)
         ref = oracle(A, B, epi, kw, rows)
