@@ -1,6 +1,7 @@
 #!/usr/bin/env python
 """In-process interleaved A/B of persistent-GEMM (v3) flag words (gemm_set_stagger: bits 0-7 stagger in
-units of s_sleep(127), bits 8-15 HQ_GEMM_EPIFLAGS diagnostics) on the BERT-base b256 shapes that run on v3.
+units of s_sleep(127), bits 8-15 HQ_GEMM_EPIFLAGS diagnostics, bit 16 the half-tile tail — kept on in every
+arm unless a word sets bit 17, which turns it off) on the BERT-base b256 shapes that run on v3.
 Usage: tools/gemm_knob_ab.py 0 0x2 [...]  (default: 0 vs stagger 2)"""
 import json
 import os
@@ -38,7 +39,7 @@ def main():
         res = {}
         for _ in range(11):
             for w in words:
-                k.gemm_set_stagger(w)
+                k.gemm_set_stagger((w & 0xFFFF) | (0 if w & (1 << 17) else 1 << 16))
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -46,7 +47,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 res.setdefault(w, []).append(e0.elapsed_time(e1) * 1e3)
-        k.gemm_set_stagger(0)
+        k.gemm_set_stagger(1 << 16)
         print(json.dumps({"gemm": name, **{hex(w): round(statistics.median(v), 1) for w, v in res.items()}}), flush=True)
 
 
