@@ -92,8 +92,9 @@ void embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tenso
 // ------------------------------------------------------------------ residual + dropout + LayerNorm
 // With q8 (f32[4] delayed-scaling state of the consuming fp8 GEMM's input): also returns y as e4m3.
 // resid = None: `a` already is z (EPI_BDR GEMM epilogue) -> returns {y, a, mean, rstd} without touching z
+// store_z = false: z is not written (returned empty) — the backward then recomputes x̂ from y (ln_bwd beta=)
 std::vector<Tensor> ln_fwd(Tensor a, c10::optional<Tensor> resid_opt, Tensor gamma, Tensor beta, double eps, double p,
-                           int64_t seed, int64_t opid, c10::optional<Tensor> q8, int64_t phase) {
+                           int64_t seed, int64_t opid, c10::optional<Tensor> q8, int64_t phase, bool store_z) {
   const bool zin = !(resid_opt.has_value() && resid_opt->defined());
   check(a, BF16, "a"); check(gamma, F32, "gamma"); check(beta, F32, "beta");
   if (!zin) check(*resid_opt, BF16, "resid");
@@ -109,11 +110,12 @@ std::vector<Tensor> ln_fwd(Tensor a, c10::optional<Tensor> resid_opt, Tensor gam
   }
   c10::DeviceGuard g(a.device());
   auto y = at::empty_like(a);
-  auto z = zin ? a : at::empty_like(a);
+  const bool wz = zin || store_z;
+  auto z = zin ? a : (store_z ? at::empty_like(a) : at::empty({0}, a.options()));
   auto mean = at::empty({T}, gamma.options()), rstd = at::empty({T}, gamma.options());
   Tensor y8 = want8 ? at::empty({T, H}, a.options().dtype(at::kFloat8_e4m3fn)) : Tensor();
   hq_ln_fwd(ptr<uint16_t>(a), zin ? nullptr : ptr<uint16_t>(*resid_opt), ptr<float>(gamma), ptr<float>(beta),
-            ptr<uint16_t>(y), zin ? nullptr : ptr<uint16_t>(z),
+            ptr<uint16_t>(y), (zin || !wz) ? nullptr : ptr<uint16_t>(z),
             ptr<float>(mean), ptr<float>(rstd), (int)T, (int)H, (float)eps, (float)p, u32(seed), u32(opid), cur_stream(),
             want8 ? reinterpret_cast<uint8_t*>(y8.data_ptr()) : nullptr, want8 ? ptr<float>(*q8) : nullptr,
             (int)(phase % 3));
@@ -125,7 +127,13 @@ std::vector<Tensor> ln_fwd(Tensor a, c10::optional<Tensor> resid_opt, Tensor gam
 std::vector<Tensor> ln_bwd(Tensor dy, c10::optional<Tensor> dy2, Tensor z, Tensor gamma, Tensor mean, Tensor rstd, double p,
                            int64_t seed, int64_t opid, c10::optional<Tensor> g_gamma, c10::optional<Tensor> g_beta,
                            c10::optional<Tensor> g_bias, bool accumulate, c10::optional<Tensor> q8, int64_t phase,
-                           bool write_da) {
+                           bool write_da, c10::optional<Tensor> beta) {
+  // beta given: `z` is the forward OUTPUT y and x̂ = (y − β)/γ (the forward ran with store_z = false)
+  const bool fromy = beta.has_value() && beta->defined();
+  if (fromy) {
+    check(*beta, F32, "beta");
+    TORCH_CHECK(beta->numel() == dy.size(1), "ln_bwd: beta length");
+  }
   check(dy, BF16, "dy"); check_opt(dy2, BF16, "dy2"); check(z, BF16, "z"); check(gamma, F32, "gamma");
   check(mean, F32, "mean"); check(rstd, F32, "rstd");
   check_opt(g_gamma, F32, "g_gamma"); check_opt(g_beta, F32, "g_beta"); check_opt(g_bias, F32, "g_bias");
@@ -151,7 +159,7 @@ std::vector<Tensor> ln_bwd(Tensor dy, c10::optional<Tensor> dy2, Tensor z, Tenso
             ptr<uint16_t>(dz), write_da ? ptr<uint16_t>(da) : nullptr, ptr<float>(part),
             outs4(optr<float>(g_gamma), optr<float>(g_beta), optr<float>(g_bias)), (int)T, (int)H, (float)p, u32(seed),
             u32(opid), accumulate, cur_stream(), want8 ? reinterpret_cast<uint8_t*>(da8.data_ptr()) : nullptr,
-            want8 ? ptr<float>(*q8) : nullptr, (int)(phase % 3));
+            want8 ? ptr<float>(*q8) : nullptr, (int)(phase % 3), fromy ? ptr<float>(*beta) : nullptr);
   if (want8) return {dz, da, da8};
   return {dz, da};
 }
@@ -700,10 +708,11 @@ PYBIND11_MODULE(_hq_kernels, m) {
         py::arg("opid"), py::arg("g_word"), py::arg("g_pos"), py::arg("g_type"), py::arg("g_gamma"), py::arg("g_beta"),
         py::arg("accumulate"), py::arg("pad_word"), py::arg("pad_pos"), py::arg("seq_len") = 0);
   m.def("ln_fwd", &ln_fwd, py::arg("a"), py::arg("resid"), py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("p"),
-        py::arg("seed"), py::arg("opid"), py::arg("q8") = py::none(), py::arg("phase") = 0);
+        py::arg("seed"), py::arg("opid"), py::arg("q8") = py::none(), py::arg("phase") = 0, py::arg("store_z") = true);
   m.def("ln_bwd", &ln_bwd, py::arg("dy"), py::arg("dy2"), py::arg("z"), py::arg("gamma"), py::arg("mean"), py::arg("rstd"),
         py::arg("p"), py::arg("seed"), py::arg("opid"), py::arg("g_gamma"), py::arg("g_beta"), py::arg("g_bias"),
-        py::arg("accumulate"), py::arg("q8") = py::none(), py::arg("phase") = 0, py::arg("write_da") = true);
+        py::arg("accumulate"), py::arg("q8") = py::none(), py::arg("phase") = 0, py::arg("write_da") = true,
+        py::arg("beta") = py::none());
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gemm_nt", &gemm_nt, py::arg("A"), py::arg("B"), py::arg("epi"), py::arg("bias") = py::none(),
         py::arg("pre") = py::none(), py::arg("resid") = py::none(), py::arg("part") = py::none(),

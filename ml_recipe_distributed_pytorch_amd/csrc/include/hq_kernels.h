@@ -30,7 +30,7 @@ void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, con
 void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const float* gamma, const float* mean,
                const float* rstd, uint16_t* dz, uint16_t* da, float* part, HqOuts outs, int T, int H, float p,
                uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s, uint8_t* da8 = nullptr,
-               float* q8 = nullptr, int phase = 0);
+               float* q8 = nullptr, int phase = 0, const float* beta = nullptr);   // beta: z is the output y
 void hq_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww, const uint16_t* wp,
                   const uint16_t* wt, const float* gamma, const float* beta, uint16_t* y, float* mean, float* rstd, int T,
                   int H, float eps, float p, uint32_t seed, uint32_t opid, int V, int P, int NTY, hipStream_t s);

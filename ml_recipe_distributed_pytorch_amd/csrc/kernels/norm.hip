@@ -57,8 +57,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict_
 #pragma unroll
       for (int i = 0; i < 4; ++i) zz[i] = fa[i] * m[i] + fr[i];
       uint2 packed = hq_pack4(zz);
-      *reinterpret_cast<uint2*>(z + base + col) = packed;
-      hq_unpack4(packed, v[c]);  // statistics of the stored (bf16) z, so backward is consistent
+      if (z) *reinterpret_cast<uint2*>(z + base + col) = packed;   // z = null: the backward recomputes x̂ from y
+      hq_unpack4(packed, v[c]);  // statistics of the bf16-rounded z (what a stored z would hold)
 #pragma unroll
       for (int i = 0; i < 4; ++i) sum += v[c][i];
     } else {
@@ -208,14 +208,19 @@ __device__ __forceinline__ void ln_bwd_load(const uint16_t* __restrict__ dy, con
 
 // RPW rows per wave: 8 at large T (partials amortised), 2 for small token counts (T = 1024: 32 blocks of
 // 8-row waves left most CUs idle and each wave latency-bound — see ln_rows_per_wave)
-template <int NCH, int RPW = kRowsPerWave, bool Q8 = false>
+// FROMY ("memory-efficient" LayerNorm backward): the third input is the forward OUTPUT y instead of z, and
+// x̂ = (y − β)/γ = y·(1/γ) − β/γ per column (one FMA) — the forward then never stores z (151 MB per LayerNorm at
+// T = 98304), and rstd is the only row statistic read.  x̂ carries y's bf16 rounding scaled by 1/γ instead of
+// z's.  A column with γ = 0 has no recoverable x̂ (set to 0): its own dz (via x̂·mean(g·γ·x̂)) and γ gradient are
+// then wrong — the limit of every "memory-efficient" LayerNorm; HQ_LN_FROM_Y=0 keeps z for such models.
+template <int NCH, int RPW = kRowsPerWave, bool Q8 = false, bool FROMY = false>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ dy2,
                                                      const uint16_t* __restrict__ z, const float* __restrict__ gamma,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      uint16_t* __restrict__ dz_out, uint16_t* __restrict__ da_out,
                                                      float* __restrict__ part, int T, int H, HqDropKey kd_, uint32_t thr,
                                                      float kscale, uint8_t* __restrict__ da8, const float* __restrict__ q8,
-                                                     float* __restrict__ part8, int phase) {
+                                                     float* __restrict__ part8, int phase, const float* __restrict__ beta) {
   const uint32_t key = kd_.get();
   // Q8 (--precision fp8 backward): da also as e5m2 under the delayed scale of the dgrad GEMM that consumes
   // it (state q8), so that GEMM runs on fp8 operands without a separate quantisation pass
@@ -230,12 +235,21 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[q][c][i] = 0.f;
-  float gam[NCH][4];
+  float gam[NCH][4], ig[FROMY ? NCH : 1][4], nb[FROMY ? NCH : 1][4];
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int col = c * 256 + lane * 4;
     float4 g = col < H ? *reinterpret_cast<const float4*>(gamma + col) : make_float4(0.f, 0.f, 0.f, 0.f);
     gam[c][0] = g.x; gam[c][1] = g.y; gam[c][2] = g.z; gam[c][3] = g.w;
+    if constexpr (FROMY) {
+      const float4 b = col < H ? *reinterpret_cast<const float4*>(beta + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float bb[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ig[c][i] = gam[c][i] != 0.f ? 1.f / gam[c][i] : 0.f;
+        nb[c][i] = -bb[i] * ig[c][i];
+      }
+    }
   }
   const int row0 = blockIdx.x * kWaves * RPW + wave;
   // loads run TWO rows ahead (c = this row, n = next, f = the one after): with one row in flight per
@@ -278,7 +292,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             g[c][i] += f2[i];
-            xh[c][i] = (fz[i] - cmu) * crs;
+            if constexpr (FROMY) xh[c][i] = fmaf(fz[i], ig[c][i], nb[c][i]);
+            else xh[c][i] = (fz[i] - cmu) * crs;
             acc[0][c][i] += g[c][i] * xh[c][i];
             acc[1][c][i] += g[c][i];
             const float dxh = g[c][i] * gam[c][i];
@@ -807,7 +822,8 @@ int hq_embed_bwd_partials(int T, int L) {
 
 void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const float* gamma, const float* mean,
                const float* rstd, uint16_t* dz, uint16_t* da, float* part, HqOuts outs, int T, int H, float p,
-               uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s, uint8_t* da8, float* q8, int phase) {
+               uint32_t seed, uint32_t opid, bool accumulate, hipStream_t s, uint8_t* da8, float* q8, int phase,
+               const float* beta) {
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const HqDropKey key = hq_drop_key(seed, opid);
   const float ks = hq_keep_scale(thr);
@@ -817,14 +833,15 @@ void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const
     constexpr int C = decltype(nch)::value;
     auto go = [&](auto kern) {
       hipLaunchKernelGGL(kern, dim3(nb), dim3(256), 4 * H * sizeof(float), s, dy, dy2, z, gamma, mean, rstd, dz, da, part,
-                         T, H, key, thr, ks, da8, q8, part8, phase);
+                         T, H, key, thr, ks, da8, q8, part8, phase, beta);
     };
+    // beta != null: `z` is the forward output y (FROMY)
     if (ln_rows_per_wave(T) == kRowsPerWave) {
-      if (da8) go(ln_bwd_kernel<C, kRowsPerWave, true>);
-      else go(ln_bwd_kernel<C, kRowsPerWave, false>);
+      if (da8) { if (beta) go(ln_bwd_kernel<C, kRowsPerWave, true, true>); else go(ln_bwd_kernel<C, kRowsPerWave, true, false>); }
+      else { if (beta) go(ln_bwd_kernel<C, kRowsPerWave, false, true>); else go(ln_bwd_kernel<C, kRowsPerWave, false, false>); }
     } else {
-      if (da8) go(ln_bwd_kernel<C, 2, true>);
-      else go(ln_bwd_kernel<C, 2, false>);
+      if (da8) { if (beta) go(ln_bwd_kernel<C, 2, true, true>); else go(ln_bwd_kernel<C, 2, true, false>); }
+      else { if (beta) go(ln_bwd_kernel<C, 2, false, true>); else go(ln_bwd_kernel<C, 2, false, false>); }
     }
   });
   if (da8) hq_fp8_amax_fold(part8, nb * kWaves, q8, phase, s, kHqBf8Max);

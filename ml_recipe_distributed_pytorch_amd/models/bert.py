@@ -191,6 +191,8 @@ class _LayerFn(torch.autograd.Function):
         # e4m3 inputs written here are kept for those weight gradients.
         fp8 = fp8 and ops.fp8_gemm_ok(x.shape[0], 3 * cfg.hidden_size, cfg.hidden_size)
         s8 = m.fp8_states(idx) if fp8 else None
+        # LayerNorm z only when the backward needs it (ops.LN_FROM_Y: recomputed from y on the GPU)
+        keep_z = not (x.is_cuda and ops.LN_FROM_Y)
         if fp8:
             x8 = info.x8.pop(idx, None)
             if x8 is None:
@@ -208,11 +210,11 @@ class _LayerFn(torch.autograd.Function):
                st.view(p + "attention.output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph, info.seed, op0 + 1)
         h1_8 = None
         if fp8:
-            h1, z1, m1, r1, h1_8 = ops.ln_fwd_q8(a1, x, *ln1, s8["ffn1"])
+            h1, z1, m1, r1, h1_8 = ops.ln_fwd_q8(a1, x, *ln1, s8["ffn1"], store_z=keep_z)
         else:   # out-projection + dropout + residual + LayerNorm (one GEMM epilogue + z-in LN under HQ_LN_FUSE=1)
             name = "attention.output.dense"
             h1, z1, m1, r1 = ops.linear_bdr_ln_fwd(ctxv, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), x,
-                                                   kinds[name], *ln1)
+                                                   kinds[name], *ln1, store_z=keep_z)
         act8 = None
         # bf16 act is only read by a bf16 FFN2 weight gradient: skipped (604 MB of stores at b256) when the
         # backward will run that weight gradient in fp8 from act8 (its gradient state calibrated by then)
@@ -231,14 +233,17 @@ class _LayerFn(torch.autograd.Function):
         if act8 is not None:
             a2 = ops.linear_fwd_fp8_own(act8, s8["ffn2"], W8("output.dense"), Bm("output.dense.bias"))
             if idx + 1 < cfg.num_hidden_layers:  # the next layer's QKV input, in e4m3
-                h2, z2, m2, r2, info.x8[idx + 1] = ops.ln_fwd_q8(a2, h1, *ln2, m.fp8_states(idx + 1)["qkv"])
+                h2, z2, m2, r2, info.x8[idx + 1] = ops.ln_fwd_q8(a2, h1, *ln2, m.fp8_states(idx + 1)["qkv"],
+                                                                 store_z=keep_z)
             else:
-                h2, z2, m2, r2 = ops.ln_fwd(a2, h1, *ln2)
+                h2, z2, m2, r2 = ops.ln_fwd(a2, h1, *ln2, store_z=keep_z)
         else:   # FFN2 + dropout + residual + LayerNorm (one GEMM epilogue + z-in LN under HQ_LN_FUSE=1)
             name = "output.dense"
             h2, z2, m2, r2 = ops.linear_bdr_ln_fwd(act, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), h1,
-                                                   kinds[name], *ln2)
-        ctx.save_for_backward(x, key_bias, qkv, ctxv, lse, z1, m1, r1, h1, pre, act, z2, m2, r2)
+                                                   kinds[name], *ln2, store_z=keep_z)
+        # a LayerNorm without z (None) recomputes x̂ from its output y (h1 / h2) in the backward
+        ctx.save_for_backward(x, key_bias, qkv, ctxv, lse, z1, m1, r1, h1, pre, act, z2, m2, r2,
+                              h2 if z2 is None else None)
         # e4m3 inputs of the out-projection / FFN1 / FFN2 GEMMs (their scales stay in the states until the next
         # forward re-quantises), for the fp8 weight gradients
         ctx.f8 = (ctx8, h1_8, act8, x8) if (fp8 and act8 is not None and h1_8 is not None) else None
@@ -248,7 +253,7 @@ class _LayerFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dh2):
-        x, key_bias, qkv, ctxv, lse, z1, m1, r1, h1, pre, act, z2, m2, r2 = ctx.saved_tensors
+        x, key_bias, qkv, ctxv, lse, z1, m1, r1, h1, pre, act, z2, m2, r2, h2 = ctx.saved_tensors
         info = ctx.info
         m = info.model
         cfg = m.config
@@ -301,13 +306,14 @@ class _LayerFn(torch.autograd.Function):
         ctx.f8 = None
 
         # --- FFN block ------------------------------------------------------------------------
-        ln2b = (dh2, None, z2, Wm("output.LayerNorm.weight"), m2, r2, ctx.ph, info.seed, op0 + 2,
-                G("output.LayerNorm.weight"), G("output.LayerNorm.bias"), G("output.dense.bias"), acc)
+        beta2 = Wm("output.LayerNorm.bias") if z2 is None else None   # x̂ from y (no stored z)
+        ln2b = (dh2, None, z2 if z2 is not None else h2, Wm("output.LayerNorm.weight"), m2, r2, ctx.ph, info.seed,
+                op0 + 2, G("output.LayerNorm.weight"), G("output.LayerNorm.bias"), G("output.dense.bias"), acc)
         if fp8:   # bf16 da2 only while its fp8 consumers (FFN2 dgrad + weight gradient) still fall back
             need = not (s8["dffn2"].step >= 1 and (f8 is not None or not trainable))
-            dz2, da2, da2_8 = ops.ln_bwd_q8(*ln2b, s8["dffn2"], need)
+            dz2, da2, da2_8 = ops.ln_bwd_q8(*ln2b, s8["dffn2"], need, beta=beta2)
         else:
-            dz2, da2 = ops.ln_bwd(*ln2b)
+            dz2, da2 = ops.ln_bwd(*ln2b, beta=beta2)
         wgrad(da2, act, G("output.dense.weight"), None, (da2_8, s8["dffn2"], f8[2], s8["ffn2"]) if f8 else None)
         dpre8 = None
         if fp8 and s8["dffn2"].calibrated:
@@ -325,14 +331,15 @@ class _LayerFn(torch.autograd.Function):
         else:
             dh1_ffn = ops.linear_dgrad(dpre, W("intermediate.dense.weight"), wt=WT("intermediate.dense.weight"))
         # --- attention block ------------------------------------------------------------------
-        ln1b = (dz2, dh1_ffn, z1, Wm("attention.output.LayerNorm.weight"), m1, r1, ctx.ph, info.seed, op0 + 1,
-                G("attention.output.LayerNorm.weight"), G("attention.output.LayerNorm.bias"),
+        beta1 = Wm("attention.output.LayerNorm.bias") if z1 is None else None
+        ln1b = (dz2, dh1_ffn, z1 if z1 is not None else h1, Wm("attention.output.LayerNorm.weight"), m1, r1, ctx.ph,
+                info.seed, op0 + 1, G("attention.output.LayerNorm.weight"), G("attention.output.LayerNorm.bias"),
                 G("attention.output.dense.bias"), acc)
         if fp8:   # likewise for the out-projection dgrad + weight gradient
             need = not (s8["dout"].step >= 1 and (f8 is not None or not trainable))
-            dz1, da1, da1_8 = ops.ln_bwd_q8(*ln1b, s8["dout"], need)
+            dz1, da1, da1_8 = ops.ln_bwd_q8(*ln1b, s8["dout"], need, beta=beta1)
         else:
-            dz1, da1 = ops.ln_bwd(*ln1b)
+            dz1, da1 = ops.ln_bwd(*ln1b, beta=beta1)
         wgrad(da1, ctxv, G("attention.output.dense.weight"), None,
               (da1_8, s8["dout"], f8[0], s8["out"]) if f8 else None)
         if fp8 and s8["dout"].calibrated:

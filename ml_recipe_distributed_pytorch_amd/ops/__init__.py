@@ -43,33 +43,46 @@ def embed_bwd(dy, ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, mean, rs
 
 
 # ------------------------------------------------------------------ residual + dropout + LayerNorm
-def ln_fwd(a, resid, gamma, beta, eps, p, seed, opid):
+def _z_or_none(out):
+    """ln_fwd's z slot: None when the kernel did not store it (store_z=False)."""
+    out = list(out)
+    if out[1] is not None and out[1].numel() == 0:
+        out[1] = None
+    return tuple(out)
+
+
+def ln_fwd(a, resid, gamma, beta, eps, p, seed, opid, store_z: bool = True):
+    """(y, z, mean, rstd).  ``store_z=False`` (GPU): z is not written and comes back None — the backward then
+    recomputes x̂ from y (``ln_bwd(..., beta=β)`` with y in z's place), one 2-byte/element store less."""
     if a.is_cuda:
-        return tuple(_k().ln_fwd(a, resid, gamma, beta, float(eps), float(p), int(seed), int(opid)))
+        return _z_or_none(_k().ln_fwd(a, resid, gamma, beta, float(eps), float(p), int(seed), int(opid),
+                                      store_z=bool(store_z)))
     return ref.ln_fwd(a, resid, gamma, beta, eps, p, seed, opid)
 
 
-def ln_fwd_q8(a, resid, gamma, beta, eps, p, seed, opid, state: "Fp8DelayedState"):
+def ln_fwd_q8(a, resid, gamma, beta, eps, p, seed, opid, state: "Fp8DelayedState", store_z: bool = True):
     """``ln_fwd`` that also writes y in e4m3 under ``state`` — the delayed-scaling state of the fp8 GEMM
     that consumes y — so that GEMM needs no separate quantisation pass: (y, z, mean, rstd, y8)."""
-    return tuple(_k().ln_fwd(a, resid, gamma, beta, float(eps), float(p), int(seed), int(opid), q8=state.buf,
-                             phase=state.next_phase()))
+    return _z_or_none(_k().ln_fwd(a, resid, gamma, beta, float(eps), float(p), int(seed), int(opid), q8=state.buf,
+                                  phase=state.next_phase(), store_z=bool(store_z)))
 
 
-def ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate):
+def ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate, beta=None):
+    """(dz, da).  ``beta`` given: ``z`` is the forward output y and x̂ = (y − β)/γ."""
     if dy.is_cuda:
         return tuple(_k().ln_bwd(dy, dy2, z, gamma, mean, rstd, float(p), int(seed), int(opid),
-                                 g_gamma, g_beta, g_bias, bool(accumulate)))
-    return ref.ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate)
+                                 g_gamma, g_beta, g_bias, bool(accumulate), beta=beta))
+    return ref.ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate, beta=beta)
 
 
 def ln_bwd_q8(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate,
-              state: "Fp8DelayedState", need_da: bool = True):
+              state: "Fp8DelayedState", need_da: bool = True, beta=None):
     """``ln_bwd`` that also writes da in e5m2 under ``state`` — the delayed-scaling state of the fp8 dgrad
     GEMM that consumes da: (dz, da, da8); ``need_da=False`` (every consumer reads da8) skips the bf16 da
     (returned as None)."""
     dz, da, da8 = _k().ln_bwd(dy, dy2, z, gamma, mean, rstd, float(p), int(seed), int(opid), g_gamma, g_beta, g_bias,
-                              bool(accumulate), q8=state.buf, phase=state.next_phase(), write_da=bool(need_da))
+                              bool(accumulate), q8=state.buf, phase=state.next_phase(), write_da=bool(need_da),
+                              beta=beta)
     return dz, (da if need_da else None), da8
 
 
@@ -143,6 +156,10 @@ _EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID, _EPI_GELUD, _EPI_DMUL, 
 # result.  Off by default: the epilogue's residual read and dropout hash are serial with the persistent GEMM's
 # MFMA work and cost what the LayerNorm saves (same-box step A/B 3847 vs 3839 samples/s, profiles/r2_ln_fuse)
 LN_FUSE = os.environ.get("HQ_LN_FUSE", "0") == "1"
+# The encoder LayerNorms' forward skips storing z (151 MB per LayerNorm at B = 256, L = 384) and the backward
+# recomputes x̂ = (y − β)/γ from the output y, which the next sublayer keeps anyway (the "memory-efficient"
+# LayerNorm backward).  HQ_LN_FROM_Y=0 keeps z (x̂ = (z − mean)·rstd, the exact-input form).
+LN_FROM_Y = os.environ.get("HQ_LN_FROM_Y", "1") == "1"
 
 
 def _check_nt(M: int, N: int, K: int, what: str):
@@ -169,7 +186,7 @@ def linear_fwd(x, w, b, b32=None, kind: str = "plain"):
     return ref.linear_fwd(x, w, b)
 
 
-def linear_bdr_ln_fwd(x, w, b, b32, resid, kind, gamma, beta, eps, p, seed, opid):
+def linear_bdr_ln_fwd(x, w, b, b32, resid, kind, gamma, beta, eps, p, seed, opid, store_z: bool = True):
     """LayerNorm(dropout_p(x·Wᵀ + b) + resid) -> (y, z, mean, rstd), bitwise what ``linear_fwd`` followed by
     ``ln_fwd`` computes.  On the GPU with ``HQ_LN_FUSE=1`` the GEMM's EPI_BDR epilogue adds the dropped-out
     projection to the residual and stores z, and the LayerNorm reads z alone (``ln_fwd`` with resid=None);
@@ -178,7 +195,7 @@ def linear_bdr_ln_fwd(x, w, b, b32, resid, kind, gamma, beta, eps, p, seed, opid
         _check_nt(x.shape[0], w.shape[0], x.shape[1], f"linear_bdr_ln_fwd[{kind}]")
         z = _k().gemm_nt(x, w, _EPI_BDR, bias=_bias32(b, b32), resid=resid, p=float(p), seed=int(seed), opid=int(opid))
         return tuple(_k().ln_fwd(z, None, gamma, beta, float(eps), 0.0, 0, 0))
-    return ln_fwd(linear_fwd(x, w, b, b32, kind), resid, gamma, beta, eps, p, seed, opid)
+    return ln_fwd(linear_fwd(x, w, b, b32, kind), resid, gamma, beta, eps, p, seed, opid, store_z=store_z)
 
 
 def linear_fwd_fp8(x, w8s, b):

@@ -93,12 +93,18 @@ def ln_fwd(a, resid, gamma, beta, eps, p, seed, opid):
     return y.to(a.dtype), z.to(a.dtype), mean, rstd
 
 
-def ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate: bool):
-    """Returns (dz, da): dz = dL/dz (residual grad), da = dropout_bwd(dz) (GEMM-output grad)."""
+def ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate: bool, beta=None):
+    """Returns (dz, da): dz = dL/dz (residual grad), da = dropout_bwd(dz) (GEMM-output grad).  With ``beta``,
+    ``z`` is the forward output y and x̂ = (y − β)/γ (0 where γ = 0), as the GPU kernel's FROMY form."""
     g = dy.float()
     if dy2 is not None:
         g = g + dy2.float()
-    xhat = (z.float() - mean[:, None]) * rstd[:, None]
+    if beta is not None:
+        gf = gamma.float()
+        ig = torch.where(gf != 0, 1.0 / gf, torch.zeros_like(gf))
+        xhat = z.float() * ig[None] - (beta.float() * ig)[None]
+    else:
+        xhat = (z.float() - mean[:, None]) * rstd[:, None]
     _acc(g_gamma, (g * xhat).sum(0), accumulate)
     _acc(g_beta, g.sum(0), accumulate)
     dz = _ln_bwd_core(g, xhat, gamma, rstd)

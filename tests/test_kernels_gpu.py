@@ -52,6 +52,46 @@ def test_ln_fwd_bwd(cuda, H, p):
             _close(gg[i], ggr[i], 5e-2, 1e-3, n)
 
 
+@pytest.mark.parametrize("H,T", [(768, 1000), (768, 24576), (1024, 1000)])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_ln_bwd_from_y(cuda, H, T, p):
+    """Memory-efficient LayerNorm: the forward with store_z=False writes no z and the backward recomputes
+    x̂ = (y − β)/γ from the output (beta=).  Against the CPU form of the same recompute (ref.ln_bwd(beta=)) and
+    against the exact-input fp32 oracle (x̂ from z) at the bf16-gradient tolerance; y / mean / rstd are
+    bitwise those of the z-storing forward.  A γ = 0 column gets x̂ = 0 (its x̂ is not recoverable from y), so its
+    own dz and γ gradient are excluded from the exact-input comparison — the documented limit of this form."""
+    k = _native.kernels()
+    torch.manual_seed(1)
+    a, r = _bf(torch.randn(T, H)), _bf(torch.randn(T, H))
+    # γ in [0.5, 1.5) (x̂'s error from y's bf16 rounding grows as |β/γ| + |x̂| over 2⁹), plus one γ = 0 column
+    gamma, beta = torch.rand(H) + 0.5, torch.randn(H) * 0.1
+    gamma[5] = 0.0
+    y, z, m, rs = k.ln_fwd(a.to(cuda), r.to(cuda), gamma.to(cuda), beta.to(cuda), 1e-12, p, 99, 4)
+    y2, z2, m2, rs2 = k.ln_fwd(a.to(cuda), r.to(cuda), gamma.to(cuda), beta.to(cuda), 1e-12, p, 99, 4, store_z=False)
+    assert z2.numel() == 0
+    assert torch.equal(y, y2) and torch.equal(m, m2) and torch.equal(rs, rs2)
+    dy, dy2 = _bf(torch.randn(T, H)), _bf(torch.randn(T, H))
+    gg = [torch.zeros(H, device=cuda) for _ in range(3)]
+    ggy = [torch.zeros(H) for _ in range(3)]
+    ggz = [torch.zeros(H) for _ in range(3)]
+    dz, da = k.ln_bwd(dy.to(cuda), dy2.to(cuda), y2, gamma.to(cuda), m2, rs2, p, 99, 4, gg[0], gg[1], gg[2], False,
+                      beta=beta.to(cuda))
+    dzy, day = ref.ln_bwd(dy, dy2, y2.cpu(), gamma, m2.cpu(), rs2.cpu(), p, 99, 4, ggy[0], ggy[1], ggy[2], False,
+                          beta=beta)
+    dzz, daz = ref.ln_bwd(dy, dy2, z.cpu(), gamma, m.cpu(), rs.cpu(), p, 99, 4, ggz[0], ggz[1], ggz[2], False)
+    _close(dz, dzy, 3e-2, 2e-2, "dz vs the same recompute")
+    _close(da, day, 3e-2, 2e-2, "da vs the same recompute")
+    # a γ = 0 column's x̂ cannot be recovered from y: its own dz (through x̂·mean(g·γ·x̂)) and γ gradient differ
+    # from the exact-input form by construction; every other column must agree
+    keep = torch.arange(H) != 5
+    _close(dz[:, keep.to(cuda)], dzz[:, keep], 5e-2, 3e-2, "dz vs the exact-input oracle")
+    for i, n in enumerate(["dgamma", "dbeta", "dbias"]):
+        _close(gg[i], ggy[i], 5e-2 * (T / 1000) ** 0.5, 1e-3, n)
+    # Σ_t g·x̂ over T rows: y's bf16 rounding in x̂ is a random walk of ~2⁻⁹ per row (0.3-0.6 % of dγ at T = 24576)
+    _close(gg[0][keep.to(cuda)], ggz[0][keep], 0.5 * (T / 1000) ** 0.5, 1e-2, "dgamma vs the exact-input oracle")
+    _close(gg[1], ggz[1], 5e-2 * (T / 1000) ** 0.5, 1e-3, "dbeta vs the exact-input oracle")
+
+
 @pytest.mark.parametrize("H,ntypes", [(768, 2), (128, 1)])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("layout", ["flat", "seq", "seq_randpos"])
