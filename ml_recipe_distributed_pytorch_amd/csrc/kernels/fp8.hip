@@ -1,9 +1,9 @@
-// OCP fp8 (e4m3fn) quantisation for the --precision fp8 forward projections (torch._scaled_mm →
-// hipBLASLt fp8 MFMA at 2x the bf16 rate on gfx950).  Current (just-in-time) per-tensor scaling,
-// with no host synchronisation:
+// OCP fp8 (e4m3fn) quantisation passes for --precision fp8 (the standalone form: the training step's fp8
+// inputs are written by their producers under delayed scaling; the GEMMs are gemm_fp8.hip's own block-scaled
+// MFMA kernels).  Current (just-in-time) per-tensor scaling, with no host synchronisation:
 //   hq_amax_bf16 : amax = max |x|                          (grid-wide max via float-as-uint atomics)
-//   hq_fp8_quant : y = sat(x · 448 / amax) → e4m3fn,  scale = amax / 448 (the dequant factor that
-//                  _scaled_mm multiplies back in), both read from / written to device memory.
+//   hq_fp8_quant : y = sat(x · 448 / amax) → e4m3fn,  scale = amax / 448 (the dequant factor the fp8 GEMM
+//                  multiplies back in), both read from / written to device memory.
 // v_cvt_pk_fp8_f32 converts two f32 to OCP e4m3 on gfx950; inputs are clamped to ±448 first so an
 // out-of-range value saturates instead of becoming NaN (e4m3fn has no infinity).
 #include "hq_common.h"
