@@ -20,109 +20,65 @@ namespace {
 constexpr int kRowsPerWave = 8;   // rows a wave walks in the backward kernels
 constexpr int kWaves = 4;         // 256-thread blocks
 
+// LayerNorm forward, RPW rows per wave.  RES = true: z = dropout(a) + resid (rounded to bf16, as HF under
+// autocast; stored only when z != null — the backward recomputes x̂ from y) ; y = LN(z).  RES = false: y =
+// LN(z) where z was already written by the producing GEMM's EPI_BDR epilogue (out-projection / FFN2).
+// Each wave issues all its rows' loads before the first reduction: one row per wave was latency-bound
+// (88.7 µs at T = 98304 with RES, 5.1 TB/s over its three streams; RPW = 2: 77.7 µs, 5.8 TB/s; RPW = 4
+// 84.0 µs — profiles/r3_ln_rpw).
 // Q8 (--precision fp8): y is also written as e4m3 under the delayed scale of the consuming GEMM's input
-// state q8 (the next QKV / FFN1 projection reads it instead of a separate quantisation pass over y).
-// Each wave walks q8_rows rows; its amax goes to a partial slot that hq_fp8_amax_fold reduces (no
-// same-address atomics: those serialise in one L2 channel — a per-block filtered atomic still cost
-// +27 µs at T = 98304, a per-wave one +97 µs).
-template <int NCH, bool Q8>
-__global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict__ a, const uint16_t* __restrict__ resid,
-                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                     uint16_t* __restrict__ y, uint16_t* __restrict__ z,
-                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out, int T,
-                                                     int H, float eps, HqDropKey kd_, uint32_t thr, float kscale,
-                                                     uint8_t* __restrict__ y8, const float* __restrict__ q8,
-                                                     float* __restrict__ part8, int phase) {
-  const uint32_t key = kd_.get();
+// state q8 (the next QKV / FFN1 projection reads it instead of a separate quantisation pass over y).  Each
+// wave's amax goes to a partial slot that hq_fp8_amax_fold reduces (no same-address atomics: those
+// serialise in one L2 channel — a per-block filtered atomic cost +27 µs at T = 98304, a per-wave one +97).
+template <int NCH, int RPW, bool RES, bool Q8 = false>
+__global__ __launch_bounds__(256) void ln_fwd_rows_kernel(const uint16_t* __restrict__ zin, const uint16_t* __restrict__ resid,
+                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                          uint16_t* __restrict__ y, uint16_t* __restrict__ z,
+                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out, int T,
+                                                          int H, float eps, HqDropKey kd_, uint32_t thr, float kscale,
+                                                          uint8_t* __restrict__ y8, const float* __restrict__ q8,
+                                                          float* __restrict__ part8, int phase) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  float amax = 0.f, inv8 = 1.f, s8 = 1.f;
-  if constexpr (Q8) {
-    s8 = hq_fp8_delayed_scale(q8, phase);
-    inv8 = 1.f / s8;
-  }
-  const int stride = gridDim.x * kWaves;
-  for (int row = blockIdx.x * kWaves + wave; row < T; row += stride) {
-  const size_t base = (size_t)row * H;
-  float v[NCH][4];
-  float sum = 0.f;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int col = c * 256 + lane * 4;
-    if (col < H) {
-      float fa[4], fr[4], m[4] = {1.f, 1.f, 1.f, 1.f};
-      hq_unpack4(*reinterpret_cast<const uint2*>(a + base + col), fa);
-      hq_unpack4(*reinterpret_cast<const uint2*>(resid + base + col), fr);
-      if (thr) hq_keep4((uint32_t)(base + col), key, thr, kscale, m);
-      float zz[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) zz[i] = fa[i] * m[i] + fr[i];
-      uint2 packed = hq_pack4(zz);
-      if (z) *reinterpret_cast<uint2*>(z + base + col) = packed;   // z = null: the backward recomputes x̂ from y
-      hq_unpack4(packed, v[c]);  // statistics of the bf16-rounded z (what a stored z would hold)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) sum += v[c][i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[c][i] = 0.f;
-    }
-  }
-  const float mean = hq_wave_sum(sum) / H;
-  float sq = 0.f;
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int col = c * 256 + lane * 4;
-    if (col < H) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) { float d = v[c][i] - mean; sq += d * d; }
-    }
-  }
-  const float rstd = rsqrtf(hq_wave_sum(sq) / H + eps);
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int col = c * 256 + lane * 4;
-    if (col < H) {
-      const float4 g = *reinterpret_cast<const float4*>(gamma + col);
-      const float4 b = *reinterpret_cast<const float4*>(beta + col);
-      float o[4] = {(v[c][0] - mean) * rstd * g.x + b.x, (v[c][1] - mean) * rstd * g.y + b.y,
-                    (v[c][2] - mean) * rstd * g.z + b.z, (v[c][3] - mean) * rstd * g.w + b.w};
-      const uint2 packed = hq_pack4(o);
-      *reinterpret_cast<uint2*>(y + base + col) = packed;
-      if constexpr (Q8) {
-        hq_unpack4(packed, o);   // quantise the bf16-rounded y, exactly what the bf16 copy holds
-#pragma unroll
-        for (int i = 0; i < 4; ++i) amax = fmaxf(amax, fabsf(o[i]));
-        *reinterpret_cast<uint32_t*>(y8 + base + col) = hq_pack_fp8x4(o, inv8);
-      }
-    }
-  }
-  if (lane == 0) { mean_out[row] = mean; rstd_out[row] = rstd; }
-  }
-  if constexpr (Q8) {   // this wave's amax -> its own partial slot (hq_fp8_amax_fold reduces them)
-    amax = hq_wave_max(amax);
-    if (lane == 0) part8[blockIdx.x * kWaves + wave] = amax;
-  }
-}
-
-// y = LN(z) where z = dropout(a) + resid was already written by the producing GEMM's EPI_BDR epilogue
-// (out-projection / FFN2): one read stream and one write stream instead of ln_fwd_kernel's two + two.  With
-// half the bytes per row a wave keeps RPW rows' loads in flight together (one row per wave left it
-// latency-bound: 75 µs at T = 98304 vs ~50 µs of HBM time).  Same statistics and rounding as ln_fwd_kernel.
-template <int NCH, int RPW>
-__global__ __launch_bounds__(256) void ln_fwd_z_kernel(const uint16_t* __restrict__ zin, const float* __restrict__ gamma,
-                                                       const float* __restrict__ beta, uint16_t* __restrict__ y,
-                                                       float* __restrict__ mean_out, float* __restrict__ rstd_out, int T,
-                                                       int H, float eps) {
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float amax = 0.f, inv8 = 1.f;
+  if constexpr (Q8) inv8 = 1.f / hq_fp8_delayed_scale(q8, phase);
   const int row0 = (blockIdx.x * kWaves + wave) * RPW;
-  float v[RPW][NCH][4];
+  uint2 ra[RPW][NCH], rr[RES ? RPW : 1][NCH];
 #pragma unroll
   for (int r = 0; r < RPW; ++r)
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = c * 256 + lane * 4;
-      if (row0 + r < T && col < H) hq_unpack4(*reinterpret_cast<const uint2*>(zin + (size_t)(row0 + r) * H + col), v[r][c]);
-      else v[r][c][0] = v[r][c][1] = v[r][c][2] = v[r][c][3] = 0.f;
+      const bool ok = row0 + r < T && col < H;
+      const size_t off = (size_t)(row0 + r) * H + col;
+      ra[r][c] = ok ? *reinterpret_cast<const uint2*>(zin + off) : make_uint2(0u, 0u);
+      if constexpr (RES) rr[r][c] = ok ? *reinterpret_cast<const uint2*>(resid + off) : make_uint2(0u, 0u);
     }
+  float v[RPW][NCH][4];
+  if constexpr (RES) {
+    const uint32_t key = kd_.get();
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int col = c * 256 + lane * 4;
+        const size_t off = (size_t)(row0 + r) * H + col;
+        float fa[4], fr[4], m[4] = {1.f, 1.f, 1.f, 1.f};
+        hq_unpack4(ra[r][c], fa);
+        hq_unpack4(rr[r][c], fr);
+        if (thr) hq_keep4((uint32_t)off, key, thr, kscale, m);
+        float zz[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) zz[i] = fa[i] * m[i] + fr[i];
+        const uint2 packed = hq_pack4(zz);
+        if (z && row0 + r < T && col < H) *reinterpret_cast<uint2*>(z + off) = packed;
+        hq_unpack4(packed, v[r][c]);   // statistics of the bf16-rounded z
+      }
+  } else {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) hq_unpack4(ra[r][c], v[r][c]);
+  }
   float mean[RPW], rstd[RPW];
 #pragma unroll
   for (int r = 0; r < RPW; ++r) {
@@ -157,7 +113,14 @@ __global__ __launch_bounds__(256) void ln_fwd_z_kernel(const uint16_t* __restric
         if (row0 + r < T) {
           float o[4] = {(v[r][c][0] - mean[r]) * rstd[r] * g.x + b.x, (v[r][c][1] - mean[r]) * rstd[r] * g.y + b.y,
                         (v[r][c][2] - mean[r]) * rstd[r] * g.z + b.z, (v[r][c][3] - mean[r]) * rstd[r] * g.w + b.w};
-          *reinterpret_cast<uint2*>(y + (size_t)(row0 + r) * H + col) = hq_pack4(o);
+          const uint2 packed = hq_pack4(o);
+          *reinterpret_cast<uint2*>(y + (size_t)(row0 + r) * H + col) = packed;
+          if constexpr (Q8) {
+            hq_unpack4(packed, o);   // quantise the bf16-rounded y, exactly what the bf16 copy holds
+#pragma unroll
+            for (int i = 0; i < 4; ++i) amax = fmaxf(amax, fabsf(o[i]));
+            *reinterpret_cast<uint32_t*>(y8 + (size_t)(row0 + r) * H + col) = hq_pack_fp8x4(o, inv8);
+          }
         }
       }
     }
@@ -166,6 +129,10 @@ __global__ __launch_bounds__(256) void ln_fwd_z_kernel(const uint16_t* __restric
 #pragma unroll
     for (int r = 0; r < RPW; ++r)
       if (row0 + r < T) { mean_out[row0 + r] = mean[r]; rstd_out[row0 + r] = rstd[r]; }
+  }
+  if constexpr (Q8) {   // this wave's amax -> its own partial slot
+    amax = hq_wave_max(amax);
+    if (lane == 0) part8[blockIdx.x * kWaves + wave] = amax;
   }
 }
 
@@ -787,27 +754,31 @@ void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, con
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const HqDropKey key = hq_drop_key(seed, opid);
   const float ks = hq_keep_scale(thr);
-  const int blocks = (T + kWaves - 1) / kWaves;
-  static const int q8_rows = [] {   // rows per wave of the e4m3 variant (HQ_LNQ8_ROWS: A/B sweeps)
-    const char* e = getenv("HQ_LNQ8_ROWS");
-    return e ? std::max(1, atoi(e)) : 4;
+  static const int rpw = [] {   // rows per wave (HQ_LN_RPW = 1 / 2 / 4: A/B sweeps)
+    const char* e = getenv("HQ_LN_RPW");
+    const int v = e ? atoi(e) : 2;
+    return v == 1 || v == 4 ? v : 2;
   }();
+  const int grid = (T + kWaves * rpw - 1) / (kWaves * rpw);
+  float* part8 = y8 ? hq_fp8_amax_parts((size_t)grid * kWaves) : nullptr;
   dispatch_nch(H, [&](auto nch) {
-    if (y8) {
-      const int g8 = (T + q8_rows * kWaves - 1) / (q8_rows * kWaves);
-      float* part8 = hq_fp8_amax_parts((size_t)g8 * kWaves);
-      hipLaunchKernelGGL((ln_fwd_kernel<decltype(nch)::value, true>), dim3(g8), dim3(256), 0, s, a, resid, gamma, beta,
-                         y, z, mean, rstd, T, H, eps, key, thr, ks, y8, q8, part8, phase);
-      hq_fp8_amax_fold(part8, g8 * kWaves, q8, phase, s);
-    } else if (!resid) {   // z-in: a = z from an EPI_BDR GEMM epilogue
-      constexpr int RPW = 2;
-      hipLaunchKernelGGL((ln_fwd_z_kernel<decltype(nch)::value, RPW>), dim3((T + kWaves * RPW - 1) / (kWaves * RPW)),
-                         dim3(256), 0, s, a, gamma, beta, y, mean, rstd, T, H, eps);
-    } else {
-      hipLaunchKernelGGL((ln_fwd_kernel<decltype(nch)::value, false>), dim3(blocks), dim3(256), 0, s, a, resid, gamma,
-                         beta, y, z, mean, rstd, T, H, eps, key, thr, ks, nullptr, nullptr, nullptr, 0);
-    }
+    constexpr int C = decltype(nch)::value;
+    auto go = [&](auto R, auto res, auto q) {
+      hipLaunchKernelGGL((ln_fwd_rows_kernel<C, decltype(R)::value, decltype(res)::value, decltype(q)::value>),
+                         dim3(grid), dim3(256), 0, s, a, resid, gamma, beta, y, z, mean, rstd, T, H, eps, key, thr, ks,
+                         y8, q8, part8, phase);
+    };
+    auto by_rows = [&](auto res, auto q) {
+      if (rpw == 1) go(std::integral_constant<int, 1>{}, res, q);
+      else if (rpw == 4) go(std::integral_constant<int, 4>{}, res, q);
+      else go(std::integral_constant<int, 2>{}, res, q);
+    };
+    // resid == null: a = z from an EPI_BDR GEMM epilogue
+    if (y8) { if (resid) by_rows(std::true_type{}, std::true_type{}); else by_rows(std::false_type{}, std::true_type{}); }
+    else if (resid) by_rows(std::true_type{}, std::false_type{});
+    else by_rows(std::false_type{}, std::false_type{});
   });
+  if (y8) hq_fp8_amax_fold(part8, grid * kWaves, q8, phase, s);
 }
 
 static int ln_rows_per_wave(int T) { return T >= 16384 ? kRowsPerWave : 2; }

@@ -101,7 +101,7 @@ def test_fp8_quant_delayed(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("T,H", [(1024, 768), (98304, 768), (1000, 1024)])
+@pytest.mark.parametrize("T,H", [(1024, 768), (98304, 768), (1000, 1024), (1003, 768), (5, 768)])
 def test_ln_fwd_fp8_output(cuda, T, H):
     """LayerNorm forward with the e4m3 copy of y for the next fp8 GEMM (producer-side quantisation): the
     bf16 outputs equal the plain kernel's bitwise, y8 = e4m3(bf16(y) / s) under the delayed scale, and the
