@@ -2,7 +2,8 @@
 """Headline benchmark: whole-node training samples/s, BERT-base QA fine-tuning at seq=384, bf16.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 it is launched by
-``torch.distributed.run`` (one rank per GPU, RCCL over xGMI).  Each timed step is a complete
+``torch.distributed.run`` (one rank per GPU, RCCL over xGMI) — and if it is not, it launches that N-rank job
+itself as a child process (``self_launch``); a job whose size differs from ``--gpus`` exits non-zero.  Each timed step is a complete
 optimizer step of the recipe's training loop (``config/test_bert.cfg`` loss/optimizer settings):
 host batch synthesis (native dummy-QA generator, pinned) → H2D → fused BERT-base forward →
 5-way QA loss → backward with bucketed RCCL all-reduce overlapped → on-device grad-norm clip →
@@ -70,8 +71,44 @@ def parse():
     return ap.parse_args()
 
 
+def selflaunch_cmd(argv, nproc: int, port: int):
+    """The N-rank job ``python bench.py --gpus N`` starts for itself when no launcher set RANK: the driver's
+    own form, ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
+    --master-port P bench.py <same args>``, one rank per GPU over RCCL."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args, argv):
+    """``--gpus N`` (N > 1) without a launcher: check that N GPUs are visible, then run the N-rank job as a
+    CHILD process (no exec: nothing here has touched the GPU — ``device_count`` does not initialise HIP) and
+    return its exit status.  None when this process is a rank (RANK set) or N == 1."""
+    if args.gpus <= 1 or "RANK" in os.environ:
+        return None
+    import subprocess
+    import torch
+    visible = torch.cuda.device_count()
+    if visible < args.gpus:
+        print(f"[bench] error: --gpus {args.gpus} requested but only {visible} GPU(s) are visible; refusing to "
+              "report a smaller job under that label", file=sys.stderr, flush=True)
+        return 2
+    cmd = selflaunch_cmd(argv, args.gpus, _free_port())
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    rc = self_launch(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     if os.environ.get("HQ_HANG_DUMP_S"):   # hang diagnosis: every rank dumps its Python stacks and exits
         import faulthandler
         faulthandler.dump_traceback_later(float(os.environ["HQ_HANG_DUMP_S"]), exit=True)
@@ -99,6 +136,11 @@ def main():
     # schedule, barrier, all_reduce(MAX), destroy).  Plain `python bench.py` (the driver's N=1 run) has none.
     launched = hqdist.env_launched()
     backend = None
+    if launched and os.environ.get("HQ_BENCH_BACKEND", "nccl") == "nccl":
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+        if torch.cuda.device_count() < local:
+            raise SystemExit(f"[bench] error: {local} ranks on this node but only {torch.cuda.device_count()} "
+                             "GPU(s) visible (RCCL needs one GPU per rank)")
     if launched:
         # HQ_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with every rank on cuda:0 (one-GPU box; gloo
         # all-reduces the CUDA buckets through host memory) — never for a measurement
@@ -110,8 +152,8 @@ def main():
     else:
         rank, device = 0, torch.device("cuda", 0)
         torch.cuda.set_device(device)
-    if world != args.gpus and rank == 0:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:   # never report an N-GPU label for a different job size
+        raise SystemExit(f"[bench] error: --gpus {args.gpus} but the job has {world} rank(s)")
 
     cfg = get_config(args.model)
     model = BertForQuestionAnswering(cfg, seed=1234, precision=args.precision).to(device).train()
@@ -218,6 +260,8 @@ def main():
            "graph_replays": engine.graph_replays,
            "reducer": reducer.kind if reducer is not None else "none",
            "reducer_buckets": reducer.n_buckets if reducer is not None else 0,
+           "uid_via_store": reducer.uid_via_store if reducer is not None else None,
+           "broadcast_done": reducer.broadcast_done if reducer is not None else None,
            "gemm_sched": reducer.gemm_sched if reducer is not None else "static",
            "comm_wait_ms": round(comm["comm_wait_ms"], 3) if "comm_wait_ms" in comm else None,
            "comm_span_ms": round(comm["comm_span_ms"], 3) if "comm_span_ms" in comm else None,

@@ -6,9 +6,9 @@ constant labels ``start_id=0, end_id=L-1, label_id=0 ('yes'), start_position=0, 
 
 The reference builds items one by one in Python (0.34–0.47 ms/sample/core).  Here:
 * ``DummyDataset.__getitems__`` (torch ≥ 2 batched fetch) synthesises a whole collated batch with
-  vectorised numpy, and
+  vectorised numpy — the path the ``Trainer`` takes (CPU and GPU, through its DataLoader), and
 * ``synth_batch_native`` uses the C++ generator in ``_hq_host`` (multi-threaded, writes straight
-  into pinned tensors) — the path ``bench.py`` and the GPU trainer use.
+  into pinned tensors) — the path ``bench.py`` and ``smoke()`` use.
 Both draw the same distribution; neither needs a vocab file (special ids come from the tokenizer
 or the model preset).
 """

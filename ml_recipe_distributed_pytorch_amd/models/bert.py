@@ -284,7 +284,10 @@ class _LayerFn(torch.autograd.Function):
                     ops.linear_wgrad_fp8(q[0], q[1], q[2], q[3], gw, acc)
                 else:
                     ops.linear_wgrad(dy, xin, gw, gb, acc)
-            if side is None:
+            if side is None or use8:
+                # fp8 runs on the compute stream: the kernel reads the delayed-scaling scale words (state buf[3])
+                # when it executes, and the next micro-batch's forward producers rewrite them on this stream —
+                # record_stream protects the operands' memory, not those values
                 run()
                 return
             side.wait_stream(torch.cuda.current_stream())

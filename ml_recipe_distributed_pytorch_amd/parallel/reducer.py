@@ -74,6 +74,8 @@ class GradReducer:
         self.group_to_bucket: Dict[str, Bucket] = {}
         self._native = None
         self._scratch = None
+        self.uid_via_store = False
+        self.broadcast_done = False
         self.stats = {"buckets_launched": 0, "bytes": 0}
         self._seq_hash = 0       # running hash of the (bucket, numel) launch sequence (SURVEY §5.2 checker)
         on_gpu = self.store.device.type == "cuda"
@@ -103,7 +105,10 @@ class GradReducer:
         self._build_buckets()
         model.set_grad_listener(self._on_group_ready)
         self.gemm_sched = self._pick_gemm_sched(on_gpu)
-        if self.world > 1 and broadcast_params:
+        # DDP-constructor broadcast whenever a process group exists (any world size: a 1-rank
+        # torchrun rehearsal runs the same native ncclBroadcast an 8-GPU job does) or the reducer is forced
+        self.broadcast_done = False
+        if broadcast_params and (self.world > 1 or (self.force and (dist.is_initialized() or self._native is not None))):
             self.broadcast_parameters()
 
     # ------------------------------------------------------------------ setup
@@ -123,16 +128,20 @@ class GradReducer:
         return "dynamic" if dynamic else "static"
 
     def _make_native(self):
-        if self.world == 1:  # forced single-rank communicator: no rendezvous needed
+        """RCCL communicator over this group's ranks.  Whenever a process group exists (also at world 1 under
+        torchrun) rank 0's unique id travels through the rendezvous TCPStore, so a 1-rank
+        rehearsal executes the same exchange as an 8-rank job; only a forced reducer without any process
+        group creates its id locally.  ``uid_via_store`` records which one ran."""
+        self.uid_via_store = False
+        if not dist.is_initialized():   # forced single-rank communicator, no process group: nothing to exchange
             uid = kernels().rccl_unique_id()
         else:
             key = f"hq_rccl_uid_{next(_uid_counter)}"
             store = dist.distributed_c10d._get_default_store()
             if self.rank == 0:
-                uid = kernels().rccl_unique_id()
-                store.set(key, uid)
-            else:
-                uid = store.get(key)
+                store.set(key, kernels().rccl_unique_id())
+            uid = store.get(key)        # rank 0 reads its own id back: the same store round trip everywhere
+            self.uid_via_store = True
         dev = self.store.device.index if self.store.device.index is not None else torch.cuda.current_device()
         red = kernels().Reducer(self.rank, self.world, bytes(uid), dev)
         logger.info(f"native RCCL reducer up (rank {self.rank}/{self.world}, device {dev})")
@@ -172,6 +181,7 @@ class GradReducer:
             dist.broadcast(m, 0, group=self.group)
         self.store.mark_master_dirty()
         self.store.sync_compute()
+        self.broadcast_done = True
 
     # ------------------------------------------------------------------ per step
     @property

@@ -92,10 +92,17 @@ class TrainEngine:
 
     So batch_split = 1 uses one graph, the reference's 128 × 2 accumulation three (first, middle, last).  The
     clip + fused optimizer step stays eager (its learning rate changes every step).  At small micro-batches
-    the step is launch-bound (the reference's 2 × 512): one graph launch replaces ~300 kernel launches."""
+    the step is launch-bound (the reference's 2 × 512): one graph launch replaces ~300 kernel launches.
+
+    Graphs are captured for at most ``max_graph_shapes`` distinct input shapes (the first ones seen); a
+    micro-batch of any other shape (collate pads each NQ batch to its own length) runs eagerly beside them,
+    so real data with many lengths cannot grow the graph set without bound.  Every capture allocates from
+    ONE private mempool: the graphs replay one at a time on one stream, so a capture may reuse what an
+    earlier one freed, and memory stays at about one micro-step's working set."""
 
     def __init__(self, model, loss_fn, optimizer, *, scheduler=None, reducer=None, max_grad_norm: float = 1.0,
-                 batch_split: int = 1, no_sync_accum: bool = True, profile: bool = False, graph: bool = False):
+                 batch_split: int = 1, no_sync_accum: bool = True, profile: bool = False, graph: bool = False,
+                 max_graph_shapes: int = 2):
         self.model = model
         self.loss_fn = loss_fn
         self.optimizer = optimizer
@@ -109,8 +116,12 @@ class TrainEngine:
         self._timer = PhaseTimer(profile, model.store.device)
         self.graph = bool(graph)
         self._graphs: Dict[tuple, tuple] = {}   # (shape key, fresh, sync) -> (graph, static_in, static_lab, record)
+        self._graph_shapes: List[tuple] = []    # shape keys with captured graphs, in capture order
+        self.max_graph_shapes = max(1, int(max_graph_shapes))
+        self._graph_pool = None                 # one private mempool shared by every capture
         self._graph_warm = 0
         self.graph_replays = 0
+        self.graph_eager_steps = 0              # micro-steps of an uncaptured shape run eagerly beside the graphs
 
     @property
     def device(self):
@@ -127,7 +138,10 @@ class TrainEngine:
                 # the reference-heads path draws its classifier dropout key on the host: a captured graph
                 # would replay one mask forever (only the fused kernels read the device seed word)
                 and fused_heads_possible(m)
-                and (r is None or (not r.timing and not r.verify)))
+                # the reducer's collectives are captured only on the native RCCL path (fence → ncclAllReduce on
+                # its comm stream → join), the one the graph tests cover; the torch.distributed fallback
+                # (work.wait(), gloo rescale) stays eager
+                and (r is None or (r._native is not None and not r.timing and not r.verify)))
 
     @staticmethod
     def _shape_key(inputs, labels):
@@ -163,14 +177,22 @@ class TrainEngine:
         side.wait_stream(torch.cuda.current_stream())
         g = torch.cuda.CUDAGraph()
         rng = torch.get_rng_state()   # the capture's forward draws a (unused) host seed: keep the stream aligned
-        with torch.cuda.graph(g, stream=side):
+        with torch.cuda.graph(g, stream=side, pool=self._graph_pool):
             loss = self.loss_fn(m(**static_in), static_lab)
             (loss / self.batch_split).backward()
             if sync:
                 self.reducer.finalize()   # the comm stream joins the capturing stream inside the graph
         torch.set_rng_state(rng)
         torch.cuda.current_stream().wait_stream(side)
+        if self._graph_pool is None:
+            self._graph_pool = g.pool()
+        if key[0] not in self._graph_shapes:
+            self._graph_shapes.append(key[0])
         self._graphs[key] = (g, static_in, static_lab, self.loss_fn.last)
+
+    def _graph_capturable(self, inputs, labels) -> bool:
+        shape = self._shape_key(inputs, labels)
+        return shape in self._graph_shapes or len(self._graph_shapes) < self.max_graph_shapes
 
     def _graph_micro_step(self, inputs, labels) -> Optional[StepResult]:
         fresh, sync, boundary = self._kind()
@@ -204,16 +226,19 @@ class TrainEngine:
         if self._graphs:
             self.model.use_device_seed(False)
         self._graphs, self._graph_warm = {}, 0
+        self._graph_shapes, self._graph_pool = [], None
 
     def micro_step(self, inputs, labels) -> Optional[StepResult]:
         """Forward+backward of one micro-batch; runs the optimizer on the accumulation boundary."""
         if self._graph_eligible():
-            if self._graph_warm >= 2 or self._graphs:
+            if (self._graph_warm >= 2 or self._graphs) and self._graph_capturable(inputs, labels):
                 return self._graph_micro_step(inputs, labels)
-            self._graph_warm += 1   # eager warm-up: kernel attributes, Wᵀ copies, allocator pools
+            if not self._graphs:
+                self._graph_warm += 1   # eager warm-up: kernel attributes, Wᵀ copies, allocator pools
         elif self._graphs:
             self.release_graph()
         if self._graphs:   # eager step beside live graphs (an uncaptured shape): host seeds again
+            self.graph_eager_steps += 1
             self.model.use_device_seed(False)
             try:
                 return self._eager_micro_step(inputs, labels)

@@ -182,7 +182,8 @@ def get_trainer_parser() -> ArgumentParser:
                         help="GPU, bf16: capture each kind of micro-step (forward + backward; first / middle / last "
                              "micro-batch of an accumulation cycle, the last one with the gradient all-reduces) into "
                              "a HIP graph after two eager warm-up micro-steps and replay them (launch-bound small "
-                             "micro-batches, e.g. the reference's 128 x 2).")
+                             "micro-batches, e.g. the reference's 128 x 2).  Graphs exist for the first two input "
+                             "shapes only (one shared mempool); batches of other padded lengths run eagerly.")
     parser.add_argument("--torch_profile_dir", type=cast2(str), default=None,
                         help="Export a torch.profiler Chrome trace of optimizer steps --torch_profile_steps here.")
     parser.add_argument("--torch_profile_steps", type=str, default="3:5",

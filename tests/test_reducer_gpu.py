@@ -1,7 +1,7 @@
 """The native RCCL gradient reducer inside a real BERT-base training step, on one GPU.
 
 With ``force=True`` the reducer keeps a 1-rank RCCL communicator active, so every bucket of the backward
-goes through the multi-GPU path (arena slice → fence → ncclAllReduce(avg) on the high-priority comm stream
+goes through the multi-GPU path (arena slice → fence → ncclAllReduce(avg) on the reducer's comm stream
 → compute-stream wait) — the 8-GPU code path minus the peers.  Averaging over one rank is the identity,
 so the weights after each step must be BITWISE equal to a run without a reducer; and with the
 weight-gradient GEMMs on a side stream (``HQ_WGRAD_STREAM=1``) the comm-stream checksums taken where the
@@ -122,8 +122,10 @@ def test_reducer_timing_reports_comm_wait(cuda):
 
 def test_torchrun_world1_runs_the_n_rank_path(cuda, tmp_path):
     """`torchrun --nproc-per-node 1 bench.py --force_reducer` executes every line of the 8-GPU bench path:
-    RCCL process group (device_id), reducer uid exchange through the TCPStore, native broadcast, the dynamic
-    GEMM schedule, barrier, all_reduce(MAX) and destroy — and the JSON proves what ran."""
+    RCCL process group (device_id), the reducer's RCCL uid shipped through the TCPStore (rank 0 sets it and
+    reads it back, as every rank of an N-rank job does), the native ncclBroadcast of the weights, the dynamic
+    GEMM schedule, barrier, all_reduce(MAX) and destroy — and the JSON proves what ran (`uid_via_store`,
+    `broadcast_done`, `rccl_comm_ranks`)."""
     import json
     import os
     import subprocess
@@ -139,5 +141,21 @@ def test_torchrun_world1_runs_the_n_rank_path(cuda, tmp_path):
     assert rec["reducer"] == "native-rccl", rec
     assert rec["process_group"] == "nccl" and rec["world_size"] == 1 and rec["rccl_comm_ranks"] == 1, rec
     assert rec["gemm_sched"] == "dynamic" and rec["reducer_buckets"] > 1, rec
+    assert rec["uid_via_store"] is True and rec["broadcast_done"] is True, rec
     assert "not the headline config" in rec["metric"], rec
     assert rec["value"] > 0 and rec["final_loss"] == rec["final_loss"], rec
+
+
+def test_bench_refuses_more_gpus_than_visible(cuda):
+    """`python bench.py --gpus 2` on a one-GPU box must fail loudly instead of reporting a 1-GPU run under a
+    2-GPU label (the self-launch checks the visible devices before starting any rank)."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    n = torch.cuda.device_count()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n + 1), "--steps", "1",
+                        "--warmup", "0"], cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       timeout=120)
+    assert r.returncode != 0 and "GPU(s) are visible" in r.stdout, r.stdout[-2000:]
+    assert '"metric"' not in r.stdout
