@@ -36,7 +36,23 @@ def build_trainer(params, model_params, device, *, rank: int, local_idx: int, us
                                             seed=params.seed, precision=params.precision)
     optimizer = factories.init_optimizer(params, model)
     auto = getattr(params, "auto_batch_split", None)
-    if device.type == "cuda" and auto is not False:  # GPUs: on by default (raise-only), off on CPU
+    merge_segments = 1
+    if device.type == "cuda" and auto in (None, True):   # GPU default: exact-objective merge
+        from ..train.memory import device_hbm_bytes, estimate, plan_exact_merge
+        hbm = device_hbm_bytes(device)
+        split, merge_segments = plan_exact_merge(model.config, params.max_seq_len, params.train_batch_size, hbm,
+                                                 params.batch_split)
+        log = logging.getLogger(__name__)
+        if split != params.batch_split:
+            log.info(f"auto_batch_split: batch_split {params.batch_split} -> {split} (the micro-batch does not fit "
+                     f"the HBM memory model; --auto_batch_split False keeps the configured split)")
+        if merge_segments > 1:
+            log.info(f"auto_batch_split: {split} micro-batches of {params.train_batch_size // split} run as "
+                     f"{split // merge_segments} merged pass(es) of {merge_segments} loss segments each (the "
+                     f"reference's mean of per-micro-batch means; --auto_batch_split raise keeps one pass per "
+                     f"micro-batch)")
+        params.batch_split = split
+    elif device.type == "cuda" and auto in ("raise", "merge"):
         from ..train.memory import device_hbm_bytes, estimate, plan_batch_split
         hbm = device_hbm_bytes(device)
         merge = auto == "merge"
@@ -77,7 +93,7 @@ def build_trainer(params, model_params, device, *, rank: int, local_idx: int, us
                    cuda_graph=bool(getattr(params, "cuda_graph", False)),
                    eval_shard=params.eval_shard, precision=params.precision,
                    torch_profile_dir=params.torch_profile_dir, torch_profile_steps=params.torch_profile_steps,
-                   sampler_seed=params.seed if params.seed is not None else 0)
+                   sampler_seed=params.seed if params.seed is not None else 0, merge_segments=merge_segments)
 
 
 def run_worker(local_idx, plan, params, model_params):

@@ -643,7 +643,8 @@ std::vector<Tensor> qa_heads_fwd(Tensor seq, int64_t L, std::vector<Tensor> w, d
 // returns losses [6], dlog [T,2], dheads [B,16]
 std::vector<Tensor> qa_loss(Tensor logits, Tensor cls, Tensor reg, Tensor t_start, Tensor t_end, Tensor t_rs, Tensor t_re,
                             Tensor t_cls, c10::optional<Tensor> lw, int64_t kind, int64_t ignore_cls,
-                            std::vector<double> weights, double alpha, double gamma, double conf, double fill) {
+                            std::vector<double> weights, double alpha, double gamma, double conf, double fill,
+                            c10::optional<Tensor> seg_len) {
   check(logits, F32, "logits"); check(cls, F32, "cls"); check(reg, F32, "reg");
   check(t_start, I64, "start_class"); check(t_end, I64, "end_class"); check(t_cls, I64, "cls target");
   check(t_rs, F32, "start_reg"); check(t_re, F32, "end_reg"); check_opt(lw, F32, "label_weights");
@@ -654,6 +655,12 @@ std::vector<Tensor> qa_loss(Tensor logits, Tensor cls, Tensor reg, Tensor t_star
                   t_re.numel() == B, "targets must have B elements");
   TORCH_CHECK(!lw.has_value() || !lw->defined() || lw->numel() == NL, "label weights [NL]");
   TORCH_CHECK(weights.size() == 5 && kind >= 0 && kind <= 2, "loss config");
+  int nseg = 1;
+  if (seg_len.has_value() && seg_len->defined()) {   // exact-objective merge: one segment per micro-batch
+    check(*seg_len, at::kInt, "segment lengths");
+    nseg = (int)seg_len->numel();
+    TORCH_CHECK(nseg >= 1 && B % nseg == 0, "segments must split the batch into equal parts");
+  }
   c10::DeviceGuard g(logits.device());
   auto f = logits.options();
   auto losses = at::empty({6}, f);
@@ -667,7 +674,8 @@ std::vector<Tensor> qa_loss(Tensor logits, Tensor cls, Tensor reg, Tensor t_star
   cfg.alpha = (float)alpha; cfg.gamma = (float)gamma; cfg.conf = (float)conf; cfg.fill = (float)fill;
   hq_qa_loss(ptr<float>(logits), ptr<float>(cls), ptr<float>(reg), ptr<int64_t>(t_start), ptr<int64_t>(t_end),
              ptr<int64_t>(t_cls), ptr<float>(t_rs), ptr<float>(t_re), optr<float>(lw), ptr<float>(dlog), ptr<float>(dheads),
-             ptr<float>(losses), ptr<float>(part), ticket(logits, 1), (int)B, (int)(T / B), (int)NL, cfg, cur_stream());
+             ptr<float>(losses), ptr<float>(part), ticket(logits, 1), (int)B, (int)(T / B), (int)NL, cfg,
+             nseg > 1 || (seg_len.has_value() && seg_len->defined()) ? optr<int>(seg_len) : nullptr, nseg, cur_stream());
   return {losses, dlog, dheads};
 }
 

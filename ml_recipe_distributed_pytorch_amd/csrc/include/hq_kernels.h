@@ -190,7 +190,8 @@ int hq_qa_loss_partials(int B);                 // rows of the [rows][4] loss sc
 // losses[6] = start, end, start_reg, end_reg, cls, total; dlog [B·L, 2] and dheads [B, 16] = d total / d preds
 void hq_qa_loss(const float* logits, const float* cls, const float* reg, const int64_t* t_start, const int64_t* t_end,
                 const int64_t* t_cls, const float* t_rs, const float* t_re, const float* lw, float* dlog, float* dheads,
-                float* losses, float* part, unsigned* cnt, int B, int L, int NL, const HqLossCfg& cfg, hipStream_t s);
+                float* losses, float* part, unsigned* cnt, int B, int L, int NL, const HqLossCfg& cfg, const int* seg_len,
+                int nseg, hipStream_t s);   // nseg equal segments (seg_len [nseg] span lengths, or null = L)
 int hq_qa_heads_bwd_span_blocks(int T);         // rows of the [rows][2H + 2] span partial scratch
 void hq_qa_heads_bwd(const uint16_t* seq, const float* dlog, const float* dheads, const float* gscale, const float* pooled,
                      const float* reg, const HqHeadWeights& w, const HqHeadGrads& g, uint16_t* dseq, float* span_part,

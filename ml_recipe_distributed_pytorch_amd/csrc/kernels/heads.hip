@@ -186,16 +186,26 @@ struct LossArgs {
   const float *t_rs, *t_re, *lw;
   float *dlog, *dheads, *losses, *part;  // part [nrow + 1][4]
   unsigned* cnt;
-  int B, L, NL, kind, ignore_cls, nrow;
+  const int* seg_len;   // [nseg] span length of each segment (its micro-batch's own padded length) or null
+  int B, L, NL, kind, ignore_cls, nrow, nseg;
   float w0, w1, w2, w3, w4, alpha, gamma, conf, fill;
 };
 
 enum { kLossCE = 0, kLossFocal = 1, kLossSmooth = 2 };
 
-__device__ __forceinline__ int span_valid_count(const int64_t* t, int B, int L, int lane) {
+// Segments (exact-objective micro-batch merge): the batch is nseg equal, contiguous segments, each one of the
+// reference's micro-batches.  Every loss term is normalised inside its segment (span CE over the segment's
+// valid spans and over its own span length, class CE / focal over its valid targets, KL batchmean and MSE over
+// its samples) and the terms are averaged over the segments — the reference's mean of per-micro-batch means
+// (trainer.py:197-204).  nseg = 1 is the plain batch.
+__device__ __forceinline__ int seg_span_len(const LossArgs& a, int s) {
+  return a.seg_len ? min(max(a.seg_len[s], 1), a.L) : a.L;
+}
+
+__device__ __forceinline__ int span_valid_count(const int64_t* t, int lo, int n, int L, int lane) {
   float c = 0.f;
-  for (int i = lane; i < B; i += 64) {
-    const int64_t v = t[i];
+  for (int i = lane; i < n; i += 64) {
+    const int64_t v = t[lo + i];
     c += (v >= 0 && v < L) ? 1.f : 0.f;
   }
   return (int)hq_wave_sum(c);
@@ -212,14 +222,17 @@ __global__ __launch_bounds__(256) void qa_loss_kernel(LossArgs a) {
   __shared__ float red[4 * 256 + 8];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int B = a.B, L = a.L;
+  const int bs = B / a.nseg;                         // samples per segment
+  const float inv_seg = 1.f / (float)a.nseg;
   if ((int)blockIdx.x < a.nrow) {  // -------------------------------------- span CE, one wave per sample
     const int b = blockIdx.x * 4 + wv;
     float nll_s = 0.f, nll_e = 0.f;
     if (b < B) {
-      const int ns = span_valid_count(a.t_start, B, L, lane), ne = span_valid_count(a.t_end, B, L, lane);
+      const int sg = b / bs, lo = sg * bs, Ls = seg_span_len(a, sg);
+      const int ns = span_valid_count(a.t_start, lo, bs, Ls, lane), ne = span_valid_count(a.t_end, lo, bs, Ls, lane);
       const float2* row = reinterpret_cast<const float2*>(a.logits) + (size_t)b * L;
       float ms = -INFINITY, me = -INFINITY, ss = 0.f, se = 0.f;
-      for (int j = lane; j < L; j += 64) {
+      for (int j = lane; j < Ls; j += 64) {
         const float2 z = row[j];
         if (z.x > ms) { ss = ss * expf(ms - z.x) + 1.f; ms = z.x; } else { ss += expf(z.x - ms); }
         if (z.y > me) { se = se * expf(me - z.y) + 1.f; me = z.y; } else { se += expf(z.y - me); }
@@ -229,16 +242,23 @@ __global__ __launch_bounds__(256) void qa_loss_kernel(LossArgs a) {
       const float Se = hq_wave_sum(me == -INFINITY ? 0.f : se * expf(me - Me));
       const float lse_s = Ms + logf(Ss), lse_e = Me + logf(Se);
       const int64_t ts = a.t_start[b], te = a.t_end[b];
-      const bool vs = ts >= 0 && ts < L, ve = te >= 0 && te < L;
-      if (vs) nll_s = lse_s - row[ts].x;
-      if (ve) nll_e = lse_e - row[te].y;
-      const float gs = vs ? a.w0 / (float)ns : 0.f, ge = ve ? a.w1 / (float)ne : 0.f;
+      const bool vs = ts >= 0 && ts < Ls, ve = te >= 0 && te < Ls;
+      // per-sample terms already normalised by the segment's valid count and the segment count; a segment
+      // with no valid span is 0/0 = NaN in torch's CE (ignore_index) — its first sample carries that NaN
+      const float cs = inv_seg / (float)ns, ce = inv_seg / (float)ne;
+      if (vs) nll_s = (lse_s - row[ts].x) * cs;
+      if (ve) nll_e = (lse_e - row[te].y) * ce;
+      if (b == lo && ns == 0) nll_s = NAN;
+      if (b == lo && ne == 0) nll_e = NAN;
+      const float gs = vs ? a.w0 * cs : 0.f, ge = ve ? a.w1 * ce : 0.f;
       float2* drow = reinterpret_cast<float2*>(a.dlog) + (size_t)b * L;
       for (int j = lane; j < L; j += 64) {
-        const float2 z = row[j];
-        float2 d;
-        d.x = gs * (expf(z.x - lse_s) - (j == ts ? 1.f : 0.f));
-        d.y = ge * (expf(z.y - lse_e) - (j == te ? 1.f : 0.f));
+        float2 d = make_float2(0.f, 0.f);   // positions past the segment's own length are not in its softmax
+        if (j < Ls) {
+          const float2 z = row[j];
+          d.x = gs * (expf(z.x - lse_s) - (j == ts ? 1.f : 0.f));
+          d.y = ge * (expf(z.y - lse_e) - (j == te ? 1.f : 0.f));
+        }
         drow[j] = d;
       }
     }
@@ -250,7 +270,8 @@ __global__ __launch_bounds__(256) void qa_loss_kernel(LossArgs a) {
       p[1] = ((red[1] + red[3]) + red[5]) + red[7];
     }
   } else {  // ------------------------------------------------------- class + regression block
-    // pass 1: class-loss normaliser (CE: Σ weights of valid targets; focal: #valid; smooth: B)
+    // pass 1: class-loss normaliser (CE: Σ weights of valid targets; focal: #valid; smooth: B) of the whole
+    // batch; with segments each sample recomputes its own segment's (bs targets) in pass 2
     float den = 0.f;
     for (int b = tid; b < B; b += 256) {
       const int64_t t = a.t_cls[b];
@@ -265,6 +286,16 @@ __global__ __launch_bounds__(256) void qa_loss_kernel(LossArgs a) {
     float lc = 0.f, lrs = 0.f, lre = 0.f;
     const float invB = 1.f / (float)B;
     for (int b = tid; b < B; b += 256) {
+      float den_s = den;   // this sample's segment normaliser (× nseg below)
+      if (a.nseg > 1 && a.kind != kLossSmooth) {
+        den_s = 0.f;
+        for (int i = (b / bs) * bs, e = i + bs; i < e; ++i) {
+          const int64_t ti = a.t_cls[i];
+          if (cls_valid(a, ti)) den_s += (a.kind == kLossCE && a.lw) ? a.lw[ti] : 1.f;
+        }
+      }
+      const float inv_den = a.kind == kLossSmooth ? invB : inv_seg / den_s;
+      if (a.kind != kLossSmooth && b % bs == 0 && den_s == 0.f) lc = NAN;   // torch: mean over no targets
       float z[kMaxNL], dz[kMaxNL];
       float m = -INFINITY;
 #pragma unroll
@@ -287,7 +318,7 @@ __global__ __launch_bounds__(256) void qa_loss_kernel(LossArgs a) {
             if (c < a.NL) {
               const float dist = c == t ? a.conf : a.fill;
               S += dist;
-              if (dist > 0.f) lc += dist * (logf(dist) - (z[c] - lse));
+              if (dist > 0.f) lc += dist * (logf(dist) - (z[c] - lse)) * invB;
             }
           }
 #pragma unroll
@@ -301,17 +332,17 @@ __global__ __launch_bounds__(256) void qa_loss_kernel(LossArgs a) {
         const float lp = zt - lse;
         if (a.kind == kLossCE) {
           const float wt = a.lw ? a.lw[t] : 1.f;
-          lc += wt * -lp;
-          const float g = a.w4 * wt / den;
+          lc += wt * -lp * inv_den;
+          const float g = a.w4 * wt * inv_den;
 #pragma unroll
           for (int c = 0; c < kMaxNL; ++c)
             if (c < a.NL) dz[c] = g * (expf(z[c] - lse) - (c == t ? 1.f : 0.f));
         } else {  // focal: loss_b = -α(1-p)^γ·log p
           const float pt = expf(lp), omp = 1.f - pt;
           const float powg = powf(omp, a.gamma);
-          lc += -a.alpha * powg * lp;
+          lc += -a.alpha * powg * lp * inv_den;
           const float d2 = omp > 0.f ? a.gamma * powf(omp, a.gamma - 1.f) * pt * lp : 0.f;
-          const float gl = -a.alpha * (powg - d2) / den * a.w4;  // d loss / d log p_t
+          const float gl = -a.alpha * (powg - d2) * inv_den * a.w4;  // d loss / d log p_t
 #pragma unroll
           for (int c = 0; c < kMaxNL; ++c)
             if (c < a.NL) dz[c] = gl * ((c == t ? 1.f : 0.f) - expf(z[c] - lse));
@@ -339,16 +370,15 @@ __global__ __launch_bounds__(256) void qa_loss_kernel(LossArgs a) {
   }
   if (!last_arriver(a.cnt, (unsigned)(a.nrow + 1), reinterpret_cast<int*>(red + 4 * 256))) return;
   if (wv != 0) return;
-  const int ns = span_valid_count(a.t_start, B, L, lane), ne = span_valid_count(a.t_end, B, L, lane);
-  float ss = 0.f, se = 0.f;
+  float ss = 0.f, se = 0.f;   // the per-sample terms arrive normalised (segment count, valid count)
   for (int r = lane; r < a.nrow; r += 64) { ss += a.part[(size_t)r * 4]; se += a.part[(size_t)r * 4 + 1]; }
   ss = hq_wave_sum(ss);
   se = hq_wave_sum(se);
   if (lane == 0) {
     const float* pc = a.part + (size_t)a.nrow * 4;
-    const float l0 = ss / (float)ns, l1 = se / (float)ne;  // 0/0 = NaN when every target is ignored (torch)
+    const float l0 = ss, l1 = se;   // NaN when a segment has every span target ignored (torch's 0/0)
     const float l2 = pc[1] / (float)B, l3 = pc[2] / (float)B;
-    const float l4 = pc[0] / pc[3];
+    const float l4 = pc[0];
     a.losses[0] = l0; a.losses[1] = l1; a.losses[2] = l2; a.losses[3] = l3; a.losses[4] = l4;
     a.losses[5] = a.w0 * l0 + a.w1 * l1 + a.w2 * l2 + a.w3 * l3 + a.w4 * l4;
   }
@@ -659,8 +689,11 @@ int hq_qa_loss_partials(int B) { return (B + 3) / 4 + 1; }
 
 void hq_qa_loss(const float* logits, const float* cls, const float* reg, const int64_t* t_start, const int64_t* t_end,
                 const int64_t* t_cls, const float* t_rs, const float* t_re, const float* lw, float* dlog, float* dheads,
-                float* losses, float* part, unsigned* cnt, int B, int L, int NL, const HqLossCfg& cfg, hipStream_t s) {
+                float* losses, float* part, unsigned* cnt, int B, int L, int NL, const HqLossCfg& cfg, const int* seg_len,
+                int nseg, hipStream_t s) {
   LossArgs a;
+  a.seg_len = seg_len;
+  a.nseg = nseg > 0 ? nseg : 1;
   a.logits = logits; a.cls = cls; a.reg = reg;
   a.t_start = t_start; a.t_end = t_end; a.t_cls = t_cls; a.t_rs = t_rs; a.t_re = t_re; a.lw = lw;
   a.dlog = dlog; a.dheads = dheads; a.losses = losses; a.part = part; a.cnt = cnt;

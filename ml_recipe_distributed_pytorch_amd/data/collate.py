@@ -55,3 +55,40 @@ def collate_fun(items: Sequence, tokenizer=None, return_items: bool = False, *, 
     if return_items:
         return [inputs, labels, list(items)]
     return [inputs, labels]
+
+
+def merge_micro_batches(micro: Sequence, pad_token_id: int = 0):
+    """One forward/backward batch from S collated micro-batches, keeping the reference's objective.
+
+    Each micro-batch ``(inputs, labels)`` was collated on its own (padded to its own max length L_s, as
+    ``collate_fun`` does per DataLoader batch).  They are right-padded to the longest L and concatenated; the
+    extra positions are padding with ``attention_mask`` False (masked keys, so every real token's encoding is
+    unchanged), and ``labels`` gains
+
+    * ``segments`` — int32 [S] of the L_s, on the batch's device (read by the loss kernel, graph-capturable),
+    * ``segment_lengths`` — the same as a tuple of ints (the CPU loss path),
+
+    with which the loss scores segment s exactly as the reference scores micro-batch s (span softmax over its
+    L_s positions, every term normalised inside the segment) and averages over segments (``models/losses.py
+    WeightedLoss._segmented``; ``heads.hip`` ``qa_loss_kernel``).  All micro-batches must have the same size."""
+    micro = list(micro)
+    if len(micro) == 1:
+        return micro[0]
+    lens = [int(inp["input_ids"].shape[1]) for inp, _ in micro]
+    sizes = {int(inp["input_ids"].shape[0]) for inp, _ in micro}
+    assert len(sizes) == 1, f"micro-batches of unequal size {sorted(sizes)} cannot be merged into equal segments"
+    Lm = max(lens)
+    fill = {"input_ids": pad_token_id, "token_type_ids": 0, "attention_mask": False}
+
+    def pad(t, key):
+        if t.dim() < 2 or t.shape[1] == Lm:
+            return t
+        ext = torch.full((t.shape[0], Lm - t.shape[1]), fill.get(key, 0), dtype=t.dtype, device=t.device)
+        return torch.cat([t, ext], 1)
+    inputs = {k: torch.cat([pad(inp[k], k) for inp, _ in micro], 0) for k in micro[0][0]}
+    labels = {k: torch.cat([lab[k] for _, lab in micro], 0) for k in micro[0][1]
+              if torch.is_tensor(micro[0][1][k]) and k != "segments"}
+    dev = inputs["input_ids"].device
+    labels["segments"] = torch.tensor(lens, dtype=torch.int32).to(dev, non_blocking=True)
+    labels["segment_lengths"] = tuple(lens)
+    return inputs, labels

@@ -231,11 +231,12 @@ def fused_loss_config(losses: Dict[str, tuple]) -> Optional[FusedLossConfig]:
 
 class _FusedLossFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, s, e, rs, re_, cls, st: _FusedState, cfg: FusedLossConfig, t_start, t_end, t_rs, t_re, t_cls):
+    def forward(ctx, s, e, rs, re_, cls, st: _FusedState, cfg: FusedLossConfig, t_start, t_end, t_rs, t_re, t_cls,
+                seg=None):
         from .._native import kernels
         losses, dlog, dheads = kernels().qa_loss(st.logits, st.cls, st.reg, t_start, t_end, t_rs, t_re, t_cls,
                                                  cfg.lw(st.logits.device), cfg.kind, cfg.ignore_cls, cfg.weights,
-                                                 cfg.alpha, cfg.gamma, cfg.conf, cfg.fill)
+                                                 cfg.alpha, cfg.gamma, cfg.conf, cfg.fill, seg)
         st.dlog, st.dheads, st.losses = dlog.view(st.B, st.L, 2), dheads, losses
         ctx.st = st
         return losses[5]
@@ -245,19 +246,25 @@ class _FusedLossFn(torch.autograd.Function):
         st = ctx.st
         st.gscale = g.detach().float().reshape(1).contiguous()
         dl, dh = st.dlog, st.dheads
-        return (dl[..., 0], dl[..., 1], dh[:, 8], dh[:, 9], dh[:, :st.NL], None, None, None, None, None, None, None)
+        return (dl[..., 0], dl[..., 1], dh[:, 8], dh[:, 9], dh[:, :st.NL], None, None, None, None, None, None, None,
+                None)
 
 
 def fused_loss(preds: HeadOutputs, targets, cfg: FusedLossConfig):
-    """(total loss, per-term device losses [6]) with the prediction gradients precomputed."""
+    """(total loss, per-term device losses [6]) with the prediction gradients precomputed.  ``targets
+    ["segments"]`` (int32 [S], optional): the batch is S merged micro-batches with those span lengths — every
+    term is normalised per segment and averaged over them (``data.collate.merge_micro_batches``)."""
     st = preds.fused
     dev = st.logits.device
 
     def t(k, dt):
         return targets[k].to(dev, dt, non_blocking=True).reshape(-1).contiguous()
+    seg = targets.get("segments")
+    if seg is not None:
+        seg = seg.to(dev, torch.int32, non_blocking=True).contiguous()
     total = _FusedLossFn.apply(preds["start_class"], preds["end_class"], preds["start_reg"], preds["end_reg"],
                                preds["cls"], st, cfg, t("start_class", torch.int64), t("end_class", torch.int64),
-                               t("start_reg", torch.float32), t("end_reg", torch.float32), t("cls", torch.int64))
+                               t("start_reg", torch.float32), t("end_reg", torch.float32), t("cls", torch.int64), seg)
     return total, st.losses
 
 

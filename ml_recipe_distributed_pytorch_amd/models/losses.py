@@ -103,12 +103,46 @@ class WeightedLoss:
             if avg_meters is not None:
                 avg_meters.update(rec.to_floats())
             return full
+        lens = targets.get("segment_lengths")
+        if lens is not None and len(lens) > 1:
+            return self._segmented(preds, targets, lens, avg_meters)
         rec = LossRecord()
         full = 0.0
         for key, (fn, weight) in self._losses.items():
             loss = fn(preds[key].float(), targets[key])
             rec[key] = loss.detach()
             full = full + weight * loss
+        rec["loss"] = full.detach()
+        self.last = rec
+        if avg_meters is not None:
+            avg_meters.update(rec.to_floats())
+        return full
+
+    def _segmented(self, preds, targets, lens, avg_meters):
+        """Merged micro-batches (``data.collate.merge_micro_batches``): each segment is one of the reference's
+        micro-batches, scored exactly as the reference scores it — span logits cut to that micro-batch's own
+        padded length, every loss module normalising over that segment alone — and the segment losses are
+        averaged: the reference's mean of per-micro-batch means (``trainer.py:197-204``).  The CPU oracle of
+        the loss kernel's segment mode; the record holds the segment means of every term."""
+        S = len(lens)
+        B = preds["cls"].shape[0]
+        bs = B // S
+        assert bs * S == B, "segments must split the batch into equal parts"
+        sums: Dict[str, torch.Tensor] = {}
+        full = 0.0
+        for s, Ls in enumerate(lens):
+            rows = slice(s * bs, (s + 1) * bs)
+            part = 0.0
+            for key, (fn, weight) in self._losses.items():
+                p = preds[key][rows]
+                if key in ("start_class", "end_class"):
+                    p = p[:, :int(Ls)]
+                loss = fn(p.float(), targets[key][rows])
+                sums[key] = sums[key] + loss.detach() if key in sums else loss.detach()
+                part = part + weight * loss
+            full = full + part
+        full = full / S
+        rec = LossRecord({k: v / S for k, v in sums.items()})
         rec["loss"] = full.detach()
         self.last = rec
         if avg_meters is not None:

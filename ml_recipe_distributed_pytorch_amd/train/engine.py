@@ -10,6 +10,10 @@ Per optimizer step (reference ``trainer.py:266-300`` semantics, re-engineered):
   optimizer.step(clip_coef=coef)                      # one fused AdamW kernel (+ bf16 copy-out)
   optimizer.zero_grad(); scheduler.step()
 Loss values stay on device (``LossRecord``); callers sync them at their logging cadence.
+
+Exact-objective merge (``merge_segments`` = G): the reference's micro-batches are collated one by one as it
+does, then G of them run as one forward/backward whose loss scores each as its own segment — the same
+gradient as G accumulated micro-steps (mean of per-micro-batch means), at merged-batch speed.
 """
 from __future__ import annotations
 
@@ -102,7 +106,7 @@ class TrainEngine:
 
     def __init__(self, model, loss_fn, optimizer, *, scheduler=None, reducer=None, max_grad_norm: float = 1.0,
                  batch_split: int = 1, no_sync_accum: bool = True, profile: bool = False, graph: bool = False,
-                 max_graph_shapes: int = 2):
+                 max_graph_shapes: int = 2, merge_segments: int = 1):
         self.model = model
         self.loss_fn = loss_fn
         self.optimizer = optimizer
@@ -110,6 +114,12 @@ class TrainEngine:
         self.reducer = reducer
         self.max_grad_norm = max_grad_norm
         self.batch_split = max(1, int(batch_split))
+        # exact-objective merge: every `merge_segments` consecutive micro-batches handed to micro_step() run as ONE
+        # forward/backward whose loss keeps them as segments (data.collate.merge_micro_batches); `batch_split`
+        # then counts those merged passes per optimizer step
+        self.merge_segments = max(1, int(merge_segments))
+        self._pending: List[tuple] = []
+        self._pad_id = int(getattr(getattr(model, "config", None), "pad_token_id", 0) or 0)
         self.no_sync_accum = no_sync_accum
         self.profile = profile
         self.micro = 0
@@ -229,7 +239,18 @@ class TrainEngine:
         self._graph_shapes, self._graph_pool = [], None
 
     def micro_step(self, inputs, labels) -> Optional[StepResult]:
-        """Forward+backward of one micro-batch; runs the optimizer on the accumulation boundary."""
+        """Forward+backward of one micro-batch; runs the optimizer on the accumulation boundary.  With
+        ``merge_segments`` = G > 1 the micro-batches are buffered and every G of them run as one merged pass."""
+        if self.merge_segments > 1:
+            self._pending.append((inputs, labels))
+            if len(self._pending) < self.merge_segments:
+                return None
+            from ..data.collate import merge_micro_batches
+            inputs, labels = merge_micro_batches(self._pending, self._pad_id)
+            self._pending = []
+        return self._pass(inputs, labels)
+
+    def _pass(self, inputs, labels) -> Optional[StepResult]:
         if self._graph_eligible():
             if (self._graph_warm >= 2 or self._graphs) and self._graph_capturable(inputs, labels):
                 return self._graph_micro_step(inputs, labels)
@@ -287,5 +308,5 @@ class TrainEngine:
         res = None
         for inputs, labels in micro_batches:
             res = self.micro_step(inputs, labels)
-        assert res is not None, "number of micro-batches must equal batch_split"
+        assert res is not None, "number of micro-batches must equal batch_split × merge_segments"
         return res

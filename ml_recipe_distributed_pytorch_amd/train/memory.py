@@ -75,6 +75,26 @@ def plan_batch_split(cfg, seq_len: int, train_batch_size: int, hbm_bytes: float,
     return train_batch_size
 
 
+def plan_exact_merge(cfg, seq_len: int, train_batch_size: int, hbm_bytes: float, requested: int = 1,
+                     headroom: float = 0.9):
+    """(batch_split, merge_segments) for the exact-objective merge (the GPU default of --auto_batch_split).
+
+    The DataLoader keeps the reference's micro-batches (``requested`` of them, each collated on its own); the
+    engine runs them in as few merged passes P as fit the memory model, P dividing ``requested``, each pass
+    holding ``merge_segments`` = requested / P micro-batches as loss segments — the reference objective at
+    merged-batch speed.  When even one micro-batch does not fit, the split is raised as ``plan_batch_split``
+    (merge=False) does and nothing is merged."""
+    requested = max(1, int(requested))
+    cap = max(max_micro_batch(cfg, seq_len, hbm_bytes, headroom), 1)
+    micro = train_batch_size // requested
+    if micro > cap:
+        return plan_batch_split(cfg, seq_len, train_batch_size, hbm_bytes, requested, headroom, merge=False), 1
+    for passes in range(1, requested + 1):
+        if requested % passes == 0 and (requested // passes) * micro <= cap:
+            return requested, requested // passes
+    return requested, 1
+
+
 def device_hbm_bytes(device=None) -> Optional[int]:
     """Total HBM of the current (or given) GPU; None without one."""
     import torch

@@ -127,6 +127,7 @@ class Trainer:
     torch_profile_dir: Optional[str] = None
     torch_profile_steps: str = "3:5"
     sampler_seed: int = 0   # per-epoch sampler permutation = f(sampler_seed, epoch): reproducible on resume
+    merge_segments: int = 1  # micro-batches per merged forward/backward pass (exact-objective merge, engine.py)
     extra_state: dict = field(default_factory=dict)
 
     def __post_init__(self):
@@ -163,10 +164,13 @@ class Trainer:
                                        allreduce_dtype=self.allreduce_dtype)
         self.engine = None
         if self.optimizer is not None:
+            G = max(1, int(self.merge_segments))
+            if self.batch_split % G:
+                raise ValueError(f"merge_segments {G} must divide batch_split {self.batch_split}")
             self.engine = TrainEngine(self.model, self.loss, self.optimizer, scheduler=self.scheduler,
                                       reducer=self.reducer, max_grad_norm=self.max_grad_norm,
-                                      batch_split=self.batch_split, no_sync_accum=self.no_sync_accum,
-                                      profile=self.profile, graph=self.cuda_graph)
+                                      batch_split=self.batch_split // G, no_sync_accum=self.no_sync_accum,
+                                      profile=self.profile, graph=self.cuda_graph, merge_segments=G)
         self.global_step = 0
         self.start_epoch = 1
         self.epoch_complete = True
@@ -274,6 +278,7 @@ class Trainer:
         self.optimizer.zero_grad()
         self._seed_sampler(epoch_i)
         self.engine.micro = 0
+        self.engine._pending = []
         avg = {}
         last_t, last_step = time.perf_counter(), self.global_step
         samples_per_step = self.train_batch_size * self.world

@@ -170,13 +170,16 @@ def get_trainer_parser() -> ArgumentParser:
                         help="1: all-reduce only at the accumulation boundary (fix of D1); 0: every micro-batch.")
     parser.add_argument("--dist_timeout", type=float, default=1800.0, help="Process-group timeout in seconds.")
     parser.add_argument("--auto_batch_split", type=_auto_split, default=None, nargs="?", const=True,
-                        help="GPU only.  Default (unset / True): raise --batch_split when a micro-batch "
-                             "train_batch_size // batch_split would not fit the HBM memory model (train/memory.py); "
-                             "never lowers it, so the objective is the reference's.  'merge': also LOWER it to the "
-                             "smallest split that fits (the reference's 128 micro-batches of 2 become one of 256 on a "
-                             "288 GB MI355X) — faster, but the span CE (ignore_index=-1, mean over valid spans), the "
-                             "weighted class CE and the batchmean KL are then normalised over the merged micro-batch "
-                             "instead of averaged per micro-batch.  False: off.")
+                        help="GPU only.  Default (unset / True): exact-objective merge — the micro-batches "
+                             "train_batch_size // batch_split are collated one by one as the reference does, then run "
+                             "in as few merged forward/backward passes as fit the HBM memory model (train/memory.py), "
+                             "the loss scoring each micro-batch as its own segment (its span length, its valid-span "
+                             "count, its class normaliser) and averaging them: the reference's mean of per-micro-batch "
+                             "means at merged speed (128 x 2 -> one pass of 256 on a 288 GB MI355X).  A micro-batch "
+                             "that does not fit raises the split.  'raise': one pass per micro-batch (only raises the "
+                             "split).  'merge': LOWER the split to the smallest that fits and collate merged batches "
+                             "— the losses are then normalised over the merged batch, not per micro-batch.  False: "
+                             "off.")
     parser.add_argument("--profile", action="store_true", help="Per-phase step timers + perf/* TB scalars.")
     parser.add_argument("--cuda_graph", type=_opt_bool, default=False, nargs="?", const=True,
                         help="GPU, bf16: capture each kind of micro-step (forward + backward; first / middle / last "
@@ -199,9 +202,10 @@ def get_trainer_parser() -> ArgumentParser:
 
 
 def _auto_split(v):
-    """--auto_batch_split: None / True (raise only), 'merge' (may lower the split), False (off)."""
-    if isinstance(v, str) and v.strip().lower() == "merge":
-        return "merge"
+    """--auto_batch_split: None / True (exact-objective merge), 'raise' (one pass per micro-batch, only raises the
+    split), 'merge' (lower the split, merged objective), False (off)."""
+    if isinstance(v, str) and v.strip().lower() in ("merge", "raise"):
+        return v.strip().lower()
     return _opt_bool(v)
 
 

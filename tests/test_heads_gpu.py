@@ -93,6 +93,37 @@ def test_fused_heads_and_loss_match_reference(cuda, kind, lw, B, L, H):
     _close(df, dr, "dseq", rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("kind,lw,S,b,L", [("ce", True, 4, 8, 96), ("focal", False, 3, 11, 64),
+                                           ("smooth", False, 128, 2, 512), ("ce", False, 2, 5, 40)])
+def test_fused_loss_segments_match_reference(cuda, kind, lw, S, b, L):
+    """Segment mode (exact-objective micro-batch merge): S segments of b samples with their own span lengths
+    L_s <= L — the loss kernel against the CPU-oracle segmented WeightedLoss (span softmax cut at L_s, every term
+    normalised per segment, averaged over segments)."""
+    NL, H = 5, 768
+    B = S * b
+    m = _model(cuda, H=H, NL=NL)
+    seq = (torch.randn(B, L, H, device=cuda) * 0.8).to(torch.bfloat16)
+    t = _targets(cuda, B, L, NL)
+    g = torch.Generator().manual_seed(5)
+    lens = [int(x) for x in torch.randint(L // 2, L + 1, (S,), generator=g)]
+    lens[0] = L
+    for s_ in range(S):   # each segment's targets lie inside its own length (or are ignored)
+        for k in ("start_class", "end_class"):
+            v = t[k][s_ * b:(s_ + 1) * b]
+            v[v >= lens[s_]] = lens[s_] - 1
+    if kind == "focal":
+        t["cls"][3] = -1
+    t["segments"] = torch.tensor(lens, dtype=torch.int32, device=cuda)
+    t["segment_lengths"] = tuple(lens)
+    of, lf, gf, df = _run(m, seq, t, _loss(kind, NL, lw), fused=True)
+    orf, lr, gr, dr = _run(m, seq, t, _loss(kind, NL, lw), fused=False)
+    for k in lr:
+        assert lf[k] == pytest.approx(lr[k], rel=2e-4, abs=1e-6), (k, lf[k], lr[k])
+    for k in gr:
+        _close(gf[k], gr[k], "grad " + k, rtol=1e-3, atol=1e-4)
+    _close(df, dr, "dseq", rtol=1e-2, atol=1e-2)
+
+
 def test_fused_heads_general_gradient_path(cuda):
     """Gradients that do not come from the fused loss (a custom objective) take the packed path."""
     B, L, H, NL = 20, 40, 768, 5
