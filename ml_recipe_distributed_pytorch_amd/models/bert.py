@@ -119,6 +119,7 @@ class _Ctx:
     def __init__(self, B, L, seed, training, model):
         self.B, self.L, self.seed, self.training, self.model = B, L, seed, training, model
         self.x8 = {}   # fp8 path: layer index -> its QKV input in e4m3 (written by the previous layer's LN)
+        self.head_mask = None   # [layers, H] per-column multipliers (each head's mask over its dh columns), or None
 
 
 class _EmbeddingFn(torch.autograd.Function):
@@ -206,6 +207,10 @@ class _LayerFn(torch.autograd.Function):
                                         Bm("attention.output.dense.bias"))
         else:
             ctxv, lse, bits = ops.attn_fwd(qkv, key_bias, B, L, nh, pa, info.seed, op0, scale)
+        # head_mask (HF: attention_probs *= head_mask[h]): scales head h's context, so the out-projection reads
+        # ctx ⊙ mvec; ctxv (the unmasked attention output) stays what the attention backward recomputes against
+        mvec = info.head_mask[idx] if info.head_mask is not None else None
+        ctx_in = ctxv if mvec is None else (ctxv.float() * mvec).to(ctxv.dtype)
         ln1 = (st.view(p + "attention.output.LayerNorm.weight", "master"),
                st.view(p + "attention.output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph, info.seed, op0 + 1)
         h1_8 = None
@@ -213,8 +218,8 @@ class _LayerFn(torch.autograd.Function):
             h1, z1, m1, r1, h1_8 = ops.ln_fwd_q8(a1, x, *ln1, s8["ffn1"], store_z=keep_z)
         else:   # out-projection + dropout + residual + LayerNorm (one GEMM epilogue + z-in LN under HQ_LN_FUSE=1)
             name = "attention.output.dense"
-            h1, z1, m1, r1 = ops.linear_bdr_ln_fwd(ctxv, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), x,
-                                                   kinds[name], *ln1, store_z=keep_z)
+            h1, z1, m1, r1 = ops.linear_bdr_ln_fwd(ctx_in, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"),
+                                                   x, kinds[name], *ln1, store_z=keep_z)
         act8 = None
         # bf16 act is only read by a bf16 FFN2 weight gradient: skipped (604 MB of stores at b256) when the
         # backward will run that weight gradient in fp8 from act8 (its gradient state calibrated by then)
@@ -249,6 +254,7 @@ class _LayerFn(torch.autograd.Function):
         ctx.f8 = (ctx8, h1_8, act8, x8) if (fp8 and act8 is not None and h1_8 is not None) else None
         ctx.bits = bits
         ctx.info, ctx.idx, ctx.ph, ctx.pa, ctx.scale = info, idx, ph, pa, scale
+        ctx.mvec = mvec
         return h2
 
     @staticmethod
@@ -343,12 +349,16 @@ class _LayerFn(torch.autograd.Function):
             dz1, da1, da1_8 = ops.ln_bwd_q8(*ln1b, s8["dout"], need, beta=beta1)
         else:
             dz1, da1 = ops.ln_bwd(*ln1b, beta=beta1)
-        wgrad(da1, ctxv, G("attention.output.dense.weight"), None,
+        mvec = ctx.mvec
+        ctx_in = ctxv if mvec is None else (ctxv.float() * mvec).to(ctxv.dtype)   # what the out-projection read
+        wgrad(da1, ctx_in, G("attention.output.dense.weight"), None,
               (da1_8, s8["dout"], f8[0], s8["out"]) if f8 else None)
         if fp8 and s8["dout"].calibrated:
             dctx = ops.linear_dgrad_fp8(da1_8, s8["dout"], W8T("attention.output.dense.weight"))
         else:
             dctx = ops.linear_dgrad(da1, W("attention.output.dense.weight"), wt=WT("attention.output.dense.weight"))
+        if mvec is not None:   # d(ctx ⊙ m)/d ctx: a masked head passes no gradient into its attention
+            dctx = (dctx.float() * mvec).to(dctx.dtype)
         bpart = None
         if fp8:   # calibrated: e5m2 dQKV only (+ QKV bias-gradient partials), the fp8 QKV wgrad reads it with x8
             need = not (s8["dqkv"].step >= 1 and (f8 is not None or not trainable))
@@ -575,7 +585,25 @@ class BertForQuestionAnswering(nn.Module):
     def encode(self, input_ids, attention_mask=None, token_type_ids=None, position_ids=None):
         return self._encode(input_ids, attention_mask, token_type_ids, position_ids)[0]
 
-    def _encode(self, input_ids, attention_mask=None, token_type_ids=None, position_ids=None):
+    def _head_mask_columns(self, head_mask):
+        """HF ``get_head_mask`` shapes — [nh] (every layer) or [layers, nh] — as per-layer column multipliers
+        [layers, H] (head h covers columns h·dh … h·dh+dh-1 of the attention context); None when all ones."""
+        cfg = self.config
+        nh, NL = cfg.num_attention_heads, cfg.num_hidden_layers
+        hm = torch.as_tensor(head_mask, dtype=torch.float32, device=self.store.device)
+        if hm.dim() == 1:
+            hm = hm.unsqueeze(0).expand(NL, nh)
+        hm = hm.reshape(NL, nh) if hm.numel() == NL * nh else None
+        if hm is None:
+            raise ValueError(f"head_mask must have {nh} or {NL}x{nh} elements, got shape {tuple(head_mask.shape)}")
+        if bool((hm == 1).all()):
+            return None
+        if self.precision == "fp8" and self.store.device.type == "cuda":
+            raise NotImplementedError("head_mask with --precision fp8 (the fp8 out-projection reads the attention "
+                                      "kernel's e4m3 context directly)")
+        return hm.repeat_interleave(cfg.head_dim, dim=1).contiguous()
+
+    def _encode(self, input_ids, attention_mask=None, token_type_ids=None, position_ids=None, head_mask=None):
         cfg = self.config
         B, L = input_ids.shape
         if L > cfg.max_position_embeddings - cfg.position_offset:
@@ -591,6 +619,8 @@ class BertForQuestionAnswering(nn.Module):
             key_bias = (1.0 - attention_mask.to(dev, torch.float32)) * -10000.0
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if self.training else 0
         info = _Ctx(B, L, seed, self.training, self)
+        if head_mask is not None:
+            info.head_mask = self._head_mask_columns(head_mask)
         anchor_e = self.store.params["transformer.embeddings.word_embeddings.weight"]
         h = _EmbeddingFn.apply(anchor_e, ids, pos, tt, info)
         for i in range(cfg.num_hidden_layers):
@@ -599,9 +629,9 @@ class BertForQuestionAnswering(nn.Module):
         return h.view(B, L, cfg.hidden_size), seed
 
     def forward(self, input_ids, attention_mask=None, token_type_ids=None, position_ids=None, head_mask=None):
-        if head_mask is not None:
-            raise NotImplementedError("head_mask is not supported by the fused encoder")
-        seq, seed = self._encode(input_ids, attention_mask, token_type_ids, position_ids)
+        """``head_mask`` (reference ``model.py:43-48`` → HF BertModel): [nh] or [layers, nh] multipliers of each
+        head's attention probabilities; a zero head contributes nothing and receives no gradient."""
+        seq, seed = self._encode(input_ids, attention_mask, token_type_ids, position_ids, head_mask)
         if fused_heads_available(self, seq):
             return fused_heads(self, seq, seed, self.training)
         if torch.is_grad_enabled() and self._fresh.get("head", True):

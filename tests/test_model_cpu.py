@@ -162,3 +162,47 @@ def test_grad_accumulation_and_zero_grad():
     m.zero_grad()
     m(ids, mask, tt)["cls"].sum().backward()
     torch.testing.assert_close(m.store.grad, g1, atol=1e-6, rtol=1e-6)
+
+
+@pytest.mark.parametrize("shape", ["layers", "heads"])
+def test_head_mask_scales_each_heads_context(shape):
+    """head_mask (reference model.py:43-48; HF multiplies head h's attention probabilities by m_h): the output
+    equals the unmasked model with the out-projection columns of head h scaled by m_h, a zero head passes no
+    gradient into its Q/K/V, and the mask [nh] applies to every layer.  (transformers 5.x dropped head_mask,
+    so the oracle is that algebraic identity.)"""
+    cfg = get_config("bert-tiny-test", hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    nh, NL, dh = cfg.num_attention_heads, cfg.num_hidden_layers, cfg.head_dim
+    a = BertForQuestionAnswering(cfg, precision="fp32", seed=3)
+    b = copy.deepcopy(a)
+    if shape == "layers":
+        hm = torch.rand(NL, nh) * 2
+        hm[0, 0] = 0.0
+    else:
+        hm = torch.rand(nh) * 2
+        hm[0] = 0.0
+    full = hm if hm.dim() == 2 else hm.unsqueeze(0).expand(NL, nh)
+    cols = full.repeat_interleave(dh, dim=1)
+    with torch.no_grad():
+        for i in range(NL):
+            b.store.params[f"transformer.encoder.layer.{i}.attention.output.dense.weight"].mul_(cols[i])
+    b.store.mark_master_dirty()
+    ids, mask, tt = _batch(cfg)
+    oa = a(ids, mask, tt, head_mask=hm)
+    ob = b(ids, mask, tt)
+    for k in oa:
+        torch.testing.assert_close(oa[k], ob[k], atol=1e-5, rtol=1e-4, msg=k)
+    w = {k: torch.randn_like(v) for k, v in oa.items()}
+    sum((oa[k] * w[k]).sum() for k in oa).backward()
+    sum((ob[k] * w[k]).sum() for k in ob).backward()
+    pb = dict(b.named_parameters())
+    for n, p in a.named_parameters():
+        g = pb[n].grad
+        if n.endswith("attention.output.dense.weight"):
+            g = g * cols[int(n.split(".")[3])]
+        torch.testing.assert_close(p.grad, g, atol=1e-5, rtol=1e-4, msg=n)
+    # the zero head of layer 0 gets no gradient in its query / key / value rows
+    q = a.store.params["transformer.encoder.layer.0.attention.self.query.weight"].grad
+    assert float(q[:dh].abs().max()) == 0.0 and float(q[dh:].abs().max()) > 0.0
+    # all-ones is the unmasked model
+    torch.testing.assert_close(a(ids, mask, tt, head_mask=torch.ones(nh))["start_class"],
+                               a(ids, mask, tt)["start_class"])

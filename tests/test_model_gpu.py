@@ -28,7 +28,13 @@ def test_tiny_model_gpu_matches_cpu(cuda, train, B, side):
     _tiny_parity(cuda, train, B=B, side=side)
 
 
-def _tiny_parity(cuda, train, B, side=False):
+def test_head_mask_gpu_matches_cpu(cuda):
+    """head_mask on the HIP path (masked context into the out-projection GEMM, masked dctx into the attention
+    backward) against the CPU reference path of the same weights."""
+    _tiny_parity(cuda, True, B=4, head_mask=torch.tensor([[0.0, 1.5], [1.0, 0.5]]))
+
+
+def _tiny_parity(cuda, train, B, side=False, head_mask=None):
     cfg = get_config("bert-tiny-test")
     cpu = BertForQuestionAnswering(cfg, seed=0)
     gpu = copy.deepcopy(cpu).to(cuda)
@@ -38,9 +44,10 @@ def _tiny_parity(cuda, train, B, side=False):
     gpu.train(train)
     ids, mask, tt = _inputs(B, 64, cfg.vocab_size)
     torch.manual_seed(11)
-    oc = cpu(ids, mask, tt)
+    kw = {} if head_mask is None else {"head_mask": head_mask}
+    oc = cpu(ids, mask, tt, **kw)
     torch.manual_seed(11)
-    og = gpu(ids.to(cuda), mask.to(cuda), tt.to(cuda))
+    og = gpu(ids.to(cuda), mask.to(cuda), tt.to(cuda), **kw)
     for key in oc:
         a, b = og[key].float().cpu(), oc[key].float()  # classifier dropout: same counter-hash mask on both
         assert (a - b).abs().max().item() < 5e-2 * (1 + b.abs().max().item()), key
