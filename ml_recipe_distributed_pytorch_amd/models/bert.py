@@ -192,8 +192,11 @@ class _LayerFn(torch.autograd.Function):
         # e4m3 inputs written here are kept for those weight gradients.
         fp8 = fp8 and ops.fp8_gemm_ok(x.shape[0], 3 * cfg.hidden_size, cfg.hidden_size)
         s8 = m.fp8_states(idx) if fp8 else None
-        # LayerNorm z only when the backward needs it (ops.LN_FROM_Y: recomputed from y on the GPU)
+        # LayerNorm z only when the backward needs it (ops.LN_FROM_Y: recomputed from y on the GPU, for the
+        # LayerNorms whose weights pass the |β| <= R·|γ| guard, BertForQuestionAnswering.refresh_ln_modes)
         keep_z = not (x.is_cuda and ops.LN_FROM_Y)
+        keep_z1 = keep_z or not m.ln_from_y_ok(idx, 0)
+        keep_z2 = keep_z or not m.ln_from_y_ok(idx, 1)
         if fp8:
             x8 = info.x8.pop(idx, None)
             if x8 is None:
@@ -215,11 +218,11 @@ class _LayerFn(torch.autograd.Function):
                st.view(p + "attention.output.LayerNorm.bias", "master"), cfg.layer_norm_eps, ph, info.seed, op0 + 1)
         h1_8 = None
         if fp8:
-            h1, z1, m1, r1, h1_8 = ops.ln_fwd_q8(a1, x, *ln1, s8["ffn1"], store_z=keep_z)
+            h1, z1, m1, r1, h1_8 = ops.ln_fwd_q8(a1, x, *ln1, s8["ffn1"], store_z=keep_z1)
         else:   # out-projection + dropout + residual + LayerNorm (one GEMM epilogue + z-in LN under HQ_LN_FUSE=1)
             name = "attention.output.dense"
             h1, z1, m1, r1 = ops.linear_bdr_ln_fwd(ctx_in, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"),
-                                                   x, kinds[name], *ln1, store_z=keep_z)
+                                                   x, kinds[name], *ln1, store_z=keep_z1)
         act8 = None
         # bf16 act is only read by a bf16 FFN2 weight gradient: skipped (604 MB of stores at b256) when the
         # backward will run that weight gradient in fp8 from act8 (its gradient state calibrated by then)
@@ -239,13 +242,13 @@ class _LayerFn(torch.autograd.Function):
             a2 = ops.linear_fwd_fp8_own(act8, s8["ffn2"], W8("output.dense"), Bm("output.dense.bias"))
             if idx + 1 < cfg.num_hidden_layers:  # the next layer's QKV input, in e4m3
                 h2, z2, m2, r2, info.x8[idx + 1] = ops.ln_fwd_q8(a2, h1, *ln2, m.fp8_states(idx + 1)["qkv"],
-                                                                 store_z=keep_z)
+                                                                 store_z=keep_z2)
             else:
-                h2, z2, m2, r2 = ops.ln_fwd(a2, h1, *ln2, store_z=keep_z)
+                h2, z2, m2, r2 = ops.ln_fwd(a2, h1, *ln2, store_z=keep_z2)
         else:   # FFN2 + dropout + residual + LayerNorm (one GEMM epilogue + z-in LN under HQ_LN_FUSE=1)
             name = "output.dense"
             h2, z2, m2, r2 = ops.linear_bdr_ln_fwd(act, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), h1,
-                                                   kinds[name], *ln2, store_z=keep_z)
+                                                   kinds[name], *ln2, store_z=keep_z2)
         # a LayerNorm without z (None) recomputes x̂ from its output y (h1 / h2) in the backward
         ctx.save_for_backward(x, key_bias, qkv, ctxv, lse, z1, m1, r1, h1, pre, act, z2, m2, r2,
                               h2 if z2 is None else None)
@@ -570,7 +573,37 @@ class BertForQuestionAnswering(nn.Module):
         res = super().load_state_dict(state_dict, strict=strict)
         self.store.mark_master_dirty()
         self.store.sync_compute()
+        self._ln_y = None   # new LayerNorm weights: re-run the from-y guard before the next forward
         return res
+
+    # -------------------------------------------------------------------- LayerNorm-from-y guard
+    # The memory-efficient LayerNorm backward recomputes x̂ = (y − β)/γ from the bf16 output y; y's rounding
+    # (2⁻⁹·|y|, |y| <= |γ|·|x̂| + |β|) puts 2⁻⁹·(|x̂| + |β/γ|) into x̂ — the same class as the stored-z form's
+    # 2⁻⁹·|z|·rstd while |β/γ| stays O(|x̂|), but unbounded for a small-|γ| column (γ = 0: x̂ is lost).
+    # Random-init weights (γ = 1, β = 0) always pass; pretrained checkpoints are checked column by column.
+    LN_FROM_Y_MAX_RATIO = 8.0
+
+    def _ln_names(self):
+        return [f"transformer.encoder.layer.{i}.{k}" for i in range(self.config.num_hidden_layers)
+                for k in ("attention.output.LayerNorm", "output.LayerNorm")]
+
+    def refresh_ln_modes(self) -> bool:
+        """Re-evaluate, per encoder LayerNorm, whether the from-y backward is safe: every column has γ != 0 and
+        |β| <= LN_FROM_Y_MAX_RATIO·|γ|; a LayerNorm that fails stores z instead.  One small device→host read.
+        Returns True when a LayerNorm changed mode (a captured HIP graph must then be re-captured)."""
+        names = self._ln_names()
+        g = torch.stack([self.store.view(n + ".weight", "master") for n in names]).abs()
+        b = torch.stack([self.store.view(n + ".bias", "master") for n in names]).abs()
+        ok = ((g > 0) & (b <= self.LN_FROM_Y_MAX_RATIO * g)).all(1).tolist()
+        old = getattr(self, "_ln_y", None)
+        self._ln_y = [bool(v) for v in ok]
+        return old is not None and old != self._ln_y
+
+    def ln_from_y_ok(self, idx: int, which: int) -> bool:
+        """Layer ``idx``'s LayerNorm ``which`` (0 = attention output, 1 = FFN output) may skip storing z."""
+        if getattr(self, "_ln_y", None) is None:
+            self.refresh_ln_modes()
+        return self._ln_y[2 * idx + which]
 
     # -------------------------------------------------------------------- forward
     def _position_ids(self, input_ids, position_ids):

@@ -131,6 +131,8 @@ class TrainEngine:
         self._graph_pool = None                 # one private mempool shared by every capture
         self._graph_warm = 0
         self.graph_replays = 0
+        self._steps = 0
+        self.ln_check_every = 100   # optimizer steps between re-runs of the LayerNorm-from-y weight guard
         self.graph_eager_steps = 0              # micro-steps of an uncaptured shape run eagerly beside the graphs
 
     @property
@@ -232,6 +234,14 @@ class TrainEngine:
             return None
         return self._apply()
 
+    def _check_ln_modes(self):
+        """Fine-tuning moves γ / β: re-run the model's LayerNorm-from-y guard (one tiny device→host read every
+        ``ln_check_every`` steps); a LayerNorm that changes mode invalidates the captured graphs."""
+        from .. import ops
+        refresh = getattr(self.model, "refresh_ln_modes", None)
+        if refresh is not None and ops.LN_FROM_Y and refresh() and self._graphs:
+            self.release_graph()
+
     def release_graph(self):
         if self._graphs:
             self.model.use_device_seed(False)
@@ -302,6 +312,9 @@ class TrainEngine:
         if self.scheduler is not None:
             self.scheduler.step()
         timer.mark("optim")
+        self._steps += 1
+        if self._steps % self.ln_check_every == 0 and self.device.type == "cuda":
+            self._check_ln_modes()
         return StepResult(losses=self.loss_fn.last, grad_norm=norm, lr=lr, timings=timer.resolve())
 
     def step(self, micro_batches) -> StepResult:

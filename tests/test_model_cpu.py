@@ -206,3 +206,21 @@ def test_head_mask_scales_each_heads_context(shape):
     # all-ones is the unmasked model
     torch.testing.assert_close(a(ids, mask, tt, head_mask=torch.ones(nh))["start_class"],
                                a(ids, mask, tt)["start_class"])
+
+
+def test_ln_from_y_guard_flags():
+    """The LayerNorm-from-y guard: a LayerNorm whose weights have a column with γ = 0 or |β| > 8·|γ| (typical of
+    pretrained checkpoints' small-γ columns) stores z; random-init weights never trip it; loading new weights
+    re-runs it."""
+    cfg = get_config("bert-tiny-test")
+    m = BertForQuestionAnswering(cfg, precision="fp32", seed=1)
+    assert [m.ln_from_y_ok(i, w) for i in range(2) for w in (0, 1)] == [True] * 4
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    sd["transformer.encoder.layer.1.attention.output.LayerNorm.weight"][7] = 1e-3
+    sd["transformer.encoder.layer.1.attention.output.LayerNorm.bias"][7] = 0.5
+    sd["transformer.encoder.layer.0.output.LayerNorm.weight"][3] = 0.0
+    m.load_state_dict(sd)
+    assert [m.ln_from_y_ok(i, w) for i in range(2) for w in (0, 1)] == [True, False, False, True]
+    with torch.no_grad():   # an optimizer moving the weights back: refresh reports the change
+        m.store.params["transformer.encoder.layer.1.attention.output.LayerNorm.bias"][7] = 0.005
+    assert m.refresh_ln_modes() is True and m.ln_from_y_ok(1, 0)
