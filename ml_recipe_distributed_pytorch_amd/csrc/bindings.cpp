@@ -732,9 +732,6 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("gemm_set_variant", [](int64_t v) { hq_gemm_set_variant((int)v); });
   m.def("gemm_set_stagger", [](int64_t v) { hq_gemm_set_stagger((int)v); });
   m.def("gemm_set_sched", [](int64_t v) { hq_gemm_set_sched((int)v); });
-  m.def("cu_hog", [](int64_t blocks, int64_t usec) {
-    hq_cu_hog((int)blocks, (int)usec, cur_stream());
-  });
   m.def("gemm_tn", &gemm_tn, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("accumulate") = false,
         py::arg("splits") = 0, py::arg("bias_out") = py::none());
   m.def("gemm_tn_splits", &gemm_tn_splits);

@@ -105,6 +105,20 @@ def build_kernels(jobs: int = 8, force: bool = False, verbose: bool = True, debu
     return out
 
 
+def build_diag(verbose: bool = True) -> str:
+    """``tools/diag/_hq_diag.so``: diagnostic kernels that are not part of the production library (the CU-hog
+    spin kernel of the GEMM schedule contention test), plain C ABI for ctypes."""
+    src = os.path.join(os.path.dirname(PKG), "tools", "diag", "cu_hog.hip")
+    out = os.path.join(os.path.dirname(src), "_hq_diag.so")
+    obj = _compile(src, ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}"], HIPCC, False)
+    _sh([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", out + ".tmp", obj,
+         "-L" + os.path.join(ROCM, "lib"), "-lamdhip64"])
+    os.replace(out + ".tmp", out)
+    if verbose:
+        print(f"[hq-build] {out}")
+    return out
+
+
 def _unicode_tables() -> str:
     gen_dir = os.path.join(BUILD, "gen")
     os.makedirs(gen_dir, exist_ok=True)
@@ -147,6 +161,7 @@ def main(argv=None):
         build_host(a.j, a.force)
     if a.kernels or both:
         build_kernels(a.j, a.force, debug=a.debug)
+        build_diag()
 
 
 if __name__ == "__main__":

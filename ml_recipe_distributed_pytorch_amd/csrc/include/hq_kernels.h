@@ -103,7 +103,6 @@ void hq_gemm_set_stagger(int v);   // v3 start offset of half the workgroups (un
 void hq_gemm_set_sched(int v);
 // Diagnostic: `blocks` workgroups (one per CU: 96 KiB LDS each) that spin for `usec` µs on stream s —
 // stands in for a collective kernel holding CUs while a GEMM runs (tools/gemm_contention_bench.py)
-void hq_cu_hog(int blocks, int usec, hipStream_t s);
 // C[M,N] = A[M,K]·B[N,K]^T (+epilogue); P = GELU pre-activation (out for EPI_GELU, in for EPI_DGELU)
 // or its derivative gelu'(pre) (out for EPI_GELUD, in for EPI_DMUL);
 // R = residual (EPI_RESID, EPI_BDR); part = [M/256][N] column partial sums (EPI_DGELU)

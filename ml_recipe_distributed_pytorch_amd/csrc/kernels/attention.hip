@@ -267,21 +267,6 @@ __device__ __forceinline__ void colsum_row64(float* dst, const f32x16_t (&a)[2],
   }
 }
 
-// Static issue priority of a workgroup's waves for the whole main loop (MI355X_MICROARCH "Two waves per
-// SIMD", item 4): VALU issue on a SIMD goes to the higher-priority, then the older wave.  g_attn_prio
-// (host: HQ_ATTN_PRIO) 0 = off, 1 = second half of the waves at prio 1, 2 = three levels (3 waves/SIMD).
-__device__ int g_attn_prio = 0;
-// forward online softmax: tolerated growth (log2 units) of a row max before a rescale (host: HQ_ATTN_DEFER)
-__device__ float g_attn_defer = 8.f;
-__device__ __forceinline__ void wave_prio(int wave, int nw) {
-  const int mode = g_attn_prio;
-  if (mode == 1) {
-    if (wave >= nw / 2) __builtin_amdgcn_s_setprio(1);
-  } else if (mode == 2) {
-    if (wave >= (2 * nw) / 3) __builtin_amdgcn_s_setprio(2);
-    else if (wave >= nw / 3) __builtin_amdgcn_s_setprio(1);
-  }
-}
 
 // Packed-f32 pair (v_pk_add/mul/fma_f32 on gfx950: two lanes' worth of f32 work per VALU issue).
 typedef float f2_t __attribute__((ext_vector_type(2)));
@@ -1080,20 +1065,6 @@ size_t hq_attn_mask_bytes(int B, int L, int nh) {
   return (size_t)B * nh * n32 * n32 * 64 * sizeof(uint16_t);
 }
 
-static void set_attn_prio() {
-  static const bool once = [] {
-    const char* e = getenv("HQ_ATTN_PRIO");
-    const int v = e ? atoi(e) : 0;
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_prio), &v, sizeof(int));
-    const char* d = getenv("HQ_ATTN_DEFER");
-    if (d) {
-      const float f = (float)atof(d);
-      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_defer), &f, sizeof(float));
-    }
-    return true;
-  }();
-  (void)once;
-}
 
 // HQ_ATTN_FORCE_SLOW=1 / attn_set_force_slow(1): every workgroup of the ring forward takes its slow path
 // (tests only: the rare rescale branch gets its own coverage, kernel playbook rule 26)
@@ -1106,7 +1077,6 @@ void hq_attn_set_force_slow(int v) { g_attn_force_slow = v ? 1 : 0; }
 void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, float* lse, uint16_t* mbits, int B, int L,
                  int nh, int dh, float p, uint32_t seed, uint32_t opid, float scale, hipStream_t s, uint8_t* ctx8,
                  float* q8, int phase) {
-  set_attn_prio();
   if (dh != D || L > 512) { fprintf(stderr, "hq_attn_fwd: head_dim %d / L %d unsupported\n", dh, L); abort(); }
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const HqDropKey key = hq_drop_key(seed, opid);
@@ -1153,7 +1123,6 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
 void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx, const float* lse, const float* key_bias,
                  const uint16_t* mbits, uint16_t* dqkv, float* delta, int B, int L, int nh, int dh, float p,
                  float scale, bool deterministic, hipStream_t s, uint8_t* dqkv8, float* q8, int phase, float* bpart) {
-  set_attn_prio();
   if (dh != D || L > 512) { fprintf(stderr, "hq_attn_bwd: head_dim %d / L %d unsupported\n", dh, L); abort(); }
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const float ks = hq_keep_scale(thr);

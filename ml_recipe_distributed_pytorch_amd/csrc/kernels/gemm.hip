@@ -1225,22 +1225,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   }
 }
 
-// 0 = auto (v3 for K <= 2304, else v2), 1 = force v1, 2 = force v2, 3 = force v3; HQ_GEMM_VARIANT sets it
-int g_gemm_variant = [] {
-  const char* e = getenv("HQ_GEMM_VARIANT");
-  return e ? atoi(e) : 0;
-}();
-// v3 start offset of odd workgroups per XCD, in units of s_sleep(127) (HQ_GEMM_STAGGER, bits 0-7) and
-// the epilogue A/B knobs (HQ_GEMM_EPIFLAGS, bits 8-15); both 0 in production
-// bit 16 (kHalfTail): v3 runs a last, at most half-full wave of tiles as 128-row half tiles (on by default;
-// HQ_GEMM_HALFTAIL=0 turns it off for A/B)
+// 0 = auto (v3 for K <= 2304, else v2), 1 = force v1, 2 = force v2, 3 = force v3, 4 = force vS; set only by
+// the tests / lab tools through gemm_set_variant (no environment knob)
+int g_gemm_variant = 0;
+// v3 flag word (gemm_set_stagger, tests / lab tools only): start offset of odd workgroups per XCD in units of
+// s_sleep(127) (bits 0-7) and the epilogue diagnostics (bits 8-15), both 0 in production; bit 16 (kHalfTail):
+// a last, at most half-full wave of tiles runs as 128-row half tiles (on)
 constexpr int kHalfTail = 1 << 16;
-int g_gemm_stagger = [] {
-  const char* e = getenv("HQ_GEMM_STAGGER");
-  const char* f = getenv("HQ_GEMM_EPIFLAGS");
-  const char* h = getenv("HQ_GEMM_HALFTAIL");
-  return (e ? atoi(e) & 0xFF : 0) | ((f ? atoi(f) & 0xFF : 0) << 8) | (h && !atoi(h) ? 0 : kHalfTail);
-}();
+int g_gemm_stagger = kHalfTail;
 
 // default static: uncontended the dynamic schedule costs ~0.9 % of the step (profiles/r2_sched); GradReducer
 // switches it on when an all-reduce overlaps the backward (world > 1); HQ_GEMM_SCHED overrides either way

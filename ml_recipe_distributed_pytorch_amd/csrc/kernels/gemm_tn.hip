@@ -459,11 +459,8 @@ int hq_gemm_tn_splits(int T, int N, int K) {
   if (S < 1) S = 1;
   const int nkt = (T + BT - 1) / BT;
   // K-tiles per block kept (prologue amortised): 4 (micro-batch 2 x 512: 388 -> 400 samples/s vs 8, batch
-  // 64 neutral; batch 256 never splits that far); HQ_TN_MIN_KT: A/B
-  static const int min_kt = [] {
-    const char* e = getenv("HQ_TN_MIN_KT");
-    return e ? std::max(1, atoi(e)) : 4;
-  }();
+  // 64 neutral; batch 256 never splits that far)
+  constexpr int min_kt = 4;
   while (S > 1 && nkt / S < min_kt) --S;
   if (nkt < 2) return 0;
   return S;

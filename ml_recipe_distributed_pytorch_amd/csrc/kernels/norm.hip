@@ -754,11 +754,7 @@ void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, con
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const HqDropKey key = hq_drop_key(seed, opid);
   const float ks = hq_keep_scale(thr);
-  static const int rpw = [] {   // rows per wave (HQ_LN_RPW = 1 / 2 / 4: A/B sweeps)
-    const char* e = getenv("HQ_LN_RPW");
-    const int v = e ? atoi(e) : 2;
-    return v == 1 || v == 4 ? v : 2;
-  }();
+  constexpr int rpw = 2;   // rows per wave (1 / 2 / 4 measured: profiles/r3_ln_rpw)
   const int grid = (T + kWaves * rpw - 1) / (kWaves * rpw);
   float* part8 = y8 ? hq_fp8_amax_parts((size_t)grid * kWaves) : nullptr;
   dispatch_nch(H, [&](auto nch) {

@@ -219,7 +219,7 @@ class _LayerFn(torch.autograd.Function):
         h1_8 = None
         if fp8:
             h1, z1, m1, r1, h1_8 = ops.ln_fwd_q8(a1, x, *ln1, s8["ffn1"], store_z=keep_z1)
-        else:   # out-projection + dropout + residual + LayerNorm (one GEMM epilogue + z-in LN under HQ_LN_FUSE=1)
+        else:   # out-projection + dropout + residual + LayerNorm (one GEMM epilogue + z-in LN under ops.LN_FUSE)
             name = "attention.output.dense"
             h1, z1, m1, r1 = ops.linear_bdr_ln_fwd(ctx_in, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"),
                                                    x, kinds[name], *ln1, store_z=keep_z1)
@@ -245,7 +245,7 @@ class _LayerFn(torch.autograd.Function):
                                                                  store_z=keep_z2)
             else:
                 h2, z2, m2, r2 = ops.ln_fwd(a2, h1, *ln2, store_z=keep_z2)
-        else:   # FFN2 + dropout + residual + LayerNorm (one GEMM epilogue + z-in LN under HQ_LN_FUSE=1)
+        else:   # FFN2 + dropout + residual + LayerNorm (one GEMM epilogue + z-in LN under ops.LN_FUSE)
             name = "output.dense"
             h2, z2, m2, r2 = ops.linear_bdr_ln_fwd(act, st.view(p + name + ".weight"), Bb(name), Bm(name + ".bias"), h1,
                                                    kinds[name], *ln2, store_z=keep_z2)

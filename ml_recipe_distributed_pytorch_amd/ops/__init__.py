@@ -151,11 +151,11 @@ def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale
 # There is no vendor-BLAS fallback: a shape the kernels do not tile raises instead of silently running
 # something else (BERT / RoBERTa base and large, and the tiny test config, all tile).
 _EPI_NONE, _EPI_BIAS, _EPI_GELU, _EPI_DGELU, _EPI_RESID, _EPI_GELUD, _EPI_DMUL, _EPI_BDR = range(8)
-# HQ_LN_FUSE=1: the out-projection / FFN2 GEMM writes z = dropout(x·Wᵀ + b) + resid itself (EPI_BDR) and the
+# LN_FUSE: the out-projection / FFN2 GEMM writes z = dropout(x·Wᵀ + b) + resid itself (EPI_BDR) and the
 # LayerNorm that follows reads z alone — one HBM pass over [T, H] less per LayerNorm, bitwise the same
 # result.  Off by default: the epilogue's residual read and dropout hash are serial with the persistent GEMM's
 # MFMA work and cost what the LayerNorm saves (same-box step A/B 3847 vs 3839 samples/s, profiles/r2_ln_fuse)
-LN_FUSE = os.environ.get("HQ_LN_FUSE", "0") == "1"
+LN_FUSE = False   # module attribute (tests/test_ln_fuse_gpu.py toggles it); no environment knob
 # The encoder LayerNorms' forward skips storing z (151 MB per LayerNorm at B = 256, L = 384) and the backward
 # recomputes x̂ = (y − β)/γ from the output y, which the next sublayer keeps anyway (the "memory-efficient"
 # LayerNorm backward).  HQ_LN_FROM_Y=0 keeps z (x̂ = (z − mean)·rstd, the exact-input form).
@@ -188,7 +188,7 @@ def linear_fwd(x, w, b, b32=None, kind: str = "plain"):
 
 def linear_bdr_ln_fwd(x, w, b, b32, resid, kind, gamma, beta, eps, p, seed, opid, store_z: bool = True):
     """LayerNorm(dropout_p(x·Wᵀ + b) + resid) -> (y, z, mean, rstd), bitwise what ``linear_fwd`` followed by
-    ``ln_fwd`` computes.  On the GPU with ``HQ_LN_FUSE=1`` the GEMM's EPI_BDR epilogue adds the dropped-out
+    ``ln_fwd`` computes.  On the GPU with ``LN_FUSE`` the GEMM's EPI_BDR epilogue adds the dropped-out
     projection to the residual and stores z, and the LayerNorm reads z alone (``ln_fwd`` with resid=None);
     otherwise the two ops run as before."""
     if x.is_cuda and LN_FUSE and x.shape[0] * w.shape[0] < 2 ** 32:

@@ -6,6 +6,7 @@ import pytest
 import torch
 
 from ml_recipe_distributed_pytorch_amd import _native
+from tools.diag import cu_hog
 
 EPI_BIAS, EPI_RESID, EPI_GELUD, EPI_DMUL = 1, 4, 5, 6
 # grids above 2 x 256 workgroups (the dynamic schedule's range): 768, 555 and 1152 tiles of 256² (555 and 1152 end in a
@@ -64,7 +65,7 @@ def test_dynamic_schedule_bitwise_equals_static(cuda, sched_reset, M, N, K, epi)
     for rep in range(3):   # counters must be re-zeroed by the previous launch
         if rep == 2:       # tiles move to other workgroups while 32 CUs are held on another stream
             with torch.cuda.stream(side):
-                k.cu_hog(32, 150)
+                cu_hog(32, 150)
         got = _run(A, B, epi, kw)
         torch.cuda.synchronize()
         for r, g in zip(ref, got):

@@ -1,7 +1,8 @@
-// Diagnostics that are not part of any training step: the CU-occupying spin kernel of the GEMM tile
-// schedule contention test (tests/test_gemm_sched_gpu.py, tools/gemm_contention_bench.py).
-#include "hq_common.h"
-#include "hq_kernels.h"
+// Diagnostic kernel, not part of any training step (kept out of the production _hq_kernels library): the
+// CU-occupying spin kernel of the GEMM tile-schedule contention test (tests/test_gemm_sched_gpu.py,
+// tools/gemm_contention_bench.py).  Built into tools/diag/_hq_diag.so by csrc/build.py build_diag(), loaded
+// with ctypes (tools/diag/__init__.py).
+#include <hip/hip_runtime.h>
 
 namespace {
 
@@ -16,12 +17,13 @@ __global__ __launch_bounds__(256) void cu_hog_kernel(long ticks) {
 
 }  // namespace
 
-void hq_cu_hog(int blocks, int usec, hipStream_t s) {
+extern "C" int hq_cu_hog(int blocks, int usec, void* stream) {
   constexpr int lds = 96 * 1024;
   static bool init = [] {
     (void)hipFuncSetAttribute((const void*)cu_hog_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     return true;
   }();
   (void)init;
-  hipLaunchKernelGGL(cu_hog_kernel, dim3(blocks), dim3(256), lds, s, (long)usec * 100);
+  hipLaunchKernelGGL(cu_hog_kernel, dim3(blocks), dim3(256), lds, static_cast<hipStream_t>(stream), (long)usec * 100);
+  return (int)hipGetLastError();
 }

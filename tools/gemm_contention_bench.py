@@ -21,6 +21,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ml_recipe_distributed_pytorch_amd import _native  # noqa: E402
+from tools.diag import cu_hog  # noqa: E402
 
 SHAPES = (  # name, N, K, epi  (M = 98304 tokens: BERT-base, batch 256 x 384)
     ("ffn1_fwd_gelud", 3072, 768, 5),
@@ -78,7 +79,7 @@ def main():
                     torch.cuda.synchronize()
                     if h:
                         with torch.cuda.stream(side):
-                            k.cu_hog(h, a.usec)
+                            cu_hog(h, a.usec)
                     e0.record(main_s)
                     k.gemm_nt(A, B, epi, **kw)
                     e1.record(main_s)
