@@ -17,7 +17,7 @@
 //   fwd : blocks [0, npool)  pooled tiles (32 samples × 64 outputs, K staged through LDS), epilogue
 //                            tanh + per-tile partial dot products of the small heads; the LAST pooled
 //                            block to finish (agent-scope ticket) folds the partials → cls / reg;
-//         blocks [npool, …)  one wave per sequence row: span logits.
+//         blocks [npool, …)  kSpanFwdRPW sequence rows per wave: span logits.
 //   loss: blocks [0, nrow)   one wave per sample: online log-sum-exp over L for start AND end
 //                            (float2 rows), CE value + gradient (softmax − onehot)·w/n written in place;
 //         block nrow         class + regression losses and gradients for all samples;
@@ -38,6 +38,9 @@ namespace {
 constexpr int kHS = 16;      // row stride of dheads / head partials: [0, NL) class logits, 8 / 9 = reg start / end
 constexpr int kMaxNL = 8;
 constexpr int kSpanRPW = 16; // span rows per wave in the backward (64 rows per block)
+constexpr int kSpanFwdRPW = 8;  // span rows per wave in the forward: all loads issued before the dot products
+                                // (one row per wave was latency-bound at the pooled path's LDS occupancy:
+                                // 102 µs for 151 MB at T = 98304)
 
 __device__ __forceinline__ float keep_mult(uint32_t idx, uint32_t key, uint32_t thr, float ks) {
   return thr ? (hq_keep(idx, key, thr) ? ks : 0.f) : 1.f;
@@ -86,24 +89,39 @@ __global__ __launch_bounds__(256) void qa_heads_fwd_kernel(FwdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int H = a.H;
   if ((int)blockIdx.x >= a.npool) {  // ---------------------------------------------- span rows
-    const int row = ((int)blockIdx.x - a.npool) * 4 + wv;
-    if (row >= a.T) return;
-    float s0 = 0.f, s1 = 0.f;
+    const int row0 = (((int)blockIdx.x - a.npool) * 4 + wv) * kSpanFwdRPW;
+    if (row0 >= a.T) return;
+    uint2 raw[kSpanFwdRPW][NCH];
+#pragma unroll
+    for (int r = 0; r < kSpanFwdRPW; ++r)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int col = c * 256 + lane * 4;
+        raw[r][c] = row0 + r < a.T && col < H ? *reinterpret_cast<const uint2*>(a.seq + (size_t)(row0 + r) * H + col)
+                                              : make_uint2(0u, 0u);
+      }
+    float4 u[NCH], v[NCH];
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = c * 256 + lane * 4;
-      if (col < H) {
-        float x[4];
-        hq_unpack4(*reinterpret_cast<const uint2*>(a.seq + (size_t)row * H + col), x);
-        const float4 u = *reinterpret_cast<const float4*>(a.wsp + col);
-        const float4 v = *reinterpret_cast<const float4*>(a.wsp + H + col);
-        s0 += x[0] * u.x + x[1] * u.y + x[2] * u.z + x[3] * u.w;
-        s1 += x[0] * v.x + x[1] * v.y + x[2] * v.z + x[3] * v.w;
-      }
+      u[c] = col < H ? *reinterpret_cast<const float4*>(a.wsp + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[c] = col < H ? *reinterpret_cast<const float4*>(a.wsp + H + col) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    s0 = hq_wave_sum(s0);
-    s1 = hq_wave_sum(s1);
-    if (lane == 0) *reinterpret_cast<float2*>(a.logits + 2 * (size_t)row) = make_float2(s0 + a.bsp[0], s1 + a.bsp[1]);
+#pragma unroll
+    for (int r = 0; r < kSpanFwdRPW; ++r) {
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        float x[4];
+        hq_unpack4(raw[r][c], x);
+        s0 += x[0] * u[c].x + x[1] * u[c].y + x[2] * u[c].z + x[3] * u[c].w;
+        s1 += x[0] * v[c].x + x[1] * v[c].y + x[2] * v[c].z + x[3] * v[c].w;
+      }
+      s0 = hq_wave_sum(s0);
+      s1 = hq_wave_sum(s1);
+      if (lane == 0 && row0 + r < a.T)
+        *reinterpret_cast<float2*>(a.logits + 2 * (size_t)(row0 + r)) = make_float2(s0 + a.bsp[0], s1 + a.bsp[1]);
+    }
     return;
   }
   // ---------------------------------------------------------------------------- pooled tile
@@ -678,7 +696,7 @@ void hq_qa_heads_fwd(const uint16_t* seq, const HqHeadWeights& w, float* logits,
   a.thr = p > 0.f ? hq_threshold(p) : 0u;
   a.kd = hq_drop_key(seed, opid);
   a.ks = hq_keep_scale(a.thr);
-  const int nspan = (a.T + 3) / 4;
+  const int nspan = (a.T + 4 * kSpanFwdRPW - 1) / (4 * kSpanFwdRPW);
   const size_t lds = (32 * 64 + 64 * 65) * sizeof(float);
   dispatch_nch(H, [&](auto nch) {
     hipLaunchKernelGGL(qa_heads_fwd_kernel<decltype(nch)::value>, dim3(a.npool + nspan), dim3(256), lds, s, a);
