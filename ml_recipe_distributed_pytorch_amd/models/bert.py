@@ -650,8 +650,11 @@ class BertForQuestionAnswering(nn.Module):
             key_bias = torch.zeros(B, L, dtype=torch.float32, device=dev)
         else:
             key_bias = (1.0 - attention_mask.to(dev, torch.float32)) * -10000.0
-        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if self.training else 0
-        info = _Ctx(B, L, seed, self.training, self)
+        # per-module train/eval as the reference's finetune mode sets it (model.eval() + .train() on the trainable
+        # modules, trainer.py:227-234): the encoder's dropout follows `transformer`, the classifier's `classifier`
+        enc_train = self.transformer.training
+        seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if (enc_train or self.classifier.training) else 0
+        info = _Ctx(B, L, seed, enc_train, self)
         if head_mask is not None:
             info.head_mask = self._head_mask_columns(head_mask)
         anchor_e = self.store.params["transformer.embeddings.word_embeddings.weight"]
@@ -666,14 +669,14 @@ class BertForQuestionAnswering(nn.Module):
         head's attention probabilities; a zero head contributes nothing and receives no gradient."""
         seq, seed = self._encode(input_ids, attention_mask, token_type_ids, position_ids, head_mask)
         if fused_heads_available(self, seq):
-            return fused_heads(self, seq, seed, self.training)
+            return fused_heads(self, seq, seed, self.classifier.training)
         if torch.is_grad_enabled() and self._fresh.get("head", True):
             # autograd accumulates into the arena views: clear the head range once per fresh step
             s, e = self._head_range
             self.store.grad[s:e].zero_()
             self._fresh["head"] = False
         span = _SpanHeadFn.apply if seq.is_cuda and seq.dtype == torch.bfloat16 else None
-        return reference_heads(self, seq, seed, self.training, span_fn=span)
+        return reference_heads(self, seq, seed, self.classifier.training, span_fn=span)
 
 
 def load_pretrained(model: BertForQuestionAnswering, path: str) -> List[str]:

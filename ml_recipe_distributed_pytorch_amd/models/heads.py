@@ -68,13 +68,13 @@ def head_views(store, which: str) -> List[torch.Tensor]:
 
 
 def fused_heads_possible(model) -> bool:
-    """The model's forward will take the fused head kernels on a bf16 GPU sequence (config / flags only)."""
+    """The model's forward will take the fused head kernels on a bf16 GPU sequence (config / flags only).
+    Frozen head parameters (``--finetune_*``, reference D16) are fine: the backward kernel's gradients for them
+    are cleared again, so they never reach the grad norm, the reducer or the optimizer."""
     cfg = model.config
     if os.environ.get("HQ_FUSED_HEADS", "1") == "0":
         return False
-    if cfg.hidden_size % 64 or cfg.hidden_size > 2048 or not 1 <= cfg.num_labels <= 8:
-        return False
-    return all(model.store.params[k].requires_grad for k in _W_KEYS)
+    return not (cfg.hidden_size % 64 or cfg.hidden_size > 2048 or not 1 <= cfg.num_labels <= 8)
 
 
 def fused_heads_available(model, seq: torch.Tensor) -> bool:
@@ -126,6 +126,9 @@ class _FusedHeadsFn(torch.autograd.Function):
         dseq = kernels().qa_heads_bwd(seq, L, dlog.view(-1, 2), dheads, gscale, st.pooled, st.reg,
                                       head_views(m.store, "master"), head_views(m.store, "grad"), acc, st.p, st.seed,
                                       HEAD_DROPOUT_OPID)
+        for k in _W_KEYS:   # frozen heads (finetune modes): no gradient, as autograd would leave them
+            if not m.store.params[k].requires_grad:
+                m.store.view(k, "grad").zero_()
         m._group_ready("head")
         return dseq, None, None
 
@@ -138,7 +141,8 @@ def fused_heads(model, seq: torch.Tensor, seed: int, training: bool) -> HeadOutp
     logits, pooled, cls, reg = kernels().qa_heads_fwd(seq, L, head_views(model.store, "master"), p, seed,
                                                       HEAD_DROPOUT_OPID)
     st = _FusedState(model, B, L, model.config.num_labels, seed, p, logits, pooled, cls, reg)
-    anchor = model.store.params["transformer.pooler.dense.weight"]
+    P = model.store.params
+    anchor = next((P[k] for k in _W_KEYS if P[k].requires_grad), P[_W_KEYS[0]])   # any trainable head parameter
     if torch.is_grad_enabled() and (seq.requires_grad or anchor.requires_grad):
         s, e, rs, re_, c = _FusedHeadsFn.apply(seq, anchor, st)
     else:

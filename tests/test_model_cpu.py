@@ -224,3 +224,23 @@ def test_ln_from_y_guard_flags():
     with torch.no_grad():   # an optimizer moving the weights back: refresh reports the change
         m.store.params["transformer.encoder.layer.1.attention.output.LayerNorm.bias"][7] = 0.005
     assert m.refresh_ln_modes() is True and m.ln_from_y_ok(1, 0)
+
+
+def test_finetune_module_train_modes():
+    """Reference finetune mode (init.py:86-92, trainer.py:227-234): model.eval() and .train() on the trainable
+    modules only — the encoder's dropout follows `transformer`, the classifier dropout follows `classifier`."""
+    cfg = get_config("bert-tiny-test")
+    m = BertForQuestionAnswering(cfg, precision="fp32", seed=1)
+    ids, mask, tt = _batch(cfg)
+    m.eval()
+    ref = m(ids, mask, tt)
+    m.classifier.train()   # finetune_class only: encoder deterministic, classifier dropout on
+    torch.manual_seed(0)
+    a = m(ids, mask, tt)
+    torch.testing.assert_close(a["start_class"], ref["start_class"])
+    assert not torch.allclose(a["cls"], ref["cls"])
+    m.eval()
+    m.transformer.train()  # finetune_transformer: encoder dropout on
+    torch.manual_seed(0)
+    b = m(ids, mask, tt)
+    assert not torch.allclose(b["start_class"], ref["start_class"])
