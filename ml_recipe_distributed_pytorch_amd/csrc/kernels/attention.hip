@@ -271,6 +271,12 @@ __device__ __forceinline__ void colsum_row64(float* dst, const f32x16_t (&a)[2],
 // Packed-f32 pair (v_pk_add/mul/fma_f32 on gfx950: two lanes' worth of f32 work per VALU issue).
 typedef float f2_t __attribute__((ext_vector_type(2)));
 
+// x if bit `pos` of w is set, else +0: v_bfe_i32 sign-extends the bit to an all-ones / all-zero word and one
+// v_and_b32 applies it (2 VALU per element instead of a bit test, a compare and a select)
+__device__ __forceinline__ float keep_and(float x, uint32_t w, int pos) {
+  return __uint_as_float(__float_as_uint(x) & (uint32_t)__builtin_amdgcn_sbfe((int)w, (unsigned)pos, 1u));
+}
+
 // lane ^ 32 exchange without LDS: v_permlane32_swap hands each half the other half's value.
 __device__ __forceinline__ float xor32_max(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -818,18 +824,18 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
 #pragma unroll
     for (int s = 1; s < 4; ++s) p_acc = mfma32(row8(tV, 0, lo_, s), of[s], p_acc);
     uint32_t bits = 0xFFFFu;
-    float ksc = 1.f;
+    f2_t ksc = {1.f, 1.f};
     if constexpr (DROP) {
       bits = (uint32_t)my_bits[kt * 64];
-      ksc = kscale;
+      ksc = f2_t{kscale, kscale};
     }
     float ds[16];
 #pragma unroll
-    for (int r = 0; r < 16; r += 2) {  // dS = P·(dP·mask − δ)
+    for (int r = 0; r < 16; r += 2) {  // dS = P·(dP·mask·ksc − δ): mask as an all-ones/zero AND (v_bfe_i32)
       const f2_t P = {__builtin_amdgcn_exp2f(s_acc[r]), __builtin_amdgcn_exp2f(s_acc[r + 1])};
-      const f2_t mk = {((bits >> r) & 1u) ? ksc : 0.f, ((bits >> (r + 1)) & 1u) ? ksc : 0.f};
-      const f2_t dp = {p_acc[r], p_acc[r + 1]};
-      const f2_t v = (dp * mk - dl2) * P;
+      f2_t dp = {p_acc[r], p_acc[r + 1]};
+      if constexpr (DROP) dp = f2_t{keep_and(dp.x, bits, r), keep_and(dp.y, bits, r + 1)};
+      const f2_t v = (dp * ksc - dl2) * P;
       ds[r] = v.x; ds[r + 1] = v.y;
     }
 #pragma unroll
@@ -965,6 +971,7 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
   const int hh_f = (krel >> 2) & 1;
   const int r_f = (krel & 3) + 4 * (krel >> 3);
   const float ksc = DROP ? kscale : 1.f;
+  const f2_t ksc2 = {ksc, ksc};
   constexpr int UNR = NT > 0 ? NT : 1;
 #pragma unroll UNR
   for (int t = 0; t < n32; ++t) {
@@ -992,22 +999,34 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
 #pragma unroll
         for (int gg = 0; gg < 2; ++gg) {
           const int g = 2 * s + gg;
-          uint32_t lo = 0xFFFFFFFFu, hi = 0xFFFFFFFFu;
-          if constexpr (DROP) {
-            const uint64_t w = *reinterpret_cast<const uint64_t*>(wsrc + 8 * g);
-            lo = (uint32_t)w >> r_f;
-            hi = (uint32_t)(w >> 32) >> r_f;
-          }
           const float4 d4 = *reinterpret_cast<const float4*>(sdl + 8 * g + 4 * hh);
-          const float mk[4] = {(lo & 1u) ? ksc : 0.f, ((lo >> 16) & 1u) ? ksc : 0.f, (hi & 1u) ? ksc : 0.f,
-                               ((hi >> 16) & 1u) ? ksc : 0.f};
-          const float dl[4] = {d4.x, d4.y, d4.z, d4.w};
+          const f2_t dl[2] = {f2_t{d4.x, d4.y}, f2_t{d4.z, d4.w}};
+          float P[4], dp[4];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const int r = 4 * g + i;
-            const float P = __builtin_amdgcn_exp2f(s_acc[r]);
-            pd[4 * gg + i] = P * mk[i];
-            dsv[4 * gg + i] = (p_acc[r] * mk[i] - dl[i]) * P;
+            P[i] = __builtin_amdgcn_exp2f(s_acc[4 * g + i]);
+            dp[i] = p_acc[4 * g + i];
+          }
+          // keep bits as AND masks: pd = P·mask (kscale is applied once, at the dV store), dS = P·(dP·mask·ksc − δ)
+          float pm[4] = {P[0], P[1], P[2], P[3]};
+          if constexpr (DROP) {
+            const uint64_t w = *reinterpret_cast<const uint64_t*>(wsrc + 8 * g);
+            const uint32_t wl = (uint32_t)w, wh = (uint32_t)(w >> 32);
+            const int pos[4] = {r_f, r_f + 16, r_f, r_f + 16};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              pm[i] = keep_and(P[i], i < 2 ? wl : wh, pos[i]);
+              dp[i] = keep_and(dp[i], i < 2 ? wl : wh, pos[i]);
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const f2_t Pj = {P[2 * j], P[2 * j + 1]}, dpj = {dp[2 * j], dp[2 * j + 1]};
+            const f2_t v = (dpj * ksc2 - dl[j]) * Pj;
+            pd[4 * gg + 2 * j] = pm[2 * j];
+            pd[4 * gg + 2 * j + 1] = pm[2 * j + 1];
+            dsv[4 * gg + 2 * j] = v.x;
+            dsv[4 * gg + 2 * j + 1] = v.y;
           }
         }
         const bf16x8_t pb = pack_b(pd, 0), sb = pack_b(dsv, 0);
@@ -1037,7 +1056,7 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
     const float inv8 = 1.f / hq_fp8_delayed_scale(q8, phase, kHqBf8Max);
     float amax = 0.f;
     if (active && kok) {
-      amax = store_row64_e5<MODE == 1>(dqkv + orow_k + 2 * H, dqkv8 + orow_k + 2 * H, dv, 1.f, inv8, hh);
+      amax = store_row64_e5<MODE == 1>(dqkv + orow_k + 2 * H, dqkv8 + orow_k + 2 * H, dv, ksc, inv8, hh);
       amax = fmaxf(amax, store_row64_e5<MODE == 1>(dqkv + orow_k + H, dqkv8 + orow_k + H, dk, LN2, inv8, hh));
     }
     amax = hq_wave_max(amax);
@@ -1045,7 +1064,7 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
     if constexpr (MODE == 2) {
       if (active) {   // every key subtile < n32 is active (L ≤ 32·n32): each partial row is written once
         float* row = bpart + ((size_t)b * n32 + ks_idx) * 3 * H + h * D;
-        colsum_row64(row + 2 * H, dv, 1.f, kok, lane, hh);
+        colsum_row64(row + 2 * H, dv, ksc, kok, lane, hh);
         colsum_row64(row + H, dk, LN2, kok, lane, hh);
       }
     }
@@ -1053,7 +1072,7 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
   }
   if (active && kok) {
     uint16_t* out = dqkv + orow_k;
-    store_row64(out + 2 * H, dv, 1.f, hh);
+    store_row64(out + 2 * H, dv, ksc, hh);   // pd carried the mask only
     store_row64(out + H, dk, LN2, hh);                   // Q' = c·Q with c = scale·log2e: dK = Σ dS·Q'/log2e
   }
 }

