@@ -1,0 +1,93 @@
+"""Run-to-run bitwise stability of the hot kernels at the headline shapes (BERT-base, B = 256, L = 384).
+
+Every kernel here is deterministic (no atomics; split-K partials are reduced in a fixed order), so repeated
+launches on the same inputs must agree bit for bit.  A launch that does not is corrupting data at random —
+the signature of round 4's late store-data read (profiles/r4_epi1: a dwordx4 store picked up a VALU result
+written 5 instructions after it issued, ~3e-5 of the GELU epilogue's elements, different ones each run),
+which tolerance checks against an fp32 oracle only catch when a corrupted value happens to be large."""
+import pytest
+import torch
+
+from ml_recipe_distributed_pytorch_amd import _native
+
+EPI_NONE, EPI_BIAS, EPI_GELU, EPI_DGELU, EPI_RESID, EPI_GELUD, EPI_DMUL = range(7)
+T, H, F = 256 * 384, 768, 3072
+REPS = 4
+
+
+def _bf(shape, gen, dev, scale=1.0):
+    return (torch.randn(*shape, device=dev, generator=gen) * scale).bfloat16()
+
+
+def _same(outs, what):
+    for i, o in enumerate(outs[1:], 1):
+        for a, b in zip(outs[0], o):
+            diff = (a.view(torch.int16) != b.view(torch.int16)) if a.dtype == torch.bfloat16 else (a != b)
+            n = int(diff.sum())
+            assert n == 0, f"{what}: launch {i} differs from launch 0 in {n} of {a.numel()} elements"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["qkv_bias", "ffn1_gelud", "ffn1_gelu", "ffn2_dmul", "attn_out_resid", "qkv_dgrad"])
+def test_gemm_nt_repeatable(cuda, name):
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(7)
+    x = _bf((T, H), g, cuda, 0.5)
+    n_out = {"qkv_bias": 3 * H, "ffn1_gelud": F, "ffn1_gelu": F, "ffn2_dmul": F, "attn_out_resid": H,
+             "qkv_dgrad": H}[name]
+    a = x if name != "qkv_dgrad" else _bf((T, 3 * H), g, cuda, 0.5)
+    k_dim = a.shape[1]
+    w = _bf((n_out, k_dim), g, cuda, 0.05)
+    bias = torch.randn(n_out, device=cuda, generator=g) * 0.1
+    outs = []
+    for _ in range(REPS):
+        if name == "qkv_bias":
+            outs.append((k.gemm_nt(a, w, EPI_BIAS, bias=bias),))
+        elif name in ("ffn1_gelud", "ffn1_gelu"):
+            pre = torch.empty(T, n_out, device=cuda, dtype=torch.bfloat16)
+            epi = EPI_GELUD if name == "ffn1_gelud" else EPI_GELU
+            outs.append((k.gemm_nt(a, w, epi, bias=bias, pre=pre), pre))
+        elif name == "ffn2_dmul":
+            gd = _bf((T, n_out), torch.Generator(device=cuda).manual_seed(11), cuda)
+            part = torch.zeros(k.gemm_nt_part_rows(T, n_out, k_dim) * n_out, device=cuda)
+            outs.append((k.gemm_nt(a, w, EPI_DMUL, pre=gd, part=part), part))
+        elif name == "attn_out_resid":
+            r = _bf((T, n_out), torch.Generator(device=cuda).manual_seed(13), cuda)
+            outs.append((k.gemm_nt(a, w, EPI_RESID, resid=r),))
+        else:
+            outs.append((k.gemm_nt(a, w, EPI_NONE),))
+    torch.cuda.synchronize()
+    _same(outs, name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_out,k_in", [(F, H), (H, F), (3 * H, H)])
+def test_gemm_tn_repeatable(cuda, n_out, k_in):
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(5)
+    dy, x = _bf((T, n_out), g, cuda), _bf((T, k_in), g, cuda)
+    outs = []
+    for _ in range(REPS):
+        out, b = torch.zeros(n_out, k_in, device=cuda), torch.zeros(n_out, device=cuda)
+        k.gemm_tn(dy, x, out, False, 0, b)
+        outs.append((out, b))
+    torch.cuda.synchronize()
+    _same(outs, f"gemm_tn {n_out}x{k_in}")
+
+
+@pytest.mark.gpu
+def test_attention_repeatable(cuda):
+    k = _native.kernels()
+    B, L, nh = 256, 384, 12
+    g = torch.Generator(device=cuda).manual_seed(3)
+    qkv = _bf((B * L, 3 * H), g, cuda)
+    kb = torch.zeros(B, L, device=cuda)
+    kb[:, 300:] = -10000.0
+    dctx = _bf((B * L, H), g, cuda)
+    outs = []
+    for _ in range(REPS):
+        ctx, lse, bits = k.attn_fwd(qkv, kb, B, L, nh, 0.1, 555, 3, 0.125)
+        dq = k.attn_bwd(dctx, qkv, ctx, lse, kb, bits, B, L, nh, 0.1, 0.125, False)
+        outs.append((ctx, lse, bits, dq))
+    torch.cuda.synchronize()
+    _same(outs, "attention")
