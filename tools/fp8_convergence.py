@@ -10,8 +10,11 @@ number of delayed-scaling productions whose fresh amax exceeded the range of the
 quantisation: e4m3 448, e5m2 57344).  At the end: the reference's eval metrics on the held-out split (MAP over
 the class softmax, start / end / class accuracy; MAPCallback + AccuracyCallback).
 
-    python tools/fp8_convergence.py --precision bf16 --out gpurun_out/r4_fp8_conv
-    python tools/fp8_convergence.py --precision fp8  --out gpurun_out/r4_fp8_conv
+    python tools/fp8_convergence.py --precision bf16 --seed 0 --out gpurun_out/r4_fp8_conv
+    python tools/fp8_convergence.py --precision fp8  --seed 0 --out gpurun_out/r4_fp8_conv
+
+Two seeds per precision (tools/gpu/r4_fp8_conv.sh) separate fp8's effect from run-to-run divergence: the
+seed sets the init and the sample order, identical for both precisions.
 """
 from __future__ import annotations
 
@@ -19,6 +22,7 @@ import argparse
 import json
 import os
 import sys
+import tempfile
 import time
 from collections import defaultdict
 from types import SimpleNamespace
@@ -27,9 +31,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def prepare(out, n_docs, seed):
+def prepare(d, n_docs, seed):
     from ml_recipe_distributed_pytorch_amd.data.synth_nq import learnable_vocab, write_jsonl
-    d = os.path.join(out, "data")
     os.makedirs(d, exist_ok=True)
     vocab = learnable_vocab(os.path.join(d, "vocab.txt"))
     data = os.path.join(d, "nq_learnable.jsonl")
@@ -38,18 +41,20 @@ def prepare(out, n_docs, seed):
     return vocab, data, os.path.join(d, "processed")
 
 
-def saturation(model):
+def saturation(model, by_site=None):
     """Productions (since the last call) whose amax overflowed the scale in use: state.buf = [amax slots 0-2,
-    dequant scale in use]; the slot of the last phase holds the fresh amax of that production."""
+    dequant scale in use]; the slot of the last phase holds the fresh amax of that production.  by_site
+    (dict) accumulates the count per quantisation site and the worst overflow factor."""
     import torch
     states = getattr(model, "_fp8_states", {})
-    bufs, lims = [], []
-    for st in states.values():
+    bufs, lims, names = [], [], []
+    for mod, st in states.items():
         for k, s in st.items():
             if s.step == 0:
                 continue
             bufs.append(s.buf)
             lims.append((57344.0 if s.grad else 448.0, (s.step - 1) % 3))
+            names.append(f"{mod}/{k}")
     if not bufs:
         return 0, 0
     b = torch.stack(bufs).cpu()
@@ -58,6 +63,9 @@ def saturation(model):
         amax, scale = float(b[i, ph]), float(b[i, 3])
         if scale > 0 and amax / scale > lim * (1 + 1e-6):
             n += 1
+            if by_site is not None:
+                c, worst = by_site.get(names[i], (0, 0.0))
+                by_site[names[i]] = (c + 1, max(worst, amax / scale / lim))
     return n, len(lims)
 
 
@@ -71,6 +79,8 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--max_seq_len", type=int, default=384)
     ap.add_argument("--out", default="gpurun_out/r4_fp8_conv")
+    ap.add_argument("--data_dir", default=os.path.join(tempfile.gettempdir(), "hq_fp8_conv_data"),
+                    help="synthetic corpus + preprocessing cache (thousands of files: keep it out of --out)")
     a = ap.parse_args()
 
     import torch
@@ -85,7 +95,7 @@ def main():
     from ml_recipe_distributed_pytorch_amd.data.items import LABELS
 
     os.makedirs(a.out, exist_ok=True)
-    vocab, data, proc = prepare(a.out, a.n_docs, 1234)
+    vocab, data, proc = prepare(a.data_dir, a.n_docs, 1234)
     dev = torch.device("cuda", 0)
     mp = SimpleNamespace(model="bert-base-uncased", hidden_dropout_prob=0.1, attention_probs_dropout_prob=0.1,
                          layer_norm_eps=1e-12, vocab_file=vocab, merges_file=None, lowercase=True,
@@ -110,6 +120,7 @@ def main():
                         collate_fn=collate, drop_last=True, num_workers=4)
     log = []
     sat_total = prod_total = 0
+    sat_sites, sat_steps = {}, []
     t0 = time.time()
     step = 0
     model.train()
@@ -122,8 +133,10 @@ def main():
             rec["step"] = step
             rec["L"] = int(inputs["input_ids"].shape[1])
             if a.precision == "fp8":
-                s, n = saturation(model)
+                s, n = saturation(model, sat_sites)
                 rec["fp8_saturated"], rec["fp8_productions"] = s, n
+                if s:
+                    sat_steps.append(step)
                 sat_total += s
                 prod_total += n
             log.append(rec)
@@ -146,10 +159,14 @@ def main():
             tl.append(float(loss_fn(preds, labels)))
             for cb in cbs:
                 cb.at_iteration_end(preds, labels, meters)
+    # test_loss: the mean over batches with a finite loss (a batch whose span targets are all ignored has an
+    # empty mean, NaN by definition); the count of such batches is reported beside it
     for cb in cbs:
         cb.at_epoch_end(meters, None)
     ev = {k: (v() if isinstance(v, AverageMeter) else v) for k, v in meters.items()}
-    ev["test_loss"] = sum(tl) / max(1, len(tl))
+    finite = [x for x in tl if x == x]
+    ev["test_loss"] = sum(finite) / max(1, len(finite))
+    ev["test_batches_nan_loss"] = len(tl) - len(finite)
     last = log[-20:]
     summary = {"precision": a.precision, "steps": step, "batch": a.batch, "lr": a.lr, "seed": a.seed,
                "train_windows": len(train_ds), "test_windows": len(test_ds), "train_seconds": round(train_s, 1),
@@ -158,10 +175,14 @@ def main():
     if a.precision == "fp8":
         summary["fp8_saturated_productions"] = sat_total
         summary["fp8_productions_checked"] = prod_total
-    with open(os.path.join(a.out, f"curve_{a.precision}.jsonl"), "w") as f:
+        summary["fp8_saturated_steps"] = {"first": sat_steps[:10], "count": len(sat_steps),
+                                          "after_step_50": sum(1 for x in sat_steps if x > 50)}
+        top = sorted(sat_sites.items(), key=lambda kv: -kv[1][0])[:12]
+        summary["fp8_saturated_sites_top"] = {k: {"count": c, "worst_overflow": round(w, 2)} for k, (c, w) in top}
+    with open(os.path.join(a.out, f"curve_{a.precision}_s{a.seed}.jsonl"), "w") as f:
         for r in log:
             f.write(json.dumps(r) + "\n")
-    with open(os.path.join(a.out, f"summary_{a.precision}.json"), "w") as f:
+    with open(os.path.join(a.out, f"summary_{a.precision}_s{a.seed}.json"), "w") as f:
         json.dump(summary, f, indent=1, default=float)
     print(json.dumps(summary, default=float), flush=True)
 
