@@ -92,6 +92,43 @@ def test_ln_bwd_from_y(cuda, H, T, p):
     _close(gg[1], ggz[1], 5e-2 * (T / 1000) ** 0.5, 1e-3, "dbeta vs the exact-input oracle")
 
 
+@pytest.mark.parametrize("T", [1000, 24576])
+def test_ln_bwd_from_y_guarded_range(cuda, T):
+    """The from-y backward across pretrained-like LayerNorm weights: γ log-uniform over [1e-3, 2], β ~ N(0, 0.5).
+    The model's guard (BertForQuestionAnswering.refresh_ln_modes) admits a LayerNorm for the from-y backward only
+    if EVERY column has γ != 0 and |β| <= LN_FROM_Y_MAX_RATIO·|γ|; with these weights it must reject (the model
+    then stores z: exact).  Within the admitted region — β clipped to ±8|γ|, every γ magnitude of the range —
+    the from-y gradients must match the exact-input oracle to the rounding model of x̂ = (y − β)/γ: y is bf16,
+    so |δx̂| <= (|x̂| + |β/γ|)·2⁻⁸ per element, and dγ = Σ_t g·x̂ collects it as a random walk over T rows."""
+    from ml_recipe_distributed_pytorch_amd.models.bert import BertForQuestionAnswering
+    ratio = BertForQuestionAnswering.LN_FROM_Y_MAX_RATIO
+    k = _native.kernels()
+    torch.manual_seed(11)
+    H = 768
+    a, r = _bf(torch.randn(T, H)), _bf(torch.randn(T, H))
+    gamma = torch.exp(torch.empty(H).uniform_(math.log(1e-3), math.log(2.0)))
+    beta = torch.randn(H) * 0.5
+    admitted = beta.abs() <= ratio * gamma
+    assert not bool(admitted.all()), "the guard must reject this LayerNorm (it then keeps z)"
+    beta = torch.where(admitted, beta, ratio * gamma * torch.sign(beta))   # the worst admitted weights
+    y, z, m, rs = k.ln_fwd(a.to(cuda), r.to(cuda), gamma.to(cuda), beta.to(cuda), 1e-12, 0.0, 99, 4)
+    y2, _, m2, rs2 = k.ln_fwd(a.to(cuda), r.to(cuda), gamma.to(cuda), beta.to(cuda), 1e-12, 0.0, 99, 4, store_z=False)
+    dy, dy2 = _bf(torch.randn(T, H)), _bf(torch.randn(T, H))
+    gg = [torch.zeros(H, device=cuda) for _ in range(3)]
+    ggz = [torch.zeros(H) for _ in range(3)]
+    dz, _ = k.ln_bwd(dy.to(cuda), dy2.to(cuda), y2, gamma.to(cuda), m2, rs2, 0.0, 99, 4, gg[0], gg[1], gg[2], False,
+                     beta=beta.to(cuda))
+    dzz, _ = ref.ln_bwd(dy, dy2, z.cpu(), gamma, m.cpu(), rs.cpu(), 0.0, 99, 4, ggz[0], ggz[1], ggz[2], False)
+    _close(dz, dzz, 5e-2, 3e-2, "dz vs the exact-input oracle")
+    _close(gg[1], ggz[1], 5e-2 * (T / 1000) ** 0.5, 1e-3, "dbeta vs the exact-input oracle")
+    # per-column dγ bound: 4σ of the random walk Σ_t g_t·δx̂_t with |δx̂_t| <= (|x̂_t| + |β/γ|)·2⁻⁸
+    xh = (z.cpu().float() - m.cpu().float()[:, None]) * rs.cpu().float()[:, None]
+    g = (dy.float() + dy2.float())
+    bound = 4.0 * 2.0 ** -8 * torch.sqrt(((g * (xh.abs() + (beta / gamma).abs()[None, :])) ** 2).sum(0)) + 1e-2
+    err = (gg[0].cpu() - ggz[0]).abs()
+    assert bool((err <= bound).all()), f"dgamma: {int((err > bound).sum())} columns beyond the rounding bound"
+
+
 @pytest.mark.parametrize("H,ntypes", [(768, 2), (128, 1)])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("layout", ["flat", "seq", "seq_randpos"])
