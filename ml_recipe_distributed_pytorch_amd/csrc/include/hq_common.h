@@ -207,12 +207,18 @@ __device__ __forceinline__ void hq_keep4(uint32_t idx0, uint32_t key, uint32_t t
 // ------------------------------------------------------------------------------ fp8 (OCP e4m3) delayed scaling
 // 4-float state per quantisation site: slots 0-2 rotate as (this step's amax, next step's (cleared), last
 // step's amax) by phase = step % 3; state[3] = the scale this step's e4m3 tensor was written with.
-// s = 2·amax_prev / 448 (unit scale before the first amax exists).
+// s = margin·amax_prev / fmax (unit scale before the first amax exists), margin 2 for the e4m3 forward inputs
+// and 64 for the e5m2 gradients: a gradient's amax moves by more than 2× from one step to the next (measured,
+// profiles/r4_fp8_conv: 9 % of the gradient productions overflowed a 2× margin, by up to 37×), and e5m2's
+// 30-binade exponent range affords the 5 binades that a 64× margin takes off its bottom.
 constexpr float kHqFp8Max = 448.f;      // OCP e4m3 (forward activations / weights)
 constexpr float kHqBf8Max = 57344.f;    // OCP e5m2 (backward activation gradients)
+constexpr float kHqFp8Margin = 2.f;
+constexpr float kHqBf8Margin = 64.f;
 __device__ __forceinline__ float hq_fp8_delayed_scale(const float* st, int phase, float fmax = kHqFp8Max) {
   const float prev = __uint_as_float(reinterpret_cast<const unsigned*>(st)[(phase + 2) % 3]);
-  return prev > 0.f ? prev * 2.f / fmax : 1.f;
+  const float margin = fmax == kHqBf8Max ? kHqBf8Margin : kHqFp8Margin;
+  return prev > 0.f ? prev * margin / fmax : 1.f;
 }
 // 4 values -> 4 e5m2 bytes (x·inv, saturated to ±57344)
 __device__ __forceinline__ uint32_t hq_pack_bf8x4(const float* f, float inv) {

@@ -174,7 +174,7 @@ __device__ __forceinline__ float store_row64_q8(uint16_t* out, uint8_t* out8, co
 // store_row64 plus an e5m2 copy (x·inv8) at out8 for the backward's dQ / dK / dV (the fp8 QKV dgrad's
 // input), quantised from the fp32 values (one rounding; the bf16 copy is rounded separately): the four
 // fp8 bytes of each 4-column half are packed BEFORE the permlane32 swap, so one swap of one dword places
-// them like the bf16 words.  Saturation (only needed when this step's amax outgrew the delayed scale's 2×
+// them like the bf16 words.  Saturation (only needed when this step's amax outgrew the delayed scale's 64×
 // headroom) runs as a wave-uniform branch.  Returns this lane's |max| for the amax.
 __device__ __forceinline__ uint32_t bf8x4_raw(float a, float b, float c, float d) {
   const uint32_t w = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
@@ -189,7 +189,7 @@ __device__ __forceinline__ float store_row64_e5(uint16_t* out, uint8_t* out8, co
 #pragma unroll
     for (int r = 0; r < 16; r += 2) amax = fmaxf(amax, fmaxf(fabsf(a[d][r]), fabsf(a[d][r + 1])));
   amax *= fabsf(mul);
-  // rare: this step's amax outgrew the scale's headroom — the fp8 copy saturates to ±57344 (e5m2 would
+  // rare: this step's amax outgrew the scale's 64× headroom — the fp8 copy saturates to ±57344 (e5m2 would
   // overflow to inf); the bf16 copy is unaffected
   const bool sat = __any(amax * inv8 >= kHqBf8Max);
   const float lim = kHqBf8Max / inv8;

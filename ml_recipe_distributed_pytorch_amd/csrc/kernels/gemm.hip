@@ -1008,11 +1008,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(127);
   __amdgpu_buffer_rsrc_t ca = rsrc_a(tile), cb = rsrc_b(tile);
   int p0 = 0;                   // LDS buffer of this tile's K-tile 0
-  // prologue of the first tile (as v2): K-tile 0 (A0 B0 B1 A1) and the first two halves of K-tile 1
+  // prologue of the first tile: K-tile 0 (A0 B0 B1 A1) and K-tile 1's A0 B0 B1 (its A1 is staged in K-tile 0)
   stage_bias(unit_n0(tile));   // oldest op of wave 0: retired by the wait below
   stA(ca, 0, 0, 0); stB(cb, 0, 0, 0); stB(cb, 1, 0, 0); stA(ca, 1, 0, 0);
-  stA(ca, 0, 1, 1); stB(cb, 0, 1, 1);
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  stA(ca, 0, 1, 1); stB(cb, 0, 1, 1); stB(cb, 1, 1, 1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   bar();
   bool first = true;
   bool prev_half = false;       // the previous unit was a half tile: its epilogue issued E / 2 vm ops
@@ -1040,60 +1040,53 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-    // One K-tile = 4 phases (v2's table); "t+1" / "t+2" halves past this tile's end come from the next
-    // tile's K-tile 0 (t+1 == nt, t+2 == nt); the next tile's K-tile 1 (t+2 == nt+1) is held back.
+    // One K-tile = 2 phases of 32 MFMAs per wave, each a (fragment reads + stage | barrier | MFMAs | barrier)
+    // pair; the two wave rows (wm) run one barrier apart, so one row's MFMAs cover the other's reads:
+    //   P01: reads B(nh 0), A(mh 0), B(nh 1); stages A1 of K-tile t+1   | MFMAs (0,0) (0,1)
+    //   P23: reads A(mh 1); stages A0, B0, B1 of K-tile t+2              | MFMAs (1,1) (1,0)
+    // Every half is staged by all 8 waves (16 rows each) and read 4-6 barrier intervals later; each wave's
+    // counted wait retires its own rows one interval before the OTHER wave row reads them.  A half is
+    // re-staged only after both rows have read it (A1 of buffer b1 two intervals after its last read, the
+    // others one).  Past this tile's end the stages come from the next tile's K-tile 0 (t+1 == nt,
+    // t+2 == nt); its K-tile 1 halves (t+2 == nt+1) are held back until the epilogue has left buffer bl.
     auto ktile = [&](int t) {
-
-      const bool more1 = t + 1 < nt || !last;
-      const bool more2 = t + 2 < nt || (t + 2 == nt && !last);
+      const bool more1 = t + 1 < nt || !last;                    // P01 stages A1 of K-tile t+1
+      const bool more2 = t + 2 < nt || (t + 2 == nt && !last);    // P23 stages K-tile t+2 (A0 B0 B1)
+      const bool prev2 = t + 1 < nt || (t + 1 == nt && !last);    // P23 of K-tile t-1 staged K-tile t+1
       const int b0 = (p0 + t) & 1, b1 = b0 ^ 1;
       const bool x1 = t + 1 >= nt, x2 = t + 2 >= nt;        // the "ahead" halves belong to the next tile
-      const __amdgpu_buffer_rsrc_t a1 = x1 ? na : ca, b1r = x1 ? nb : cb;
+      const __amdgpu_buffer_rsrc_t a1 = x1 ? na : ca;
       const __amdgpu_buffer_rsrc_t a2 = x2 ? na : ca, b2r = x2 ? nb : cb;
       const int k1 = x1 ? t + 1 - nt : t + 1, k2 = x2 ? t + 2 - nt : t + 2;
-      // P0 (0,0)
+      // P01: A1 of K-tile t (staged in P01 of t-1; younger: P23(t-1)'s 3 halves, or at t = 0 the epilogue's
+      // E vm ops and the 3 held-back halves); K-tile t's A0 B0 B1 were retired by P23(t-1)'s wait
       if (t == 0 && !first) {
         if (prev_half) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E / 2) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E) : "memory");
-      } else if (more1) {
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      }
-      readB(b0, 0, bf0);
-      readA(b0, 0);
-      if (more1) stB(b1r, 1, k1, b1);
-      bar();
-      mma(0, 0, bf0);
-      bar();
-      // P1 (0,1)
-      if (t == 0 && !first) {
-        if (prev_half) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E / 2) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E) : "memory");
-      } else if (more1) {
+      } else if (t == 0 || prev2) {
         asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      readB(b0, 0, bf0);
+      readA(b0, 0);
       readB(b0, 1, bf1);
       if (more1) stA(a1, 1, k1, b1);
       if (t == 0 && draw) draw_ticket();
       bar();
+      mma(0, 0, bf0);
       mma(0, 1, bf1);
       bar();
-      // P2 (1,1)
+      // P23: K-tile t+1's A0 B0 B1 (read by the other wave row in its next P01) — younger: this P01's A1
+      if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (!half) readA(b0, 1);
-      if (more2) stA(a2, 0, k2, b0);
+      if (more2) { stA(a2, 0, k2, b0); stB(b2r, 0, k2, b0); stB(b2r, 1, k2, b0); }
       bar();
-      if (!half) mma(1, 1, bf1);
-      bar();
-      // P3 (1,0)
-      if (more1) {
-        if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      if (!half) {
+        mma(1, 1, bf1);
+        mma(1, 0, bf0);
       }
-      if (more2) stB(b2r, 0, k2, b0);
-      bar();
-      if (!half) mma(1, 0, bf0);
       bar();
     };
     if (__builtin_amdgcn_readfirstlane(wm) == 0) {
@@ -1339,7 +1332,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
     stage_bias(unit_n0(next));
-    stA(na, 0, 1, bl); stB(nb, 0, 1, bl);
+    stA(na, 0, 1, bl); stB(nb, 0, 1, bl); stB(nb, 1, 1, bl);
     int after = next + nwg;
     if (sched) {
       const unsigned sx = *reinterpret_cast<const unsigned*>(smem + TICKET);

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const uint16_t* __
     asm volatile("" ::: "memory");
   };
 
-  // prologue (always real loads): tile 0 A0 B0 B1 A1, tile 1 A0 B0; retire A0(0), B0(0)
+  // prologue (always real loads): tile 0 A0 B0 B1 A1, tile 1 A0 B0 B1; retire tile 0
   {
     auto pro = [&](const __amdgpu_buffer_rsrc_t& rs, const int (&vo)[2], int ld, int half, int t, char* img) {
       char* dst = img + wave_u * 2048;
@@ -192,36 +192,31 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const uint16_t* __
     pro(rA, voA, N, 1, 0, smem + 1 * HALF);
     pro(rA, voA, N, 0, 1, smem + STAGE + 0 * HALF);
     pro(rB, voB, K, 0, 1, smem + STAGE + 2 * HALF);
+    pro(rB, voB, K, 1, 1, smem + STAGE + 3 * HALF);
   }
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   bar();
 
-  // schedule and hazard proof: gemm.hip, gemm_nt2_kernel (identical phase / stage / wait table)
+  // two phases of 32 MFMAs per K-tile (schedule, waits and hazard argument: gemm.hip, gemm_nt3_kernel):
+  //   P01: reads B(0) A(0) B(1), stages A1 of t+1 | (0,0) (0,1);   P23: reads A(1), stages A0 B0 B1 of t+2 | (1,1) (1,0)
   auto ktile = [&](int t) {
     const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
-    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    // A1(t): younger are P23(t-1)'s three halves when it staged K-tile t+1 (the prologue's K-tile 1 at t = 0)
+    if (t == 0 || more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readB(t, 0, bf0);
     readA(t, 0);
-    if (more1) stB(1, t + 1);
-    bar();
-    mma(0, 0, bf0);
-    bar();
-    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readB(t, 1, bf1);
     if (more1) stA(1, t + 1);
     bar();
+    mma(0, 0, bf0);
     mma(0, 1, bf1);
     bar();
+    // A0 B0 B1 of t+1 (read by the other wave row next): younger is this P01's A1 stage
+    if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readA(t, 1);
-    if (more2) stA(0, t + 2);
+    if (more2) { stA(0, t + 2); stB(0, t + 2); stB(1, t + 2); }
     bar();
     mma(1, 1, bf1);
-    bar();
-    if (more1) {
-      if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    }
-    if (more2) stB(0, t + 2);
-    bar();
     mma(1, 0, bf0);
     bar();
   };

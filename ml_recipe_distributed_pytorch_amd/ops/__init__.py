@@ -212,7 +212,7 @@ class Fp8DelayedState:
     """Per-site delayed-scaling state of an fp8 GEMM input: a device f32[4] (three rotating amax slots
     + the scale in use, see gemm_fp8.hip) and a host step counter selecting the slots — so neither the
     quantiser nor the GEMM ever synchronises with the host.  Forward inputs are e4m3 (scale = 2·amax/448);
-    backward activation gradients are e5m2 (scale = 2·amax/57344, ``grad=True``)."""
+    backward activation gradients are e5m2 (scale = 64·amax/57344, ``grad=True``; hq_common.h margins)."""
 
     def __init__(self, device, buf: Optional[torch.Tensor] = None, grad: bool = False):
         self.buf = torch.zeros(4, dtype=torch.float32, device=device) if buf is None else buf

@@ -159,3 +159,27 @@ def test_bench_refuses_more_gpus_than_visible(cuda):
                        timeout=120)
     assert r.returncode != 0 and "GPU(s) are visible" in r.stdout, r.stdout[-2000:]
     assert '"metric"' not in r.stdout
+
+
+def test_gloo_rehearsal_two_ranks_share_one_gpu(cuda, tmp_path):
+    """The one configuration in which ranks share a GPU — the 2-rank gloo rehearsal, both ranks on cuda:0 —
+    runs to completion with HIP's default 4 hardware queues per process (`_ranks_share_a_gpu`): round 2 saw this
+    setup hang in the gloo all-reduce with 8 queues per process (16 on the device, profiles/r2_reducer).
+    Production never shares a GPU (one rank per device; docs/ROUND4.md §7a)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT, free_port
+    out = tmp_path / "bench.json"
+    env = dict(os.environ, HQ_BENCH_BACKEND="gloo", HQ_HANG_DUMP_S="200")
+    env.pop("GPU_MAX_HW_QUEUES", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--batch", "16", "--seq", "128", "--json_out", str(out)]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=280)
+    assert r.returncode == 0, r.stdout[-4000:]
+    rec = json.loads(out.read_text())
+    assert rec["process_group"] == "gloo" and rec["world_size"] == 2, rec
+    assert rec["hw_queues"] == 4, rec   # not raised: the two ranks share cuda:0
+    assert rec["value"] > 0, rec
