@@ -208,35 +208,26 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
     asm volatile("" ::: "memory");
   };
 
-  stA(0, 0); stB(0, 0); stB(1, 0); stA(1, 0); stA(0, 1); stB(0, 1);
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  stA(0, 0); stB(0, 0); stB(1, 0); stA(1, 0); stA(0, 1); stB(0, 1); stB(1, 1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   bar();
-  // phase / stage / wait table and hazard proof: gemm.hip, gemm_nt2_kernel
+  // two 32-MFMA phases per K-tile; stage / wait table and hazard argument: gemm.hip, gemm_nt3_kernel
   auto ktile = [&](int t) {
     const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
-    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    if (t == 0 || more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readB(t, 0, bf0);
     readA(t, 0);
-    if (more1) stB(1, t + 1);
-    bar();
-    mma(0, 0, bf0);
-    bar();
-    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readB(t, 1, bf1);
     if (more1) stA(1, t + 1);
     bar();
+    mma(0, 0, bf0);
     mma(0, 1, bf1);
     bar();
+    if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readA(t, 1);
-    if (more2) stA(0, t + 2);
+    if (more2) { stA(0, t + 2); stB(0, t + 2); stB(1, t + 2); }
     bar();
     mma(1, 1, bf1);
-    bar();
-    if (more1) {
-      if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    }
-    if (more2) stB(0, t + 2);
-    bar();
     mma(1, 0, bf0);
     bar();
   };
@@ -433,8 +424,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* _
   __amdgpu_buffer_rsrc_t ca = rsrc_a(tile), cb = rsrc_b(tile);
   int p0 = 0;
   stA(ca, 0, 0, 0); stB(cb, 0, 0, 0); stB(cb, 1, 0, 0); stA(ca, 1, 0, 0);
-  stA(ca, 0, 1, 1); stB(cb, 0, 1, 1);
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  stA(ca, 0, 1, 1); stB(cb, 0, 1, 1); stB(cb, 1, 1, 1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   bar();
   bool first = true;
 
@@ -447,50 +438,37 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* _
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    // phase / stage / wait table: gemm.hip gemm_nt3_kernel
+    // two 32-MFMA phases per K-tile; stage / wait table and hazard argument: gemm.hip gemm_nt3_kernel
     auto ktile = [&](int t) {
       const bool more1 = t + 1 < nt || !last;
       const bool more2 = t + 2 < nt || (t + 2 == nt && !last);
+      const bool prev2 = t + 1 < nt || (t + 1 == nt && !last);
       const int b0 = (p0 + t) & 1, b1 = b0 ^ 1;
       const bool x1 = t + 1 >= nt, x2 = t + 2 >= nt;
-      const __amdgpu_buffer_rsrc_t a1 = x1 ? na : ca, b1r = x1 ? nb : cb;
+      const __amdgpu_buffer_rsrc_t a1 = x1 ? na : ca;
       const __amdgpu_buffer_rsrc_t a2 = x2 ? na : ca, b2r = x2 ? nb : cb;
       const int k1 = x1 ? t + 1 - nt : t + 1, k2 = x2 ? t + 2 - nt : t + 2;
       if (t == 0 && !first) {
         asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E) : "memory");
-      } else if (more1) {
-        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      }
-      readB(b0, 0, bf0);
-      readA(b0, 0);
-      if (more1) stB(b1r, 1, k1, b1);
-      bar();
-      mma(0, 0, bf0);
-      bar();
-      if (t == 0 && !first) {
-        asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E) : "memory");
-      } else if (more1) {
+      } else if (t == 0 || prev2) {
         asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      readB(b0, 0, bf0);
+      readA(b0, 0);
       readB(b0, 1, bf1);
       if (more1) stA(a1, 1, k1, b1);
       bar();
+      mma(0, 0, bf0);
       mma(0, 1, bf1);
       bar();
+      if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       readA(b0, 1);
-      if (more2) stA(a2, 0, k2, b0);
+      if (more2) { stA(a2, 0, k2, b0); stB(b2r, 0, k2, b0); stB(b2r, 1, k2, b0); }
       bar();
       mma(1, 1, bf1);
-      bar();
-      if (more1) {
-        if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      }
-      if (more2) stB(b2r, 0, k2, b0);
-      bar();
       mma(1, 0, bf0);
       bar();
     };
@@ -564,7 +542,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* _
     // every wave has read its staging rounds out of buffer bl: stage the next tile's K-tile-1 halves there
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
-    stA(na, 0, 1, bl); stB(nb, 0, 1, bl);
+    stA(na, 0, 1, bl); stB(nb, 0, 1, bl); stB(nb, 1, 1, bl);
     tile = next;
     next = tile + nwg;
     ca = na;

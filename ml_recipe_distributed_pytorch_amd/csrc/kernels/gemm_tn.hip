@@ -365,34 +365,25 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn8_kernel(const uint8_t* __
   };
 
   // prologue, schedule and waits: identical to gemm_tn_kernel (2 DMA instructions per wave per half)
-  stA(0, 0); stB(0, 0); stB(1, 0); stA(1, 0); stA(0, 1); stB(0, 1);
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  stA(0, 0); stB(0, 0); stB(1, 0); stA(1, 0); stA(0, 1); stB(0, 1); stB(1, 1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   bar();
   auto ktile = [&](int t) {
     const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
-    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    if (t == 0 || more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readB(t, 0, bf0);
     readA(t, 0);
-    if (more1) stB(1, t + 1);
-    bar();
-    mma(0, 0, bf0);
-    bar();
-    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readB(t, 1, bf1);
     if (more1) stA(1, t + 1);
     bar();
+    mma(0, 0, bf0);
     mma(0, 1, bf1);
     bar();
+    if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readA(t, 1);
-    if (more2) stA(0, t + 2);
+    if (more2) { stA(0, t + 2); stB(0, t + 2); stB(1, t + 2); }
     bar();
     mma(1, 1, bf1);
-    bar();
-    if (more1) {
-      if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    }
-    if (more2) stB(0, t + 2);
-    bar();
     mma(1, 0, bf0);
     bar();
   };
