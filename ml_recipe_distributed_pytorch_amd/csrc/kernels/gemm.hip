@@ -665,41 +665,33 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
     else stage_half(Bb, ldb, half, t, smem + (t & 1) * STAGE + PANEL);
   };
   proA(0, 0); proB(0, 0); proB(1, 0); proA(1, 0);
-  proA(0, 1); proB(0, 1);
-  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  proA(0, 1); proB(0, 1); proB(1, 1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   bar();
 
-  // One K-tile = 4 phases; `G1` = the staggered group (one barrier behind).
+  // One K-tile = 2 phases of 32 MFMAs (stage / wait table and hazard argument: gemm_nt3_kernel below);
+  // `G1` = the staggered group (one barrier behind).
   auto ktile = [&](int t) {
     const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
-    // P0 (0,0)
-    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    // P01 (0,0) (0,1): A1 of K-tile t; younger: the previous P23's three halves (the prologue's at t = 0)
+    if (t == 0 || more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readB(t, 0, bf0);
     readA(t, 0);
-    if (more1) stB(1, t + 1);
-    bar();
-    mma(0, 0, bf0);
-    bar();
-    // P1 (0,1)
-    if (more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readB(t, 1, bf1);
     if (more1) stA(1, t + 1);
     bar();
+    mma(0, 0, bf0);
     mma(0, 1, bf1);
     bar();
-    // P2 (1,1)
+    // P23 (1,1) (1,0): K-tile t+1's A0 B0 B1 for the other wave row; younger: this P01's A1
+    if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!half) readA(t, 1);
-    if (more2) stA(0, t + 2);
+    if (more2) { stA(0, t + 2); stB(0, t + 2); stB(1, t + 2); }
     bar();
-    if (!half) mma(1, 1, bf1);
-    bar();
-    // P3 (1,0)
-    if (more1) {
-      if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (!half) {
+      mma(1, 1, bf1);
+      mma(1, 0, bf0);
     }
-    if (more2) stB(0, t + 2);
-    bar();
-    if (!half) mma(1, 0, bf0);
     bar();
   };
   if (ABL & 4) {
