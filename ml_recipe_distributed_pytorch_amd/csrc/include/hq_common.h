@@ -43,16 +43,14 @@ __device__ __forceinline__ uint2 hq_pack4(const float* f) {
 }
 
 // ------------------------------------------------------------------------------ GELU (erf form)
-// Normal CDF Φ(x) and pdf φ(x) sharing ONE exp: Abramowitz–Stegun 7.1.26 for erf(|x|/√2)
-// (|err| < 1.5e-7, far below bf16 resolution) with raw v_rcp / v_exp; the negative tail is
-// computed as q directly (no 1 - (1 - q) cancellation).  ~14 VALU ops vs ~30 for libm erff.
+// Normal CDF Φ(x) and pdf φ(x) sharing ONE exp: Abramowitz–Stegun 7.1.25 for erf(|x|/√2) (three terms,
+// |erf err| < 2.5e-5 → |Φ err| < 1.3e-5, far below bf16 resolution; 1/√2 and ½ folded into the constants)
+// with raw v_rcp / v_exp; the negative tail is computed as q directly (no 1 - (1 - q) cancellation).
 __device__ __forceinline__ void hq_normal_cdf_pdf(float x, float& cdf, float& pdf) {
-  const float z = fabsf(x) * 0.70710678118654752f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
-  const float poly =
-      fmaf(fmaf(fmaf(fmaf(1.061405429f, t, -1.453152027f), t, 1.421413741f), t, -0.284496736f), t, 0.254829592f) * t;
-  const float e = __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);  // e^{-x²/2}
-  const float q = 0.5f * poly * e;                                         // Φ(-|x|)
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.33267340f, fabsf(x), 1.f));     // p / √2
+  const float poly = fmaf(fmaf(0.3739278f, t, -0.0479399f), t, 0.1740121f) * t;
+  const float e = __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);       // e^{-x²/2}
+  const float q = poly * e;                                                    // Φ(-|x|)
   cdf = x >= 0.f ? 1.f - q : q;
   pdf = 0.3989422804014327f * e;
 }
@@ -77,16 +75,13 @@ __device__ __forceinline__ void hq_gelu_grad8(float* x, float* g) {
 #pragma unroll
   for (int e = 0; e < 8; e += 2) {
     const hq_f2_t v = {x[e], x[e + 1]};
-    const hq_f2_t z = hq_f2_t{fabsf(v.x), fabsf(v.y)} * hq_s2(0.70710678118654752f);
-    const hq_f2_t den = hq_fma2(hq_s2(0.3275911f), z, hq_s2(1.f));
+    const hq_f2_t den = hq_fma2(hq_s2(0.33267340f), hq_f2_t{fabsf(v.x), fabsf(v.y)}, hq_s2(1.f));
     const hq_f2_t t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-    hq_f2_t p = hq_fma2(hq_s2(1.061405429f), t, hq_s2(-1.453152027f));
-    p = hq_fma2(p, t, hq_s2(1.421413741f));
-    p = hq_fma2(p, t, hq_s2(-0.284496736f));
-    p = hq_fma2(p, t, hq_s2(0.254829592f)) * t;
+    hq_f2_t p = hq_fma2(hq_s2(0.3739278f), t, hq_s2(-0.0479399f));
+    p = hq_fma2(p, t, hq_s2(0.1740121f)) * t;
     const hq_f2_t ea = (v * v) * hq_s2(-0.72134752044448170f);
     const hq_f2_t ex = {__builtin_amdgcn_exp2f(ea.x), __builtin_amdgcn_exp2f(ea.y)};
-    const hq_f2_t q = (hq_s2(0.5f) * p) * ex;                       // Φ(-|x|)
+    const hq_f2_t q = p * ex;                                        // Φ(-|x|)
     const hq_f2_t omq = hq_s2(1.f) - q;
     const hq_f2_t cdf = {v.x >= 0.f ? omq.x : q.x, v.y >= 0.f ? omq.y : q.y};
     const hq_f2_t pdf = hq_s2(0.3989422804014327f) * ex;
@@ -95,18 +90,6 @@ __device__ __forceinline__ void hq_gelu_grad8(float* x, float* g) {
     g[e] = gr.x; g[e + 1] = gr.y;
     x[e] = y.x; x[e + 1] = y.y;
   }
-}
-
-// Cheaper GELU/GELU' pair (A&S 7.1.25, three terms: |erf err| < 2.5e-5 → |Φ err| < 1.3e-5, still far below
-// bf16 resolution): 3 FMAs instead of 5 in the rational part, 1/√2 and ½ folded into the constants.
-__device__ __forceinline__ void hq_gelu_pair_fast(float x, float& y, float& g) {
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.33267340f, fabsf(x), 1.f));   // p / √2
-  const float poly = fmaf(fmaf(0.3739278f, t, -0.0479399f), t, 0.1740121f) * t;
-  const float e = __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);     // e^{-x²/2}
-  const float q = poly * e;                                                  // Φ(-|x|)
-  const float cdf = x >= 0.f ? 1.f - q : q;
-  y = x * cdf;
-  g = fmaf(x * 0.3989422804014327f, e, cdf);
 }
 
 // ------------------------------------------------------------------------------ reductions

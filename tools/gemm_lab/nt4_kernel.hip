@@ -269,7 +269,7 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_nt4_kernel(const uint16_t* _
         float x[8], gr[8];
         hq_unpack8(piece, x);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) hq_gelu_pair_fast(x[e], x[e], gr[e]);
+        for (int e = 0; e < 8; ++e) { const float xv = x[e]; gr[e] = hq_gelu_grad(xv); x[e] = hq_gelu(xv); }
         *reinterpret_cast<uint4*>(P + goff) = hq_pack8(gr);
         piece = hq_pack8(x);
       } else if constexpr (EPI == HQ_EPI_DMUL || EPI == HQ_EPI_DGELU) {
