@@ -820,14 +820,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
 // walking tiles (tile = id, id + grid, …) and runs the LDS-DMA pipeline straight across the tile seam:
 // K-tile 0 of the next tile is staged during the last two K-tiles of this one (exactly the loads the
 // steady state would issue for t+1 / t+2), so its data lands under the last MFMA phases and the
-// epilogue.  Only the next tile's K-tile-1 first halves (A0, B0), which v2 would stage into the buffer
-// the epilogue now borrows, are held back until the epilogue is done.
+// epilogue, and the next tile's K-tile-1 A0 / B0 / B1 halves go into the last K-tile's buffer as soon as
+// every wave has read it, ahead of the epilogue.
 //
-// Epilogue LDS: the buffer of this tile's last K-tile (free once every wave passed its last MFMA
-// phase) holds seven waves' 64-row staging regions, wave 7's lies past both buffers; the 128 local
-// rows of each wave are staged in two 64-row rounds.  The epilogue's global loads/stores (E per lane,
-// EPI-dependent, all issued between the next tile's K-tile-0 halves and its K-tile-1 halves) are
-// counted into the first K-tile's vmcnt waits.  Raw barriers only (a __syncthreads fence would drain
+// Epilogue LDS: the 128 local rows of each wave are staged in four 32-row rounds through a 4.5 KB region
+// per wave — waves 0-2 in the A1 half of the last K-tile's buffer (the next tile stages its K-tile-1 A1 there
+// only in its first phase), waves 3-4 past both buffers, waves 5-7 past the bias.  The epilogue's global
+// loads/stores (E per lane, EPI-dependent, issued after the next tile's K-tile-1 halves) are counted into
+// the first K-tile's vmcnt waits.  Raw barriers only (a __syncthreads fence would drain
 // the in-flight DMA).
 typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
@@ -860,7 +860,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   constexpr int E = NT3Epi<EPI>::E;
   constexpr int TICKET = SPARE + REGION + 2 * BN * 4;   // LDS word: the tile after `next` (dynamic schedule)
   constexpr int BIASL = TICKET + 16;                    // the unit's 256 fp32 bias values (1 KiB, LDS-DMA by wave 0)
-  static_assert(7 * REGION <= STAGE && BIASL + 1024 <= 160 * 1024, "LDS plan");
+  // epilogue staging: 32-row rounds, QREG bytes per wave — waves 0-2 in the A1 half of the last K-tile's
+  // buffer, 3-4 in SPARE, 5-7 past the bias — so that the buffer's other three halves take the next tile's
+  // K-tile 1 BEFORE the epilogue's stores (vmcnt retires in issue order: K-tile 1 issued after the stores
+  // could not be waited for before they drained, which the first K-tile's counted waits then did)
+  constexpr int QREG = 32 * RS;
+  constexpr int TAIL = BIASL + 1024;
+  static_assert(3 * QREG <= PANEL / 2 && 2 * QREG <= REGION && TAIL + 3 * QREG <= 160 * 1024, "LDS plan");
   constexpr bool kBiasE = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD || EPI == HQ_EPI_BDR;
   const bool ht_on = (stagger >> 16) & 1;   // kHalfTail
   stagger &= 0xFF;
@@ -1040,7 +1046,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     // counted wait retires its own rows one interval before the OTHER wave row reads them.  A half is
     // re-staged only after both rows have read it (A1 of buffer b1 two intervals after its last read, the
     // others one).  Past this tile's end the stages come from the next tile's K-tile 0 (t+1 == nt,
-    // t+2 == nt); its K-tile 1 halves (t+2 == nt+1) are held back until the epilogue has left buffer bl.
+    // t+2 == nt); its K-tile-1 A0 B0 B1 (t+2 == nt+1) go into buffer bl right after the last K-tile.
     auto ktile = [&](int t) {
       const bool more1 = t + 1 < nt || !last;                    // P01 stages A1 of K-tile t+1
       const bool more2 = t + 2 < nt || (t + 2 == nt && !last);    // P23 stages K-tile t+2 (A0 B0 B1)
@@ -1050,8 +1056,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       const __amdgpu_buffer_rsrc_t a1 = x1 ? na : ca;
       const __amdgpu_buffer_rsrc_t a2 = x2 ? na : ca, b2r = x2 ? nb : cb;
       const int k1 = x1 ? t + 1 - nt : t + 1, k2 = x2 ? t + 2 - nt : t + 2;
-      // P01: A1 of K-tile t (staged in P01 of t-1; younger: P23(t-1)'s 3 halves, or at t = 0 the epilogue's
-      // E vm ops and the 3 held-back halves); K-tile t's A0 B0 B1 were retired by P23(t-1)'s wait
+      // P01: A1 of K-tile t (staged in P01 of t-1; younger: P23(t-1)'s 3 halves, or at t = 0 the K-tile-1
+      // halves and the epilogue's E vm ops); K-tile t's A0 B0 B1 were retired by P23(t-1)'s wait
       if (t == 0 && !first) {
         if (prev_half) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E / 2) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E) : "memory");
@@ -1069,9 +1075,17 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       mma(0, 0, bf0);
       mma(0, 1, bf1);
       bar();
-      // P23: K-tile t+1's A0 B0 B1 (read by the other wave row in its next P01) — younger: this P01's A1
-      if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // P23: K-tile t+1's A0 B0 B1 (read by the other wave row in its next P01) — younger: this P01's A1 and,
+      // at t = 0 of a following unit, the previous unit's epilogue (E vm ops, E / 2 after a half tile), which was
+      // issued after K-tile 1
+      if (t == 0 && !first) {
+        if (prev_half) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 + E / 2) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 + E) : "memory");
+      } else if (more1) {
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       if (!half) readA(b0, 1);
       if (more2) { stA(a2, 0, k2, b0); stB(b2r, 0, k2, b0); stB(b2r, 1, k2, b0); }
       bar();
@@ -1092,24 +1106,28 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     if (draw && tid == 0)
       *reinterpret_cast<unsigned*>(smem + TICKET) = 2u * (unsigned)cnt_x + ticket;   // sequence index s
     const int bl = (p0 + nt - 1) & 1;
-    char* wreg = wave < 7 ? smem + bl * STAGE + wave * REGION : smem + SPARE;
+    char* wreg = wave < 3 ? smem + bl * STAGE + PANEL / 2 + wave * QREG
+                          : (wave < 5 ? smem + SPARE + (wave - 3) * QREG : smem + TAIL + (wave - 5) * QREG);
+    // every wave is past its last read of buffer bl: the next tile's K-tile-1 A0 / B0 / B1 halves go there now,
+    // ahead of the epilogue's loads and stores (its A1 half holds waves 0-2's staging; P01 of K-tile 0 stages it)
+    if (!last) { stA(na, 0, 1, bl); stB(nb, 0, 1, bl); stB(nb, 1, 1, bl); }
 
-    // ---- epilogue (v2's math), 64 local rows per round.  Ordered so that nothing in round 1 waits for round 0's
-    // stores (vmcnt counts loads and stores in issue order): the bias and BOTH rounds' epilogue operands
-    // (aux: 16 pieces per lane, 64 VGPRs — the fragment registers are dead) are loaded before the first store,
-    // and the staging writes are inline-asm ds_writes, which hipcc does not fence with vmcnt(0) as it does a
-    // builtin LDS store while LDS-DMA may be in flight.  Nothing targets this wave's staging region by DMA
-    // during the epilogue (the next tile's K-tile-1 halves go there only after it), and LDS executes a wave's
-    // ds operations in order, so round 1's writes cannot overtake round 0's reads.
+    // ---- epilogue (v2's math), 32 local rows per round (4 rounds, 2 in a half tile).  Ordered so that no round
+    // waits for an earlier round's stores (vmcnt counts loads and stores in issue order): the bias and ALL the
+    // epilogue operands (aux: 16 pieces per lane, 64 VGPRs — the fragment registers are dead) are loaded before
+    // the first store, and the staging writes are inline-asm ds_writes, which hipcc does not fence with vmcnt(0)
+    // as it does a builtin LDS store while LDS-DMA may be in flight.  Nothing targets a wave's staging region by
+    // DMA during the epilogue, and LDS executes a wave's ds operations in order, so a round's writes cannot
+    // overtake the previous round's reads.
     constexpr int SEGS = WN / 8, ROWS_PER_IT = 64 / SEGS;
     constexpr bool kReadsAux = EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR;
     constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD || EPI == HQ_EPI_BDR;
     const int seg = lane % SEGS, rsub = lane / SEGS;
     const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;
     const uint32_t wreg_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)wreg;
-    auto goff_of = [&](int rnd, int it) {   // it: 0..7 within a round
-      const int lr = it * ROWS_PER_IT + rsub;  // 0..63
-      return (size_t)(m0 + rnd * 128 + wm * 64 + lr) * ldc + gcol;
+    // round q: rows (q >> 1)·128 + wm·64 + (q & 1)·32 + it·8 + rsub of the tile (it: 0..3 within the round)
+    auto goff_of = [&](int q, int it) {
+      return (size_t)(m0 + (q >> 1) * 128 + wm * 64 + (q & 1) * 32 + it * ROWS_PER_IT + rsub) * ldc + gcol;
     };
     // epilogue global traffic through buffer descriptors over the unit's rows: ONE per-lane offset register
     // (row rsub of the wave's 64-row block, column gcol) and a wave-uniform scalar offset per piece, instead
@@ -1119,7 +1137,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       return __builtin_amdgcn_make_buffer_rsrc((void*)(base + (size_t)m0 * ldc), (short)0, rows_u * ldc * 2, 0x00020000);
     };
     const int vo_lane = ((wm * 64 + rsub) * ldc + gcol) * 2;
-    auto so_of = [&](int rnd, int it) { return (rnd * 128 + it * ROWS_PER_IT) * ldc * 2; };
+    auto so_of = [&](int q, int it) { return ((q >> 1) * 128 + (q & 1) * 32 + it * ROWS_PER_IT) * ldc * 2; };
     auto bload = [&](__amdgpu_buffer_rsrc_t r, int rnd, int it) {
       const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, vo_lane, so_of(rnd, it), 0);
       return make_uint4(v.x, v.y, v.z, v.w);
@@ -1138,8 +1156,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     float csum[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[e] = 0.f;
-    // NR = 2 rounds (full tile) or 1 (half tile), a compile-time count: with a runtime `half` test hipcc sinks
-    // round 1's operand loads into the branch, i.e. behind round 0's stores
+    // NR = 2 row halves (full tile) or 1 (half tile), a compile-time count: with a runtime `half` test hipcc
+    // sinks the later rounds' operand loads into the branch, i.e. behind the first round's stores
     auto epilogue = [&](auto nr_c) {
       constexpr int NR = decltype(nr_c)::value;
       // BDR keeps per-round operand loads (both rounds' 64 VGPRs spill beside its dropout hash)
@@ -1157,10 +1175,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       const __amdgpu_buffer_rsrc_t rC = rsrc_of(C);
       const __amdgpu_buffer_rsrc_t rP = rsrc_of(P ? P : C);
       const __amdgpu_buffer_rsrc_t rA = (EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR) ? rsrc_of(R) : rP;   // aux source
-      uint4 aux[kReadsAux ? (kAll ? 8 * NR : 8) : 1];
-      // per round: stage (inline-asm ds_writes: no vmcnt fence), read the 8 pieces back, math, stores; round 1's
-      // operands are loaded after round 0's staging, still before round 0's first store
-      uint4 pieces[NR][8];
+      constexpr int NQ = 2 * NR;   // 32-row rounds
+      uint4 aux[kReadsAux ? (kAll ? 8 * NR : 4) : 1];
+      // per round: stage (inline-asm ds_writes: no vmcnt fence), read its 4 pieces back, math, stores; the
+      // second row half's operands are loaded after the first round's staging, still before its first store
+      uint4 pieces[NQ][4];
       // acc (+bias) → bf16 pairs for every round up front: the 128 accumulator VGPRs die here (64 hold the packed
       // tile), which is what lets both rounds' operands and a round of pieces stay in registers without spilling
       u32x2_t pk[NR][16];
@@ -1179,70 +1198,70 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
           }
         }
       __builtin_amdgcn_sched_barrier(0);   // packed now, not sunk to the staging (the fp32 accumulators die)
-      if constexpr (kAll) {   // round 0's operands now (their latency hides under the staging) ...
+      if constexpr (kAll) {   // the first row half's operands now (their latency hides under the staging) ...
 #pragma unroll
-        for (int it = 0; it < 8; ++it) aux[it] = bload(rA, 0, it);
+        for (int it = 0; it < 8; ++it) aux[it] = bload(rA, it >> 2, it & 3);
       }
-      auto stage_round = [&](int rnd) {
+      auto stage_round = [&](int q) {   // rows (q & 1)·32 … +31 of row half q >> 1: 16-row blocks I = 2·(q & 1) + i
+        const int rnd = q >> 1, sub = q & 1;
 #pragma unroll
         for (int J = 0; J < 4; ++J) {
           const int nh = J >> 1, j = J & 1;
           const int lc = nh * 32 + j * 16 + fq * 4;
 #pragma unroll
-          for (int I = 0; I < 4; ++I)
-            asm volatile("ds_write_b64 %0, %1" :: "v"(wreg_lds + (uint32_t)((I * 16 + fr) * RS + lc * 2)),
-                         "v"(pk[rnd][J * 4 + I]) : "memory");
+          for (int i = 0; i < 2; ++i)
+            asm volatile("ds_write_b64 %0, %1" :: "v"(wreg_lds + (uint32_t)((i * 16 + fr) * RS + lc * 2)),
+                         "v"(pk[rnd][J * 4 + 2 * sub + i]) : "memory");
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if constexpr (!kReadsAux) {
           // inline asm: a builtin LDS read would make hipcc drain vmcnt(0), i.e. wait for the next tile's
-          // K-tile-0 DMA (epilogues with operand loads wait for those, which are younger, anyway).  The reads
-          // and their lgkmcnt wait are ONE asm statement: the outputs are defined only when it completes (with
+          // K-tile DMA (epilogues with operand loads wait for those, which are younger, anyway).  The reads and
+          // their lgkmcnt wait are ONE asm statement: the outputs are defined only when it completes (with
           // separate statements hipcc may copy an output register before the data has returned).
           static_assert(ROWS_PER_IT * RS == 1152, "ds_read offsets below");
-          u32x4_t v0, v1, v2, v3, v4, v5, v6, v7;
+          u32x4_t v0, v1, v2, v3;
           asm volatile(
-              "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:1152\n\tds_read_b128 %2, %8 offset:2304\n\t"
-              "ds_read_b128 %3, %8 offset:3456\n\tds_read_b128 %4, %8 offset:4608\n\tds_read_b128 %5, %8 offset:5760\n\t"
-              "ds_read_b128 %6, %8 offset:6912\n\tds_read_b128 %7, %8 offset:8064\n\ts_waitcnt lgkmcnt(0)"
-              : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3), "=&v"(v4), "=&v"(v5), "=&v"(v6), "=&v"(v7)
+              "ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:1152\n\tds_read_b128 %2, %4 offset:2304\n\t"
+              "ds_read_b128 %3, %4 offset:3456\n\ts_waitcnt lgkmcnt(0)"
+              : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)
               : "v"(wreg_lds + (uint32_t)(rsub * RS + seg * 16))
               : "memory");
-          const u32x4_t vv[8] = {v0, v1, v2, v3, v4, v5, v6, v7};
+          const u32x4_t vv[4] = {v0, v1, v2, v3};
 #pragma unroll
-          for (int it = 0; it < 8; ++it) pieces[rnd][it] = make_uint4(vv[it].x, vv[it].y, vv[it].z, vv[it].w);
+          for (int it = 0; it < 4; ++it) pieces[q][it] = make_uint4(vv[it].x, vv[it].y, vv[it].z, vv[it].w);
         } else {
 #pragma unroll
-          for (int it = 0; it < 8; ++it)
-            pieces[rnd][it] = *reinterpret_cast<const uint4*>(wreg + (it * ROWS_PER_IT + rsub) * RS + seg * 16);
+          for (int it = 0; it < 4; ++it)
+            pieces[q][it] = *reinterpret_cast<const uint4*>(wreg + (it * ROWS_PER_IT + rsub) * RS + seg * 16);
         }
       };
 #pragma unroll
-      for (int rnd = 0; rnd < NR; ++rnd) {
-        if (rnd > 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // round 0's piece reads returned
-        stage_round(rnd);
+      for (int q = 0; q < NQ; ++q) {
+        if (q > 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous round's piece reads returned
+        stage_round(q);
         if constexpr (kAll && NR > 1) {
-          if (rnd == 0) {   // round 1's operands: after round 0's staging (accumulators half dead), before its stores
+          if (q == 0) {   // the second row half's operands: after the first staging, before its stores
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int it = 0; it < 8; ++it) aux[8 + it] = bload(rA, 1, it);
+            for (int it = 0; it < 8; ++it) aux[8 + it] = bload(rA, 2 + (it >> 2), it & 3);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
         if constexpr (kReadsAux && !kAll) {
 #pragma unroll
-          for (int it = 0; it < 8; ++it) aux[it] = bload(rA, rnd, it);
+          for (int it = 0; it < 4; ++it) aux[it] = bload(rA, q, it);
         }
         constexpr bool kTwo = EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD;   // P and C stores per piece
         u32x4_t holdP = {0u, 0u, 0u, 0u}, holdC = holdP;                    // the previous piece's store data
 #pragma unroll
-        for (int it = 0; it < 8; ++it) {
-          uint4 piece = pieces[rnd][it];
-          const size_t goff = goff_of(rnd, it);
-          const uint4 ax = aux[kAll ? rnd * 8 + it : (kReadsAux ? it : 0)];
+        for (int it = 0; it < 4; ++it) {
+          uint4 piece = pieces[q][it];
+          const size_t goff = goff_of(q, it);
+          const uint4 ax = aux[kAll ? q * 4 + it : (kReadsAux ? it : 0)];
           u32x4_t sP = holdP;
           if constexpr (EPI == HQ_EPI_GELU) {
-            sP = bstore(rP, rnd, it, piece);
+            sP = bstore(rP, q, it, piece);
             float x[8];
             hq_unpack8(piece, x);
 #pragma unroll
@@ -1252,7 +1271,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
             float x[8], g[8];
             hq_unpack8(piece, x);
             hq_gelu_grad8(x, g);   // g = gelu'(x), x = gelu(x)
-            sP = bstore(rP, rnd, it, hq_pack8(g));
+            sP = bstore(rP, q, it, hq_pack8(g));
             piece = hq_pack8(x);
           } else if constexpr (EPI == HQ_EPI_DMUL) {
             float d[8], gd[8];
@@ -1278,7 +1297,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
           } else if constexpr (EPI == HQ_EPI_BDR) {
             piece = hq_epi_bdr8(piece, ax, (uint32_t)goff, dr, key);
           }
-          const u32x4_t sC = bstore(rC, rnd, it, piece);
+          const u32x4_t sC = bstore(rC, q, it, piece);
           if (it > 0) {
             if constexpr (kTwo) asm volatile("" :: "v"(holdP), "v"(holdC));
             else asm volatile("" :: "v"(holdC));
@@ -1289,12 +1308,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
           // ahead of the serial csum chain and spills them)
           if constexpr (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL) __builtin_amdgcn_sched_barrier(0);
         }
-        // round end: 64 wait states with the last stores' data held (BIAS stores back to back: all 8 pieces)
+        // round end: 64 wait states with the last stores' data held (BIAS stores back to back: all 4 pieces)
 #define HQ_PAD64 "s_nop 15\n\ts_nop 15\n\ts_nop 15\n\ts_nop 15"
         if constexpr (EPI == HQ_EPI_BIAS) {
-          auto u = [&](int i) { const uint4& q = pieces[rnd][i]; return u32x4_t{q.x, q.y, q.z, q.w}; };
-          asm volatile(HQ_PAD64 :: "v"(u(0)), "v"(u(1)), "v"(u(2)), "v"(u(3)), "v"(u(4)), "v"(u(5)), "v"(u(6)),
-                       "v"(u(7)));
+          auto u = [&](int i) { const uint4& w = pieces[q][i]; return u32x4_t{w.x, w.y, w.z, w.w}; };
+          asm volatile(HQ_PAD64 :: "v"(u(0)), "v"(u(1)), "v"(u(2)), "v"(u(3)));
         } else if constexpr (kTwo) {
           asm volatile(HQ_PAD64 :: "v"(holdP), "v"(holdC));
         } else {
@@ -1319,12 +1337,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       for (int c = tid; c < BN; c += kThreads) part[(size_t)tm * N + n0 + c] = red[c] + red[BN + c];
     }
     if (last) break;
-    // every wave has read its staging rounds out of buffer bl (and the bias): stage the next tile's K-tile-1
-    // halves there, and the next unit's bias (an extra, younger op of wave 0 only: its counted waits wait longer)
+    // every wave has read the bias (and its staging rounds): stage the next unit's bias (an extra, younger op of
+    // wave 0 only: its counted waits wait longer)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
     stage_bias(unit_n0(next));
-    stA(na, 0, 1, bl); stB(nb, 0, 1, bl); stB(nb, 1, 1, bl);
     int after = next + nwg;
     if (sched) {
       const unsigned sx = *reinterpret_cast<const unsigned*>(smem + TICKET);
@@ -1470,7 +1487,7 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
                       2 * rt_t <= ncu_t && grid > ncu_t;
   const bool v3_auto = g_gemm_variant == 0 && (K <= 2304 || tail_t);
   if (bn == 256 && (g_gemm_variant == 3 || v3_auto) && K >= 2 * BK && srd_ok) {
-    constexpr size_t lds = 2 * 2 * 256 * 128 + 64 * 144 + 2 * 256 * 4 + 16 + 1024;
+    constexpr size_t lds = 2 * 2 * 256 * 128 + 64 * 144 + 2 * 256 * 4 + 16 + 1024 + 3 * 32 * 144;
     static int ncu = [] {
       int dev = 0, n = 0;
       (void)hipGetDevice(&dev);
