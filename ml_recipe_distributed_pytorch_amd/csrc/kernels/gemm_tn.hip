@@ -369,6 +369,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn8_kernel(const uint8_t* __
   };
 
   // prologue, schedule and waits: identical to gemm_tn_kernel (2 DMA instructions per wave per half)
+  const bool row1 = __builtin_amdgcn_readfirstlane(wm) != 0;
   stA(0, 0); stB(0, 0); stB(1, 0); stA(1, 0); stA(0, 1); stB(0, 1); stB(1, 1);
   asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   bar();
@@ -383,7 +384,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn8_kernel(const uint8_t* __
     mma(0, 0, bf0);
     mma(0, 1, bf1);
     bar();
-    if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (row1) {   // only the trailing wave row (gemm.hip, gemm_nt3_kernel)
+      if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     readA(t, 1);
     if (more2) { stA(0, t + 2); stB(0, t + 2); stB(1, t + 2); }
     bar();
