@@ -128,13 +128,17 @@ static inline float hq_keep_scale(uint32_t thr) { return thr < 65536u ? 65536.0f
 // fmix32's quarter-rate 32-bit multiplies (9 full-rate VALU per pair instead of ~18 slot-equivalents):
 // the first xorshift folds the high byte into the low 24 bits before each 24-bit multiply.  Avalanche
 // 0.4996-0.5003 per input bit, no detectable pair/stride correlation (ops/rng.py documents the test).
-__device__ __forceinline__ uint32_t hq_mix24(uint32_t x) {  // x = pair_index ^ key
-  x ^= x >> 16;
+// hq_mix24 after its first xorshift.  For c < 2^16, hq_mix24(x ^ c) == hq_mix24_post((x ^ (x >> 16)) ^ c):
+// a loop hashing x ^ c for several small c does the first xorshift once.
+__device__ __forceinline__ uint32_t hq_mix24_post(uint32_t x) {
   x = __umul24(x, 0x9E3779u);
   x ^= x >> 15;
   x = __umul24(x, 0xC2B2AEu);
   x ^= x >> 16;
   return x;
+}
+__device__ __forceinline__ uint32_t hq_mix24(uint32_t x) {  // x = pair_index ^ key
+  return hq_mix24_post(x ^ (x >> 16));
 }
 __device__ __forceinline__ uint32_t hq_pair_hash(uint32_t idx_even, uint32_t key) {
   uint32_t x = (idx_even >> 1) ^ key;

@@ -276,6 +276,10 @@ typedef float f2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ float keep_and(float x, uint32_t w, int pos) {
   return __uint_as_float(__float_as_uint(x) & (uint32_t)__builtin_amdgcn_sbfe((int)w, (unsigned)pos, 1u));
 }
+// bit of the forward's 16-bit keep word that holds element r of a lane's 16 (even elements in the low byte,
+// odd in the high: the forward builds them as packed-pair flags, see attn_fwd_ring_kernel)
+__host__ __device__ constexpr int kbit(int r) { return ((r & 1) << 3) | (r >> 1); }
+typedef uint16_t u16x2_t __attribute__((ext_vector_type(2)));
 
 // lane ^ 32 exchange without LDS: v_permlane32_swap hands each half the other half's value.
 __device__ __forceinline__ float xor32_max(float v) {
@@ -556,20 +560,27 @@ __global__ __launch_bounds__(RW * 64, DROP ? 3 : 4) void attn_fwd_ring_kernel(co
       const f2_t a2 = f2_t{sc[8], sc[9]} + f2_t{sc[10], sc[11]}, a3 = f2_t{sc[12], sc[13]} + f2_t{sc[14], sc[15]};
       l2 += (a0 + a1) + (a2 + a3);
     }
+    // dropout on the PACKED bf16 P: element pair p = (2p, 2p + 1) is one bf16x2 word of pack_b and one
+    // 32-bit hash (low half → element 2p).  Packed u16 saturating ops turn the hash halves into keep flags
+    // (z = sat(thr − h) is 0 iff kept; sat(1 − z) is the flag) and the flags into a per-half AND mask —
+    // 5 VALU per pair instead of two compares, two f32 selects and a bit insert per element.
+    uint32_t km[8];
     if constexpr (DROP) {
-      uint32_t bits = 0;
+      uint32_t kb = 0;   // keep flags: element 2p at bit p, element 2p + 1 at bit 16 + p
       if constexpr (EVEN) {
-        const uint32_t pk = (((row_idx >> 1) + (uint32_t)kt * 16u) ^ key) ^ (2u * (uint32_t)hh);
+        uint32_t pk = (((row_idx >> 1) + (uint32_t)kt * 16u) ^ key) ^ (2u * (uint32_t)hh);
+        pk ^= pk >> 16;                                   // hq_mix24's first xorshift, once per tile
+        const u16x2_t thr2 = {(uint16_t)thr, (uint16_t)thr}, one2 = {1, 1}, zero2 = {0, 0};
 #pragma unroll
         for (int g = 0; g < 4; ++g)
 #pragma unroll
           for (int ip = 0; ip < 2; ++ip) {
-            const uint32_t hsh = hq_mix24(pk ^ (uint32_t)(4 * g + ip));
-            const int r = 4 * g + 2 * ip;
-            const bool k0 = (hsh & 0xFFFFu) >= thr, k1 = (hsh >> 16) >= thr;
-            sc[r] = k0 ? sc[r] : 0.f;
-            sc[r + 1] = k1 ? sc[r + 1] : 0.f;
-            bits |= ((uint32_t)k0 << r) | ((uint32_t)k1 << (r + 1));
+            const uint32_t hsh = hq_mix24_post(pk ^ (uint32_t)(4 * g + ip));   // = hq_mix24(pair ^ key)
+            const int p = 2 * g + ip;
+            const u16x2_t z = __builtin_elementwise_sub_sat(thr2, __builtin_bit_cast(u16x2_t, hsh));
+            const u16x2_t kf = __builtin_elementwise_sub_sat(one2, z);
+            km[p] = __builtin_bit_cast(uint32_t, zero2 - kf);
+            kb |= __builtin_bit_cast(uint32_t, kf) << p;
           }
       } else {
 #pragma unroll
@@ -577,17 +588,26 @@ __global__ __launch_bounds__(RW * 64, DROP ? 3 : 4) void attn_fwd_ring_kernel(co
           const uint32_t idx0 = row_idx + kt * 32 + 8 * g + 4 * hh;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const bool k = hq_keep(idx0 + i, key, thr);
-            sc[4 * g + i] = k ? sc[4 * g + i] : 0.f;
-            bits |= (uint32_t)k << (4 * g + i);
+            const int r = 4 * g + i;
+            kb |= (uint32_t)hq_keep(idx0 + i, key, thr) << ((r >> 1) + 16 * (r & 1));
           }
         }
+#pragma unroll
+        for (int p = 0; p < 8; ++p)
+          km[p] = ((kb >> p) & 1u ? 0xFFFFu : 0u) | ((kb >> (16 + p)) & 1u ? 0xFFFF0000u : 0u);
       }
-      my_bits[(size_t)kt * 64] = (uint16_t)bits;
+      // stored word: element r at bit kbit(r) (bytes 0 and 2 of kb)
+      my_bits[(size_t)kt * 64] = (uint16_t)((kb & 0xFFu) | ((kb >> 8) & 0xFF00u));
     }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      const bf16x8_t pb = pack_b(sc, s);
+      bf16x8_t pb = pack_b(sc, s);
+      if constexpr (DROP) {
+        typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+        u32x4 u = __builtin_bit_cast(u32x4, pb);
+        u &= u32x4{km[4 * s], km[4 * s + 1], km[4 * s + 2], km[4 * s + 3]};
+        pb = __builtin_bit_cast(bf16x8_t, u);
+      }
 #pragma unroll
       for (int d = 0; d < 2; ++d) o[d] = mfma32(tr8(tV, 0, lo_, s, d), pb, o[d]);
     }
@@ -834,7 +854,7 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
     for (int r = 0; r < 16; r += 2) {  // dS = P·(dP·mask·ksc − δ): mask as an all-ones/zero AND (v_bfe_i32)
       const f2_t P = {__builtin_amdgcn_exp2f(s_acc[r]), __builtin_amdgcn_exp2f(s_acc[r + 1])};
       f2_t dp = {p_acc[r], p_acc[r + 1]};
-      if constexpr (DROP) dp = f2_t{keep_and(dp.x, bits, r), keep_and(dp.y, bits, r + 1)};
+      if constexpr (DROP) dp = f2_t{keep_and(dp.x, bits, kbit(r)), keep_and(dp.y, bits, kbit(r + 1))};
       const f2_t v = (dp * ksc - dl2) * P;
       ds[r] = v.x; ds[r + 1] = v.y;
     }
@@ -969,7 +989,7 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
   f32x16_t dv[2] = {zero16, zero16}, dk[2] = {zero16, zero16};
   const int krel = lane & 31;
   const int hh_f = (krel >> 2) & 1;
-  const int r_f = (krel & 3) + 4 * (krel >> 3);
+  const int r_f = kbit((krel & 3) + 4 * (krel >> 3));   // bit position in the forward's keep word
   const float ksc = DROP ? kscale : 1.f;
   const f2_t ksc2 = {ksc, ksc};
   constexpr int UNR = NT > 0 ? NT : 1;
