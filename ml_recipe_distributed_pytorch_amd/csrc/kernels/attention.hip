@@ -413,7 +413,7 @@ __device__ __forceinline__ void wait_vm(int n) {
 }
 
 template <bool DROP, bool EVEN, int NT, int RAHEAD>
-__global__ __launch_bounds__(RW * 64, DROP ? 3 : 4) void attn_fwd_ring_kernel(const uint16_t* __restrict__ qkv,
+__global__ __launch_bounds__(RW * 64, 4) void attn_fwd_ring_kernel(const uint16_t* __restrict__ qkv,
                                                                    const float* __restrict__ key_bias,
                                                                    uint16_t* __restrict__ ctx, float* __restrict__ lse,
                                                                    uint16_t* __restrict__ mbits, int L, int nh,
