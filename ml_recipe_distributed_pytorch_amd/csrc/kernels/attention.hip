@@ -720,7 +720,7 @@ __device__ __forceinline__ void split3(float x, uint16_t& hi, uint16_t& mid, uin
 // MODE 0: bf16 dQKV; 1: bf16 + e5m2 copy (fp8 backward, calibrating); 2: e5m2 only + column partials of the
 // QKV bias gradient into bpart [B·n32][3H] (fp8 backward, calibrated: every consumer reads the e5m2 copy)
 template <bool DROP, int NT, int RAHEAD, int MODE = 0>
-__global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
+__global__ __launch_bounds__(RW * 64, MODE == 0 && NT > 0 ? 4 : 3) void attn_bwd_dq_ring_kernel(
     const uint16_t* __restrict__ qkv, const uint16_t* __restrict__ dctx, const uint16_t* __restrict__ ctx,
     const float* __restrict__ lse, const float* __restrict__ key_bias, const uint16_t* __restrict__ mbits,
     float* __restrict__ delta, uint16_t* __restrict__ dqkv, int L, int nh, int n_qb, float c_scale, float scale,
@@ -731,7 +731,7 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
   constexpr int RNS = RAHEAD + 2;
   const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
   char* ring = reinterpret_cast<char*>(smem);                       // [RNS][K 4 KB | V 4 KB]
-  uint4* sA = reinterpret_cast<uint4*>(ring + RNS * 2 * RTILE);     // [Lp] A' words (b_hi,b_lo|1,1|1,0|0)
+  uint32_t* sA = reinterpret_cast<uint32_t*>(ring + RNS * 2 * RTILE);  // [Lp] A' word 0 (b_hi,b_lo); 1-3 constant
   uint16_t* sM = reinterpret_cast<uint16_t*>(sA + Lp);              // [RW][n32][64] dropout words
   const int nblk = gridDim.x, ob = blockIdx.x, xcd = ob & 7, qq = nblk >> 3, rr = nblk & 7;
   const int lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (ob >> 3);
@@ -785,7 +785,7 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
     const float bl = t < L ? key_bias[(size_t)b * L + t] * LOG2E : -1e30f;
     const uint16_t hi = bf16_rne(bl);
     const uint16_t lo = t < L ? bf16_rne(bl - hq_bf2f(hi)) : 0;
-    sA[t] = make_uint4((uint32_t)hi | ((uint32_t)lo << 16), 0x3F803F80u, 0x3F80u, 0u);
+    sA[t] = (uint32_t)hi | ((uint32_t)lo << 16);
   }
   const int kv_off = dma_lane_off(wave * 8, ld, lane) + wave * 8 * ld;
   auto stage = [&](int kt) {
@@ -821,7 +821,7 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
   }
   LdsOffsets lo_;
   lo_.init(lane);
-  const uint4* aug_src = sA + (lane & 31);
+  const uint32_t* aug_src = sA + (lane & 31);
   const uint16_t* my_bits = sM + wave * n32 * 64 + lane;
   const f32x16_t zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   f32x16_t dq[2] = {zero16, zero16};
@@ -834,8 +834,7 @@ __global__ __launch_bounds__(RW * 64, 3) void attn_bwd_dq_ring_kernel(
     const char* sK = ring + (kt % RNS) * 2 * RTILE;
     const uint16_t* tK = reinterpret_cast<const uint16_t*>(sK);
     const uint16_t* tV = reinterpret_cast<const uint16_t*>(sK + RTILE);
-    const uint4 aw = aug_src[kt * 32];
-    const bf16x8_t ka = __builtin_bit_cast(bf16x8_t, u32x4{aw.x, aw.y, aw.z, aw.w});
+    const bf16x8_t ka = __builtin_bit_cast(bf16x8_t, u32x4{aug_src[kt * 32], 0x3F803F80u, 0x3F80u, 0u});
     f32x16_t s_acc = mfma32(row8(tK, 0, lo_, 0), qf[0], zero16);
 #pragma unroll
     for (int s = 1; s < 4; ++s) s_acc = mfma32(row8(tK, 0, lo_, s), qf[s], s_acc);
@@ -1170,8 +1169,11 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
   (void)deterministic;   // both backward kernels are deterministic (no atomics)
   {
     const int nb = (L + RQ - 1) / RQ;                 // 128-row blocks (queries for dQ, keys for dK/dV)
-    constexpr int AH = 3;
-    const size_t lds_dq = (size_t)(AH + 2) * 2 * RTILE + Lp * sizeof(uint4) + (bits ? (size_t)RW * n32 * 128 : 0);
+    // ring depth: 2 tiles ahead on the bf16 path (39.5 KB of LDS per workgroup at L = 384 with dropout, so
+    // 4 workgroups — 4 waves per SIMD — share a CU), 3 on the fp8 paths (their e5m2 epilogues need > 128 VGPRs)
+    constexpr int AH = 2, AH8 = 3;
+    const size_t lds_dq = (size_t)((dqkv8 ? AH8 : AH) + 2) * 2 * RTILE + Lp * sizeof(uint32_t) +
+                          (bits ? (size_t)RW * n32 * 128 : 0);
     const size_t lds_kv = 2 * (size_t)(2 * RTILE + 512 + 128 + RW * 128);
     // dQ and dK/dV grids are the same size: partials [dQ waves | dK/dV waves], one fold after both
     const int nparts = B * nh * nb * RW;
@@ -1188,11 +1190,11 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
                            L, nh, nb, scale * LOG2E, scale, ks, dqkv8, q8, part8, phase, bpart);
       };
       if (dqkv8 && bpart) {   // --precision fp8, calibrated: e5m2 + bias partials, no bf16
-        if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH, 2>, attn_bwd_dkdv_ring_kernel<true, NT, 2>);
-        else launch(attn_bwd_dq_ring_kernel<false, NT, AH, 2>, attn_bwd_dkdv_ring_kernel<false, NT, 2>);
+        if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH8, 2>, attn_bwd_dkdv_ring_kernel<true, NT, 2>);
+        else launch(attn_bwd_dq_ring_kernel<false, NT, AH8, 2>, attn_bwd_dkdv_ring_kernel<false, NT, 2>);
       } else if (dqkv8) {   // --precision fp8: the e5m2-writing variants
-        if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH, 1>, attn_bwd_dkdv_ring_kernel<true, NT, 1>);
-        else launch(attn_bwd_dq_ring_kernel<false, NT, AH, 1>, attn_bwd_dkdv_ring_kernel<false, NT, 1>);
+        if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH8, 1>, attn_bwd_dkdv_ring_kernel<true, NT, 1>);
+        else launch(attn_bwd_dq_ring_kernel<false, NT, AH8, 1>, attn_bwd_dkdv_ring_kernel<false, NT, 1>);
       } else {
         if (bits) launch(attn_bwd_dq_ring_kernel<true, NT, AH>, attn_bwd_dkdv_ring_kernel<true, NT>);
         else launch(attn_bwd_dq_ring_kernel<false, NT, AH>, attn_bwd_dkdv_ring_kernel<false, NT>);
