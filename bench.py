@@ -19,6 +19,12 @@ import sys
 import time
 from types import SimpleNamespace
 
+
+def _gemm_sched_label() -> str:
+    """'dynamic' / 'static': the persistent GEMM's tile schedule actually in effect in the kernel library."""
+    from ml_recipe_distributed_pytorch_amd._native import kernels
+    return "dynamic" if kernels().gemm_get_sched() else "static"
+
 METRIC = "samples/sec (whole node) BERT-base QA fine-tune seq=384 at 1/2/4/8 MI355X"   # BASELINE.json
 
 
@@ -275,7 +281,8 @@ def main():
            "reducer_buckets": reducer.n_buckets if reducer is not None else 0,
            "uid_via_store": reducer.uid_via_store if reducer is not None else None,
            "broadcast_done": reducer.broadcast_done if reducer is not None else None,
-           "gemm_sched": reducer.gemm_sched if reducer is not None else "static",
+           # the kernel library's setting in effect (HQ_GEMM_SCHED at load, or the reducer's choice)
+           "gemm_sched": _gemm_sched_label(),
            "comm_wait_ms": round(comm["comm_wait_ms"], 3) if "comm_wait_ms" in comm else None,
            "comm_span_ms": round(comm["comm_span_ms"], 3) if "comm_span_ms" in comm else None,
            "mfu_bf16_dense": round(value * flops_per_sample / (world * 2.5e15), 4),

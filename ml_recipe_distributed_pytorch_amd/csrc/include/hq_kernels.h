@@ -101,6 +101,7 @@ void hq_gemm_set_stagger(int v);   // v3 start offset of half the workgroups (un
 // only their share), 0 = static round-robin (tile = id + k·grid); HQ_GEMM_SCHED sets it, default 0 (the
 // DP reducer selects 1 when world > 1)
 void hq_gemm_set_sched(int v);
+int hq_gemm_get_sched();   // the setting in effect (HQ_GEMM_SCHED at load, or the last set)
 // Diagnostic: `blocks` workgroups (one per CU: 96 KiB LDS each) that spin for `usec` µs on stream s —
 // stands in for a collective kernel holding CUs while a GEMM runs (tools/gemm_contention_bench.py)
 // C[M,N] = A[M,K]·B[N,K]^T (+epilogue); P = GELU pre-activation (out for EPI_GELU, in for EPI_DGELU)

@@ -1559,6 +1559,7 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
 
 void hq_gemm_set_variant(int v) { g_gemm_variant = v; }
 void hq_gemm_set_stagger(int v) { g_gemm_stagger = v; }
+int hq_gemm_get_sched() { return g_gemm_sched; }
 void hq_gemm_set_sched(int v) {
   g_gemm_sched = v;
   if (v) {   // allocate the slots now, eagerly: a first GEMM inside a graph capture must not hipMalloc
