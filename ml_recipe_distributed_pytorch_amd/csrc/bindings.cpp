@@ -243,6 +243,61 @@ void gemm_tn(Tensor dy, Tensor x, Tensor out, bool accumulate, int64_t splits, c
              has_bias ? ptr<float>(*bias_out) : nullptr, (int)T, (int)N, (int)K, S, accumulate, cur_stream());
 }
 
+// --precision fp32: exact-f32 strided / batched GEMM (gemm_f32.hip).  C(z, i, j) = alpha·Σ_k A(z,i,k)·B(z,j,k)
+// (+ bias[j]) (+ R(z,i,j)), every operand addressed from its tensor's data_ptr by the given strides — the bounds
+// check below proves every element the grid touches lies inside its tensor's storage.
+namespace {
+void f32_span_check(const Tensor& t, const char* name, std::initializer_list<std::pair<int64_t, int64_t>> dims) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == F32, name, " must be a float32 GPU tensor");
+  int64_t hi = 0;
+  for (auto& d : dims) {
+    TORCH_CHECK(d.first >= 1 && d.second >= 0, name, ": bad extent/stride");
+    hi += (d.first - 1) * d.second;
+  }
+  const int64_t avail = (int64_t)(t.storage().nbytes() / 4) - t.storage_offset();
+  TORCH_CHECK(hi < avail, name, ": strided extent ", hi + 1, " exceeds the tensor's storage (", avail, " floats)");
+  TORCH_CHECK(((uintptr_t)t.data_ptr() & 15) == 0, name, " must be 16-byte aligned");
+}
+}  // namespace
+
+void gemm_f32(Tensor A, Tensor B, Tensor C, int64_t M, int64_t N, int64_t K, std::vector<int64_t> sa,
+              std::vector<int64_t> sb, std::vector<int64_t> sc, int64_t batch, int64_t nb_in, double alpha,
+              c10::optional<Tensor> bias, c10::optional<Tensor> R, int64_t ldr) {
+  // sa = {sa_i, sa_k, ba_out, ba_in}, sb = {sb_j, sb_k, bb_out, bb_in}, sc = {ldc, bc_out, bc_in}
+  TORCH_CHECK(sa.size() == 4 && sb.size() == 4 && sc.size() == 3, "gemm_f32: stride vectors");
+  TORCH_CHECK(M > 0 && N > 0 && K > 0 && batch >= 1 && nb_in >= 1 && batch % nb_in == 0, "gemm_f32: bad sizes");
+  TORCH_CHECK(M * N < (int64_t)1 << 31 && K < (int64_t)1 << 31, "gemm_f32: sizes exceed 32-bit tile indexing");
+  const int64_t nbo = batch / nb_in;
+  TORCH_CHECK(sa[1] == 1 || sa[0] == 1, "gemm_f32: A needs a unit i or k stride");
+  TORCH_CHECK(sb[1] == 1 || sb[0] == 1, "gemm_f32: B needs a unit j or k stride");
+  // float4 staging: the contiguous extent is a multiple of 4 and the other stride keeps quads 16-B aligned
+  if (sa[1] == 1) {
+    TORCH_CHECK(K % 4 == 0 && sa[0] % 4 == 0, "gemm_f32: k-contiguous A needs K % 4 == 0, sa_i % 4 == 0");
+  } else {
+    TORCH_CHECK(M % 4 == 0 && sa[1] % 4 == 0, "gemm_f32: i-contiguous A needs M % 4 == 0, sa_k % 4 == 0");
+  }
+  if (sb[1] == 1) {
+    TORCH_CHECK(K % 4 == 0 && sb[0] % 4 == 0, "gemm_f32: k-contiguous B needs K % 4 == 0, sb_j % 4 == 0");
+  } else {
+    TORCH_CHECK(N % 4 == 0 && sb[1] % 4 == 0, "gemm_f32: j-contiguous B needs N % 4 == 0, sb_k % 4 == 0");
+  }
+  TORCH_CHECK(sa[2] % 4 == 0 && sa[3] % 4 == 0 && sb[2] % 4 == 0 && sb[3] % 4 == 0, "gemm_f32: batch strides % 4");
+  f32_span_check(A, "A", {{M, sa[0]}, {K, sa[1]}, {nbo, sa[2]}, {nb_in, sa[3]}});
+  f32_span_check(B, "B", {{N, sb[0]}, {K, sb[1]}, {nbo, sb[2]}, {nb_in, sb[3]}});
+  f32_span_check(C, "C", {{M, sc[0]}, {N, 1}, {nbo, sc[1]}, {nb_in, sc[2]}});
+  const bool has_r = R.has_value() && R->defined();
+  if (has_r) f32_span_check(*R, "R", {{M, ldr}, {N, 1}, {nbo, sc[1]}, {nb_in, sc[2]}});
+  const bool has_b = bias.has_value() && bias->defined();
+  if (has_b) { check(*bias, F32, "bias"); TORCH_CHECK(bias->numel() == N, "gemm_f32: bias must hold N"); }
+  c10::DeviceGuard g(A.device());
+  const int ks = hq_gemm_f32_splits((int)M, (int)N, (int)K, (int)batch);
+  Tensor ws = ks > 1 ? at::empty({ks, M, N}, C.options()) : Tensor();
+  hq_gemm_f32(ptr<float>(A), ptr<float>(B), ptr<float>(C), has_b ? ptr<float>(*bias) : nullptr,
+              has_r ? ptr<float>(*R) : nullptr, ks > 1 ? ptr<float>(ws) : nullptr, (int)M, (int)N, (int)K, sa[0], sa[1],
+              sb[0], sb[1], (int)sc[0], (int)ldr, (int)batch, (int)nb_in, sa[2], sa[3], sb[2], sb[3], sc[1], sc[2],
+              (float)alpha, ks, cur_stream());
+}
+
 // fp8 weight gradient: out [N,K] f32 (+)= (dy8ᵀ·x8)·sa·sb, dy8 e5m2 [T,N], x8 e4m3 [T,K] (token-major)
 int64_t gemm_tn8_splits(int64_t T, int64_t N, int64_t K) { return hq_gemm_tn8_splits((int)T, (int)N, (int)K); }
 
@@ -736,6 +791,9 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("gemm_tn", &gemm_tn, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("accumulate") = false,
         py::arg("splits") = 0, py::arg("bias_out") = py::none());
   m.def("gemm_tn_splits", &gemm_tn_splits);
+  m.def("gemm_f32", &gemm_f32, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("M"), py::arg("N"), py::arg("K"),
+        py::arg("sa"), py::arg("sb"), py::arg("sc"), py::arg("batch") = 1, py::arg("nb_in") = 1, py::arg("alpha") = 1.0,
+        py::arg("bias") = py::none(), py::arg("R") = py::none(), py::arg("ldr") = 0);
   m.def("attn_set_force_slow", [](int64_t v) { hq_attn_set_force_slow((int)v); });
   m.def("transpose_tiles", &transpose_tiles);
   m.def("transpose_tiles8", &transpose_tiles8);

@@ -116,6 +116,15 @@ void hq_gemm_nt(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
                 float* part, int M, int N, int K, int lda, int ldb, int ldc, int epi, int bn, hipStream_t s,
                 float drop_p = 0.f, uint32_t drop_seed = 0, uint32_t drop_opid = 0, float* ws = nullptr);
 
+// Exact-fp32 strided GEMM on the f32 MFMA (gemm_f32.hip, --precision fp32): C = alpha·A·Bᵀ (+bias[j]) (+R),
+// A(i,k) = A[i·sa_i + k·sa_k], B(j,k) = B[j·sb_j + k·sb_k] (sa_k == 1 or sa_i == 1; likewise B), batch z =
+// outer·nb_in + inner with per-operand strides (C and R share C's); ksplit > 1 (batch 1): ws holds ksplit M·N slabs.
+int hq_gemm_f32_splits(int M, int N, int K, int batch);
+void hq_gemm_f32(const float* A, const float* B, float* C, const float* bias, const float* R, float* ws, int M, int N,
+                 int K, long long sa_i, long long sa_k, long long sb_j, long long sb_k, int ldc, int ldr, int batch,
+                 int nb_in, long long ba_out, long long ba_in, long long bb_out, long long bb_in, long long bc_out,
+                 long long bc_in, float alpha, int ksplit, hipStream_t s);
+
 // Weight-gradient GEMM (gemm_tn.hip): out[N,K] (+)= Aᵀ·B, A = dy [T,N] bf16, B = x [T,K] bf16 (token-major),
 // split-K over T into S fp32 slabs part[S][N][K] (caller-provided) reduced into out; with bout != null
 // also the fused bias gradient bout[N] (+)= Σ_t A[t, n] through slabs bpart[S][N].

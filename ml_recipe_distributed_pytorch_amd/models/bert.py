@@ -194,7 +194,7 @@ class _LayerFn(torch.autograd.Function):
         s8 = m.fp8_states(idx) if fp8 else None
         # LayerNorm z only when the backward needs it (ops.LN_FROM_Y: recomputed from y on the GPU, for the
         # LayerNorms whose weights pass the |β| <= R·|γ| guard, BertForQuestionAnswering.refresh_ln_modes)
-        keep_z = not (x.is_cuda and ops.LN_FROM_Y)
+        keep_z = not (x.is_cuda and x.dtype != torch.float32 and ops.LN_FROM_Y)
         keep_z1 = keep_z or not m.ln_from_y_ok(idx, 0)
         keep_z2 = keep_z or not m.ln_from_y_ok(idx, 1)
         if fp8:
@@ -573,7 +573,13 @@ class BertForQuestionAnswering(nn.Module):
         res = super().load_state_dict(state_dict, strict=strict)
         self.store.mark_master_dirty()
         self.store.sync_compute()
-        self._ln_y = None   # new LayerNorm weights: re-run the from-y guard before the next forward
+        # new LayerNorm weights: re-run the from-y guard NOW (outside any graph capture — its one device→host
+        # read must never land inside a capture of the next forward) and bump the mode version, which makes a
+        # TrainEngine with live graphs re-capture them
+        self._ln_y = None
+        self._ln_pending = None
+        self.refresh_ln_modes()
+        self.ln_mode_version = getattr(self, "ln_mode_version", 0) + 1
         return res
 
     # -------------------------------------------------------------------- LayerNorm-from-y guard
@@ -591,13 +597,42 @@ class BertForQuestionAnswering(nn.Module):
         """Re-evaluate, per encoder LayerNorm, whether the from-y backward is safe: every column has γ != 0 and
         |β| <= LN_FROM_Y_MAX_RATIO·|γ|; a LayerNorm that fails stores z instead.  One small device→host read.
         Returns True when a LayerNorm changed mode (a captured HIP graph must then be re-captured)."""
+        return self._apply_ln_flags(self._ln_flags().tolist())
+
+    def _ln_flags(self) -> torch.Tensor:
         names = self._ln_names()
         g = torch.stack([self.store.view(n + ".weight", "master") for n in names]).abs()
         b = torch.stack([self.store.view(n + ".bias", "master") for n in names]).abs()
-        ok = ((g > 0) & (b <= self.LN_FROM_Y_MAX_RATIO * g)).all(1).tolist()
+        return ((g > 0) & (b <= self.LN_FROM_Y_MAX_RATIO * g)).all(1)
+
+    def _apply_ln_flags(self, ok) -> bool:
         old = getattr(self, "_ln_y", None)
         self._ln_y = [bool(v) for v in ok]
-        return old is not None and old != self._ln_y
+        changed = old is not None and old != self._ln_y
+        if changed:
+            self.ln_mode_version = getattr(self, "ln_mode_version", 0) + 1
+        return changed
+
+    def poll_ln_modes(self) -> bool:
+        """Asynchronous form of ``refresh_ln_modes`` for the training loop (no host sync, ever): applies the
+        flags of the check launched at the previous call if its copy has landed, then launches the next check
+        (a few tiny kernels + a non-blocking copy into pinned memory behind an event) on the current stream.
+        A γ / β update that leaves the guard's region is picked up one to two optimizer steps later.
+        Returns True when a LayerNorm changed mode."""
+        changed = False
+        pend = getattr(self, "_ln_pending", None)
+        if pend is not None:
+            host, ev = pend
+            if not ev.query():
+                return False          # still in flight: keep it, launch nothing new
+            changed = self._apply_ln_flags(host.tolist())
+        flags = self._ln_flags()
+        host = torch.empty(flags.shape, dtype=torch.bool, pin_memory=True)
+        host.copy_(flags, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._ln_pending = (host, ev)
+        return changed
 
     def ln_from_y_ok(self, idx: int, which: int) -> bool:
         """Layer ``idx``'s LayerNorm ``which`` (0 = attention output, 1 = FFN output) may skip storing z."""

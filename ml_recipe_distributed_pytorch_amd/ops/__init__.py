@@ -5,6 +5,8 @@
   epilogues for every encoder projection forward and dgrad, ``gemm_tn.hip`` split-K weight gradients).
   No vendor BLAS: an untileable shape raises.
 * CPU tensors → ``ops.reference`` (pure PyTorch, fp32), which is also the numerics oracle.
+* fp32 GPU tensors (``--precision fp32``, the reference's Apex-off mode) → ``ops.f32``: every GEMM-shaped product
+  on the own exact-f32 MFMA kernel (``gemm_f32.hip``), the row-wise / elementwise parts as the fp32 oracle ops.
 """
 from __future__ import annotations
 
@@ -13,6 +15,7 @@ from typing import Optional
 
 import torch
 
+from . import f32
 from . import reference as ref
 from . import rng  # noqa: F401
 from .._native import kernels
@@ -23,8 +26,13 @@ def _k():
 
 
 # ------------------------------------------------------------------------------------ embedding
+def _hip(t) -> bool:
+    """The bf16 / fp8 fused-kernel path handles this GPU tensor (fp32 GPU tensors take ``ops.f32``)."""
+    return t.is_cuda and t.dtype != torch.float32
+
+
 def embed_fwd(ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, beta, eps, p, seed, opid, out_dtype):
-    if ids.is_cuda:
+    if _hip(w_word):
         return tuple(_k().embed_fwd(ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, beta,
                                     float(eps), float(p), int(seed), int(opid)))
     return ref.embed_fwd(ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, beta, eps, p, seed, opid, out_dtype)
@@ -34,7 +42,7 @@ def embed_bwd(dy, ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, mean, rs
               g_word, g_pos, g_type, g_gamma, g_beta, accumulate, pad_word=-1, pad_pos=-1, seq_len=0):
     """``seq_len`` = L of the [B, L] token layout (0: unknown) — lets the kernel walk one position across
     the batch and sum the position-embedding gradient in registers."""
-    if dy.is_cuda:
+    if _hip(dy):
         return _k().embed_bwd(dy, ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, mean, rstd, float(p),
                               int(seed), int(opid), g_word, g_pos, g_type, g_gamma, g_beta, bool(accumulate),
                               int(pad_word), int(pad_pos), int(seq_len))
@@ -54,7 +62,7 @@ def _z_or_none(out):
 def ln_fwd(a, resid, gamma, beta, eps, p, seed, opid, store_z: bool = True):
     """(y, z, mean, rstd).  ``store_z=False`` (GPU): z is not written and comes back None — the backward then
     recomputes x̂ from y (``ln_bwd(..., beta=β)`` with y in z's place), one 2-byte/element store less."""
-    if a.is_cuda:
+    if _hip(a):
         return _z_or_none(_k().ln_fwd(a, resid, gamma, beta, float(eps), float(p), int(seed), int(opid),
                                       store_z=bool(store_z)))
     return ref.ln_fwd(a, resid, gamma, beta, eps, p, seed, opid)
@@ -69,7 +77,7 @@ def ln_fwd_q8(a, resid, gamma, beta, eps, p, seed, opid, state: "Fp8DelayedState
 
 def ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate, beta=None):
     """(dz, da).  ``beta`` given: ``z`` is the forward output y and x̂ = (y − β)/γ."""
-    if dy.is_cuda:
+    if _hip(dy):
         return tuple(_k().ln_bwd(dy, dy2, z, gamma, mean, rstd, float(p), int(seed), int(opid),
                                  g_gamma, g_beta, g_bias, bool(accumulate), beta=beta))
     return ref.ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate, beta=beta)
@@ -88,13 +96,13 @@ def ln_bwd_q8(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_b
 
 # ------------------------------------------------------------------------------------------ GELU
 def gelu_fwd(pre):
-    if pre.is_cuda:
+    if _hip(pre):
         return _k().gelu_fwd(pre)
     return ref.gelu_fwd(pre)
 
 
 def gelu_bwd(dout, pre, g_bias, accumulate):
-    if dout.is_cuda:
+    if _hip(dout):
         return _k().gelu_bwd(dout, pre, g_bias, bool(accumulate))
     return ref.gelu_bwd(dout, pre, g_bias, accumulate)
 
@@ -103,6 +111,9 @@ def gelu_bwd(dout, pre, g_bias, accumulate):
 def attn_fwd(qkv, key_bias, B, L, nh, p, seed, opid, scale):
     """Returns (ctx [T,H], lse [B,nh,L] fp32, keep-bits or None).  The HIP forward stores the dropout
     keep-bits it drew so the backward never re-hashes; the CPU reference regenerates them."""
+    if f32.active(qkv):
+        ctx, lse = f32.attn_fwd(qkv, key_bias, B, L, nh, p, seed, opid, scale)
+        return ctx, lse, None
     if qkv.is_cuda:
         ctx, lse, bits = _k().attn_fwd(qkv, key_bias, int(B), int(L), int(nh), float(p), int(seed), int(opid),
                                        float(scale))
@@ -139,6 +150,8 @@ def attn_bwd_q8(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, scale, state: 
 
 
 def attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, B, L, nh, p, seed, opid, scale):
+    if f32.active(dctx):
+        return f32.attn_bwd(dctx, qkv, ctx, lse, key_bias, B, L, nh, p, seed, opid, scale)
     if dctx.is_cuda:
         return _k().attn_bwd(dctx, qkv, ctx, lse, key_bias, bits, int(B), int(L), int(nh), float(p), float(scale),
                              deterministic())
@@ -180,6 +193,8 @@ def _part(M: int, N: int, K: int, device):
 
 def linear_fwd(x, w, b, b32=None, kind: str = "plain"):
     """y = x·Wᵀ + b (MFMA NT kernel with the fp32 bias ``b32`` in its epilogue on the GPU)."""
+    if f32.active(x):
+        return f32.linear_fwd(x, w, b)
     if x.is_cuda:
         _check_nt(x.shape[0], w.shape[0], x.shape[1], f"linear_fwd[{kind}]")
         return _k().gemm_nt(x, w, _EPI_BIAS, bias=_bias32(b, b32))
@@ -191,7 +206,7 @@ def linear_bdr_ln_fwd(x, w, b, b32, resid, kind, gamma, beta, eps, p, seed, opid
     ``ln_fwd`` computes.  On the GPU with ``LN_FUSE`` the GEMM's EPI_BDR epilogue adds the dropped-out
     projection to the residual and stores z, and the LayerNorm reads z alone (``ln_fwd`` with resid=None);
     otherwise the two ops run as before."""
-    if x.is_cuda and LN_FUSE and x.shape[0] * w.shape[0] < 2 ** 32:
+    if _hip(x) and LN_FUSE and x.shape[0] * w.shape[0] < 2 ** 32:
         _check_nt(x.shape[0], w.shape[0], x.shape[1], f"linear_bdr_ln_fwd[{kind}]")
         z = _k().gemm_nt(x, w, _EPI_BDR, bias=_bias32(b, b32), resid=resid, p=float(p), seed=int(seed), opid=int(opid))
         return tuple(_k().ln_fwd(z, None, gamma, beta, float(eps), 0.0, 0, 0))
@@ -320,20 +335,20 @@ def linear_wgrad_fp8(dy8, dy_state: Fp8DelayedState, x8, x_state: Fp8DelayedStat
 def linear_gelu_fwd(x, w, b, b32=None):
     """(pre, act) with pre = x·Wᵀ + b, act = gelu(pre) — the CPU oracle form; the GPU uses
     ``linear_gelu_fwd_d`` (derivative stored instead of pre)."""
-    if x.is_cuda:
+    if _hip(x):
         _check_nt(x.shape[0], w.shape[0], x.shape[1], "linear_gelu_fwd")
         pre = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
         act = _k().gemm_nt(x, w, _EPI_GELU, bias=_bias32(b, b32), pre=pre)
         return pre, act
-    pre = ref.linear_fwd(x, w, b)
+    pre = f32.linear_fwd(x, w, b) if f32.active(x) else ref.linear_fwd(x, w, b)
     return pre, gelu_fwd(pre)
 
 
 def linear_gelu_fwd_d(x, w, b, b32=None):
     """(saved, act, is_deriv).  GPU: one MFMA GEMM whose epilogue evaluates Φ and φ once and stores
     gelu'(pre) (bf16) beside act, so the backward needs one multiply per element (``linear_dgrad_gelu_d``);
-    CPU: (pre, act, False)."""
-    if x.is_cuda:
+    CPU / fp32 GPU: (pre, act, False)."""
+    if _hip(x):
         _check_nt(x.shape[0], w.shape[0], x.shape[1], "linear_gelu_fwd_d")
         gd = torch.empty(x.shape[0], w.shape[0], dtype=x.dtype, device=x.device)
         act = _k().gemm_nt(x, w, _EPI_GELUD, bias=_bias32(b, b32), pre=gd)
@@ -358,6 +373,8 @@ def linear_dgrad_gelu_d(dy, w, saved, is_deriv, g_bias, accumulate, wt=None):
 
 def linear_dgrad(dy, w, wt=None):
     """dy·W.  GPU: NT kernel on the Wᵀ working copy ``wt`` (ParamStore.view_t)."""
+    if f32.active(dy):
+        return f32.linear_dgrad(dy, w)
     if dy.is_cuda:
         assert wt is not None, "GPU dgrad needs the Wᵀ working copy"
         _check_nt(dy.shape[0], w.shape[1], dy.shape[1], "linear_dgrad")
@@ -367,6 +384,8 @@ def linear_dgrad(dy, w, wt=None):
 
 def linear_dgrad_add(dy, w, resid, wt=None):
     """resid + dy·W (fuses the residual-gradient add)."""
+    if f32.active(dy):
+        return f32.linear_dgrad(dy, w, resid)
     if dy.is_cuda:
         assert wt is not None, "GPU dgrad needs the Wᵀ working copy"
         _check_nt(dy.shape[0], w.shape[1], dy.shape[1], "linear_dgrad_add")
@@ -377,6 +396,8 @@ def linear_dgrad_add(dy, w, resid, wt=None):
 def linear_dgrad_gelu(dy, w, pre, g_bias, accumulate, wt=None):
     """dpre = (dy·W) ⊙ gelu'(pre) and g_bias (+)= Σ_rows dpre — the dgrad of the layer after GELU
     fused with the GELU backward and the bias gradient of the layer before it."""
+    if f32.active(dy):
+        return ref.gelu_bwd(f32.linear_dgrad(dy, w), pre, g_bias, accumulate)
     if dy.is_cuda:
         assert wt is not None, "GPU dgrad needs the Wᵀ working copy"
         M, N = dy.shape[0], w.shape[1]
@@ -393,6 +414,8 @@ def linear_wgrad(dy, x, g_w, g_b, accumulate):
     """g_w (fp32 arena view) (+)= dyᵀ·x with fp32 GEMM output; g_b (+)= column sums of dy.
     GPU: the split-K TN MFMA kernel (gemm_tn.hip) with the bias gradient fused; raises for shapes it does
     not tile (N, K multiples of 128)."""
+    if f32.active(dy):
+        return f32.linear_wgrad(dy, x, g_w, g_b, accumulate)
     if dy.is_cuda:
         T, N = dy.shape
         K = x.shape[1]
@@ -413,6 +436,6 @@ def colsum_into(part, out, accumulate):
 
 
 def bias_grad(dy, g_b, accumulate):
-    if dy.is_cuda:
+    if _hip(dy):
         return _k().bias_grad(dy, g_b, bool(accumulate))
     ref._acc(g_b, dy.float().sum(0), accumulate)

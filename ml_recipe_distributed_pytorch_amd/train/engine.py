@@ -132,7 +132,9 @@ class TrainEngine:
         self._graph_warm = 0
         self.graph_replays = 0
         self._steps = 0
-        self.ln_check_every = 100   # optimizer steps between re-runs of the LayerNorm-from-y weight guard
+        # optimizer steps between launches of the (asynchronous, sync-free) LayerNorm-from-y weight guard
+        self.ln_check_every = 10
+        self._ln_version = getattr(model, "ln_mode_version", 0)
         self.graph_eager_steps = 0              # micro-steps of an uncaptured shape run eagerly beside the graphs
 
     @property
@@ -157,8 +159,18 @@ class TrainEngine:
 
     @staticmethod
     def _shape_key(inputs, labels):
-        return tuple((k, tuple(v.shape), v.dtype) for d in (inputs, labels) for k, v in sorted(d.items())
-                     if torch.is_tensor(v))
+        """Tensor shapes/dtypes AND every non-tensor value (e.g. a merged batch's ``segment_lengths`` tuple):
+        a replay refreshes only the captured tensors, so a host value the captured step read (the module-path
+        loss slices each segment by its L_s) must select its own graph, never replay a stale one."""
+        def part(k, v):
+            if torch.is_tensor(v):
+                return (k, tuple(v.shape), v.dtype)
+            try:
+                hash(v)
+            except TypeError:
+                v = repr(v)
+            return (k, "value", v)
+        return tuple(part(k, v) for d in (inputs, labels) for k, v in sorted(d.items()))
 
     def _kind(self):
         k = self.micro % self.batch_split
@@ -235,12 +247,23 @@ class TrainEngine:
         return self._apply()
 
     def _check_ln_modes(self):
-        """Fine-tuning moves γ / β: re-run the model's LayerNorm-from-y guard (one tiny device→host read every
-        ``ln_check_every`` steps); a LayerNorm that changes mode invalidates the captured graphs."""
+        """Fine-tuning moves γ / β: re-run the model's LayerNorm-from-y guard every ``ln_check_every`` steps —
+        asynchronously (``poll_ln_modes``: device flags copied into pinned memory behind an event, applied at the
+        next check, no host sync); a LayerNorm that changes mode invalidates the captured graphs."""
         from .. import ops
-        refresh = getattr(self.model, "refresh_ln_modes", None)
-        if refresh is not None and ops.LN_FROM_Y and refresh() and self._graphs:
-            self.release_graph()
+        poll = getattr(self.model, "poll_ln_modes", None)
+        if poll is not None and ops.LN_FROM_Y:
+            poll()
+        self._sync_ln_version()
+
+    def _sync_ln_version(self):
+        """Release the graphs when the model's LayerNorm modes changed since they were captured (a guard check, or
+        a ``load_state_dict`` — which re-runs the guard eagerly — between steps)."""
+        v = getattr(self.model, "ln_mode_version", 0)
+        if v != self._ln_version:
+            self._ln_version = v
+            if self._graphs:
+                self.release_graph()
 
     def release_graph(self):
         if self._graphs:
@@ -261,6 +284,7 @@ class TrainEngine:
         return self._pass(inputs, labels)
 
     def _pass(self, inputs, labels) -> Optional[StepResult]:
+        self._sync_ln_version()
         if self._graph_eligible():
             if (self._graph_warm >= 2 or self._graphs) and self._graph_capturable(inputs, labels):
                 return self._graph_micro_step(inputs, labels)

@@ -244,3 +244,28 @@ def test_finetune_module_train_modes():
     torch.manual_seed(0)
     b = m(ids, mask, tt)
     assert not torch.allclose(b["start_class"], ref["start_class"])
+
+
+def test_ln_guard_load_state_dict_bumps_version():
+    """load_state_dict re-runs the LayerNorm-from-y guard eagerly (never inside a later graph capture) and bumps
+    ``ln_mode_version``, which a TrainEngine compares before every pass to release stale graphs."""
+    cfg = get_config("bert-tiny-test")
+    m = BertForQuestionAnswering(cfg, precision="fp32", seed=1)
+    v0 = getattr(m, "ln_mode_version", 0)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    sd["transformer.encoder.layer.0.output.LayerNorm.weight"][3] = 0.0
+    m.load_state_dict(sd)
+    assert m._ln_y is not None and m._ln_y[1] is False          # already evaluated, no lazy refresh pending
+    assert m.ln_mode_version == v0 + 1
+
+
+def test_engine_graph_key_includes_segment_lengths():
+    """Two merged batches with the same padded length but different per-segment lengths must not share a
+    captured graph: the module-path loss slices by the host tuple ``segment_lengths``, which a replay
+    cannot refresh."""
+    from ml_recipe_distributed_pytorch_amd.train.engine import TrainEngine
+    ids = torch.zeros(4, 16, dtype=torch.int64)
+    a = TrainEngine._shape_key({"input_ids": ids}, {"segments": torch.tensor([12, 16]), "segment_lengths": (12, 16)})
+    b = TrainEngine._shape_key({"input_ids": ids}, {"segments": torch.tensor([16, 9]), "segment_lengths": (16, 9)})
+    c = TrainEngine._shape_key({"input_ids": ids}, {"segments": torch.tensor([16, 9]), "segment_lengths": (16, 9)})
+    assert a != b and b == c
