@@ -95,8 +95,12 @@ def test_fp32_model_gpu_matches_cpu(cuda, train):
     gpu.zero_grad()
     sum(v.sum() for v in oc.values()).backward()
     sum(v.sum() for v in og.values()).backward()
+    # relative per tensor, with an absolute floor at 1e-6 of the largest gradient (the key bias gradient is zero
+    # up to rounding: softmax is invariant to it)
+    gmax = max(float(p.grad.abs().max()) for p in cpu.parameters())
     for (n, pc), (_, pg) in zip(cpu.named_parameters(), gpu.named_parameters()):
-        assert _rel(pg.grad.cpu(), pc.grad) < 1e-3, n
+        err = float((pg.grad.cpu().double() - pc.grad.double()).abs().max())
+        assert err <= 1e-3 * float(pc.grad.abs().max()) + 1e-6 * gmax, (n, err)
 
 
 def test_fp32_train_steps_gpu(cuda):
