@@ -55,7 +55,9 @@ def parse():
                          "process; one micro-batch — 288 GB HBM3E holds it, the reference split it 128 ways)")
     ap.add_argument("--seq", type=int, default=384)
     ap.add_argument("--model", default="bert-base-uncased")
-    ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16"])
+    ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16", "emb_bf16"],
+                    help="gradient all-reduce wire dtype: every bucket fp32 / bf16, or only the embeddings bucket (the "
+                         "step's exposed comm tail) in bf16")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
                     help="compute precision; fp8 = OCP e4m3 forward projections and e5m2-gradient dgrads "
                          "(BASELINE config #5)")
@@ -238,6 +240,7 @@ def main():
     if launched:
         hqdist.barrier()
     torch.cuda.synchronize()
+    bytes0 = reducer.stats["bytes"] if reducer is not None else 0
     t0 = time.perf_counter()
     phase = {}
     for _ in range(args.steps):
@@ -249,10 +252,14 @@ def main():
         hqdist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if launched:   # the slowest rank's clock (a 1-rank all_reduce at world 1)
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    rank_ms = None
+    if launched:   # the slowest rank's clock (a 1-rank gather at world 1) + every rank's, for the spread
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device if backend == "nccl" else "cpu")
+        every = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(every, t)
+        rank_ms = [float(x.item()) / args.steps * 1e3 for x in every]
+        elapsed = max(float(x.item()) for x in every)
+    ar_bytes = ((reducer.stats["bytes"] - bytes0) / args.steps) if reducer is not None else 0
     final_loss = res.losses.to_floats().get("loss", float("nan"))
     comm = reducer.pop_timings() if reducer is not None else {}
     ms = elapsed / args.steps * 1e3
@@ -285,6 +292,13 @@ def main():
            "gemm_sched": _gemm_sched_label(),
            "comm_wait_ms": round(comm["comm_wait_ms"], 3) if "comm_wait_ms" in comm else None,
            "comm_span_ms": round(comm["comm_span_ms"], 3) if "comm_span_ms" in comm else None,
+           # multi-GPU diagnosis: per-rank step-time spread, bytes all-reduced per step (wire dtype), and the
+           # algorithm bandwidth those bytes achieved over the comm span (bytes / span; busbw = algbw·2(N-1)/N)
+           "rank_ms_min": round(min(rank_ms), 3) if rank_ms else None,
+           "rank_ms_max": round(max(rank_ms), 3) if rank_ms else None,
+           "allreduce_bytes_per_step": int(ar_bytes) if reducer is not None else None,
+           "algbw_GBps": (round(ar_bytes / (comm["comm_span_ms"] * 1e-3) / 1e9, 1)
+                          if reducer is not None and comm.get("comm_span_ms") else None),
            "mfu_bf16_dense": round(value * flops_per_sample / (world * 2.5e15), 4),
            "max_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2),
            "final_loss": round(final_loss, 4)}

@@ -603,6 +603,26 @@ std::vector<Tensor> grad_norm(Tensor grad, double max_norm) {
   return {norm, coef};
 }
 
+// grad norm over the chunk table (ParamStore.norm_chunks): partials[c0:c1] on the current stream
+void sq_norm_chunks(Tensor grad, Tensor chunks, int64_t c0, int64_t c1, Tensor partials) {
+  check(grad, F32, "grad"); check(chunks, I64, "chunks"); check(partials, F32, "partials");
+  TORCH_CHECK(chunks.dim() == 2 && chunks.size(1) == 2 && partials.numel() == chunks.size(0), "chunk table / partials");
+  TORCH_CHECK(0 <= c0 && c0 <= c1 && c1 <= chunks.size(0), "chunk range");
+  c10::DeviceGuard g(grad.device());
+  hq_sq_norm_chunks(ptr<float>(grad), ptr<int64_t>(chunks), (int)c0, (int)c1, ptr<float>(partials), cur_stream());
+}
+
+// (norm, coef) from a complete partials vector (deterministic fixed-order sum)
+std::vector<Tensor> clip_from_partials(Tensor partials, double max_norm) {
+  check(partials, F32, "partials");
+  c10::DeviceGuard g(partials.device());
+  auto norm = at::empty({1}, partials.options());
+  auto coef = at::empty({1}, partials.options());
+  hq_clip_coef(ptr<float>(partials), (int)partials.numel(), (float)max_norm, ptr<float>(norm), ptr<float>(coef),
+               cur_stream());
+  return {norm, coef};
+}
+
 HqOptGroups groups_of(const std::vector<double>& lr, const std::vector<double>& wd) {
   TORCH_CHECK(lr.size() == wd.size() && lr.size() <= (size_t)kOptMaxGroups, "at most 8 param groups");
   HqOptGroups gr{};
@@ -836,6 +856,8 @@ PYBIND11_MODULE(_hq_kernels, m) {
      py::arg("L"), py::arg("nh"), py::arg("p"), py::arg("scale"), py::arg("deterministic"), py::arg("q8"), py::arg("phase"),
      py::arg("write_bf16") = true);
   m.def("grad_norm", &grad_norm);
+  m.def("sq_norm_chunks", &sq_norm_chunks);
+  m.def("clip_from_partials", &clip_from_partials);
   m.def("sq_norm_partials", [](Tensor x, int64_t nparts) {
     check(x, F32, "x");
     TORCH_CHECK(x.is_contiguous(), "x must be contiguous");
@@ -858,6 +880,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
       .def("broadcast", &HqReducer::broadcast, py::call_guard<py::gil_scoped_release>())
       .def("wait", &HqReducer::wait)
       .def("probe_f32", &HqReducer::probe_f32)
+      .def("sq_norm_chunks", &HqReducer::sq_norm_chunks)
       .def("fence_from", &HqReducer::fence_from)
       .def("synchronize", &HqReducer::synchronize, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("comm_stream", &HqReducer::comm_stream)

@@ -77,6 +77,8 @@ def build_kernels(jobs: int = 8, force: bool = False, verbose: bool = True, debu
               "-D__HIP_PLATFORM_AMD__=1", "-Wno-unused-result"]
     if debug:
         common += ["-DHQ_DEBUG=1", "-g1"]
+    # lab / A-B builds only (tools/build_ab_lib.py): extra defines for the kernel sources, e.g. -DHQ_EPI_DIAG=1
+    common += [f for f in os.environ.get("HQ_KERNEL_CFLAGS", "").split() if f.startswith("-D")]
     kernel_srcs = sorted(os.path.join(HERE, "kernels", f) for f in os.listdir(os.path.join(HERE, "kernels"))
                          if f.endswith(".hip"))
     runtime_srcs = sorted(os.path.join(HERE, "runtime", f) for f in os.listdir(os.path.join(HERE, "runtime"))

@@ -74,6 +74,9 @@ struct HqOptGroups {
   float wd[kOptMaxGroups];
 };
 void hq_sq_norm_partials(const float* g, int64_t n, float* partials, int nparts, hipStream_t s);
+// Σg² of chunks c0 … c1-1 of the grad arena (chunks: int64 [C][2] = start, numel; numel <= kNormChunk, % 4 == 0)
+constexpr int64_t kNormChunk = 1 << 18;
+void hq_sq_norm_chunks(const float* g, const int64_t* chunks, int c0, int c1, float* partials, hipStream_t s);
 void hq_clip_coef(const float* partials, int nparts, float max_norm, float* norm_out, float* coef_out, hipStream_t s);
 void hq_adamw(float* master, uint16_t* compute, const float* grad, float* m, float* v, const HqOptChunk* chunks,
               int nchunks, HqOptGroups groups, float beta1, float beta2, float eps, float step_size_mult,

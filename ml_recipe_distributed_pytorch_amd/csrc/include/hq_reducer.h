@@ -21,6 +21,9 @@ class HqReducer {
   // ordering probe (tests, HQ_REDUCER_VERIFY): after the same fence an all-reduce would take, the comm
   // stream writes deterministic per-block sum-of-squares partials of [ptr, ptr+count) to `partials`
   void probe_f32(int64_t ptr, int64_t count, int64_t partials, int nparts, int64_t compute_stream);
+  // grad-norm partials of chunks c0 … c1-1 (hq_sq_norm_chunks), on the comm stream right behind the bucket's
+  // all-reduce that produced them (no fence: stream order is the dependency)
+  void sq_norm_chunks(int64_t grad, int64_t chunks, int c0, int c1, int64_t partials);
   // comm stream waits for all work issued so far on `stream` (e.g. a side stream computing grads)
   void fence_from(int64_t stream);
   void synchronize();

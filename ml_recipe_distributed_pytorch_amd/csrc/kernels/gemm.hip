@@ -837,9 +837,14 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
 typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
+// HQ_EPI_DIAG (lab builds only, never in the production library): bit 0 = the persistent kernel's epilogue issues no
+// global stores (data kept live), bit 1 = GELUD skips the GELU math — isolates store cost from VALU cost.
+#ifndef HQ_EPI_DIAG
+#define HQ_EPI_DIAG 0
+#endif
 template <int EPI>
 struct NT3Epi {
-  static constexpr int kStores = 16 * (1 + (EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD ? 1 : 0));
+  static constexpr int kStores = (HQ_EPI_DIAG & 1) ? 0 : 16 * (1 + (EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD ? 1 : 0));
   static constexpr int kLoads = (EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR) ? 16 : 0;
   static constexpr int E = kStores + kLoads;   // vm ops per lane (the part store of waves 0-3 is not counted: a
 };                                             // smaller count only waits longer)
@@ -1158,7 +1163,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     // 64-wait-state pad that holds the last piece (and, for BIAS's back-to-back stores, every piece).
     auto bstore = [&](__amdgpu_buffer_rsrc_t r, int rnd, int it, const uint4& d) {
       const u32x4_t v = {d.x, d.y, d.z, d.w};
+#if HQ_EPI_DIAG & 1
+      asm volatile("" :: "v"(v));
+#else
       __builtin_amdgcn_raw_buffer_store_b128(v, r, vo_lane, so_of(rnd, it), 0);
+#endif
       return v;
     };
     float csum[8];
@@ -1278,7 +1287,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
           } else if constexpr (EPI == HQ_EPI_GELUD) {
             float x[8], g[8];
             hq_unpack8(piece, x);
+#if HQ_EPI_DIAG & 2
+            for (int e = 0; e < 8; ++e) g[e] = x[e];
+#else
             hq_gelu_grad8(x, g);   // g = gelu'(x), x = gelu(x)
+#endif
             sP = bstore(rP, q, it, hq_pack8(g));
             piece = hq_pack8(x);
           } else if constexpr (EPI == HQ_EPI_DMUL) {

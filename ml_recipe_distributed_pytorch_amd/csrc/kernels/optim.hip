@@ -31,6 +31,35 @@ __global__ __launch_bounds__(256) void sq_norm_kernel(const float* __restrict__ 
   if (threadIdx.x == 0) partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
+// Σg² of one chunk of the grad arena per block: chunk c = [chunks[2c], +chunks[2c+1]) (starts 16-B aligned, sizes % 4 == 0,
+// <= kNormChunk floats).  The chunk table cuts every readiness group of the arena into pieces, so a group's partials
+// are the same numbers whether the full pass writes them after the backward or the gradient reducer's comm stream
+// writes them right after that group's bucket all-reduce — the clip coefficient is bitwise the same either way.
+__global__ __launch_bounds__(256) void sq_norm_chunks_kernel(const float* __restrict__ g, const int64_t* __restrict__ chunks,
+                                                             int c0, float* __restrict__ partials) {
+  __shared__ float red[4];
+  const int c = c0 + blockIdx.x;
+  const float4* p = reinterpret_cast<const float4*>(g + chunks[2 * c]);
+  const int n4 = (int)(chunks[2 * c + 1] / 4);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int i = threadIdx.x;
+  for (; i + 3 * 256 < n4; i += 4 * 256) {   // four independent loads in flight per thread
+    const float4 a = p[i], b = p[i + 256], d = p[i + 512], e = p[i + 768];
+    s0 += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+    s1 += b.x * b.x + b.y * b.y + b.z * b.z + b.w * b.w;
+    s2 += d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w;
+    s3 += e.x * e.x + e.y * e.y + e.z * e.z + e.w * e.w;
+  }
+  for (; i < n4; i += 256) {
+    const float4 a = p[i];
+    s0 += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+  }
+  float s = hq_wave_sum((s0 + s1) + (s2 + s3));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partials[c] = red[0] + red[1] + red[2] + red[3];
+}
+
 __global__ __launch_bounds__(256) void clip_coef_kernel(const float* __restrict__ partials, int nparts, float max_norm,
                                                         float* __restrict__ norm_out, float* __restrict__ coef_out) {
   __shared__ float red[4];
@@ -164,6 +193,10 @@ int grid_for(int64_t n4) { return (int)std::max<int64_t>(1, std::min<int64_t>((n
 
 void hq_sq_norm_partials(const float* g, int64_t n, float* partials, int nparts, hipStream_t s) {
   hipLaunchKernelGGL(sq_norm_kernel, dim3(nparts), dim3(256), 0, s, g, n, partials);
+}
+
+void hq_sq_norm_chunks(const float* g, const int64_t* chunks, int c0, int c1, float* partials, hipStream_t s) {
+  if (c1 > c0) hipLaunchKernelGGL(sq_norm_chunks_kernel, dim3(c1 - c0), dim3(256), 0, s, g, chunks, c0, partials);
 }
 
 void hq_clip_coef(const float* partials, int nparts, float max_norm, float* norm_out, float* coef_out, hipStream_t s) {

@@ -111,6 +111,10 @@ void HqReducer::probe_f32(int64_t ptr, int64_t count, int64_t partials, int npar
   hq_sq_norm_partials((const float*)ptr, count, (float*)partials, nparts, (hipStream_t)stream_);
 }
 
+void HqReducer::sq_norm_chunks(int64_t grad, int64_t chunks, int c0, int c1, int64_t partials) {
+  hq_sq_norm_chunks((const float*)grad, (const int64_t*)chunks, c0, c1, (float*)partials, (hipStream_t)stream_);
+}
+
 void HqReducer::wait(int64_t compute_stream) {
   hipEvent_t e = (hipEvent_t)next_event();
   HIP_CHECK_THROW(hipEventRecord(e, (hipStream_t)stream_));

@@ -287,6 +287,25 @@ class ParamStore:
                 out.append((e.offset + r0 * row_numel, (r1 - r0) * row_numel, hf_name))
         return out
 
+    NORM_CHUNK = 1 << 18   # floats per grad-norm chunk (hq_kernels.h kNormChunk)
+
+    def norm_chunks(self):
+        """(chunk table int64 [C, 2] on the arena's device, {group: (c0, c1)}): every readiness group cut into pieces
+        of <= NORM_CHUNK floats.  The grad norm is the fixed-order sum of one Σg² partial per chunk, so it is the same
+        number whether the full pass computes every partial after the backward or the gradient reducer computes a
+        bucket's partials on its comm stream right after that bucket's all-reduce."""
+        cached = getattr(self, "_norm_chunks", None)
+        if cached is not None and cached[0].device == self.grad.device:
+            return cached
+        rows, spans = [], {}
+        for g, s, e in self.group_ranges():
+            c0 = len(rows)
+            for o in range(s, e, self.NORM_CHUNK):
+                rows.append([o, min(self.NORM_CHUNK, e - o)])
+            spans[g] = (c0, len(rows))
+        self._norm_chunks = (torch.tensor(rows, dtype=torch.int64).to(self.grad.device), spans)
+        return self._norm_chunks
+
     def group_ranges(self) -> List[Tuple[str, int, int]]:
         """Contiguous (group, start, end) ranges in arena order."""
         out: List[Tuple[str, int, int]] = []

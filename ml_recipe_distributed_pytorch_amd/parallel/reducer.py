@@ -7,7 +7,10 @@ bucket has reported, the bucket's all-reduce is issued immediately, so communica
 the remaining backward.  ``finalize()`` makes the compute stream wait for the last bucket.
 
 * GPU + nccl: the native C++ ``Reducer`` owns an RCCL communicator and a normal-priority comm
-  stream; ncclAvg in place on the arena slice (fp32) or through a bf16 scratch (``allreduce_dtype``).
+  stream; ncclAvg in place on the arena slice (fp32) or through a bf16 scratch (``allreduce_dtype``:
+  ``fp32`` | ``bf16`` for every bucket | ``emb_bf16`` — only the embeddings bucket in bf16: the 89 MiB word-
+  embedding gradient is produced by the LAST backward kernel, so its all-reduce is the one exposed tail of
+  the step; halving its bytes halves that tail while every other bucket stays exact fp32).
 * CPU / gloo (and GPU when ``native=False``): ``torch.distributed.all_reduce(async_op=True)``.
 * ``prepare(sync=False)`` = DDP ``no_sync``: no communication during accumulation micro-batches
   (fixes reference D1, which all-reduced every micro-batch).
@@ -20,6 +23,10 @@ the remaining backward.  ``finalize()`` makes the compute stream wait for the la
 * ``verify=True`` (or ``HQ_REDUCER_VERIFY=1``): the comm stream also records a deterministic checksum of
   every bucket at the exact point its all-reduce reads it; ``check_order()`` compares them with the final
   gradients — a bucket read before its (side-stream) weight-gradient GEMMs finished shows up as a mismatch.
+* Grad-norm partials (native path): right after a bucket's all-reduce (and bf16 cast-back) the comm stream writes
+  the Σg² partials of that bucket's chunks (``ParamStore.norm_chunks``), so when the last bucket lands the clip
+  coefficient needs one tiny fold instead of a pass over the whole 418 MiB arena on the step's critical path
+  (``norm_partials()``; bitwise the same coefficient as the full pass, ``train/optim.grad_norm_and_clip``).
 * ``timing=True``: HIP events on the compute and comm streams give the comm span and the EXPOSED wait
   (comm still running after the backward's last kernel) per synchronised step (``pop_timings()``).
 
@@ -44,10 +51,11 @@ _uid_counter = itertools.count()
 
 
 class Bucket:
-    __slots__ = ("index", "start", "end", "groups", "pending", "launched", "work")
+    __slots__ = ("index", "start", "end", "groups", "pending", "launched", "work", "dtype")
 
-    def __init__(self, index, start, end, groups):
+    def __init__(self, index, start, end, groups, dtype="fp32"):
         self.index, self.start, self.end, self.groups = index, start, end, list(groups)
+        self.dtype = dtype
         self.pending = len(self.groups)
         self.launched = False
         self.work = None
@@ -71,6 +79,7 @@ class GradReducer:
         self.force = bool(force)
         self.active = False
         self.buckets: List[Bucket] = []
+        self._bucket_chunks: Dict[int, Tuple[int, int]] = {}
         self.group_to_bucket: Dict[str, Bucket] = {}
         self._native = None
         self._scratch = None
@@ -103,6 +112,25 @@ class GradReducer:
         self._tev: List[tuple] = []
         self._first_ev = None
         self._build_buckets()
+        self._norm_parts = None
+        self._norm_ready = False
+        if self._native is not None:
+            chunks, spans = self.store.norm_chunks()
+            self._norm_chunks = chunks
+            self._norm_parts = torch.zeros(chunks.shape[0], dtype=torch.float32, device=self.store.device)
+            for b in self.buckets:   # a bucket's groups are consecutive arena ranges -> one contiguous chunk run
+                cs = [spans[g] for g in b.groups]
+                b_c0, b_c1 = min(c[0] for c in cs), max(c[1] for c in cs)
+                assert b_c1 - b_c0 == sum(c[1] - c[0] for c in cs), "bucket groups must be contiguous"
+                self._bucket_chunks[b.index] = (b_c0, b_c1)
+            # chunks of groups that no bucket carries (frozen parameters): computed on the compute stream at finalize
+            self._uncovered, at = [], 0
+            for c0, c1 in sorted(self._bucket_chunks.values()):
+                if c0 > at:
+                    self._uncovered.append((at, c0))
+                at = max(at, c1)
+            if at < chunks.shape[0]:
+                self._uncovered.append((at, int(chunks.shape[0])))
         model.set_grad_listener(self._on_group_ready)
         self.gemm_sched = self._pick_gemm_sched(on_gpu)
         # DDP-constructor broadcast whenever a process group exists (any world size: a 1-rank
@@ -154,7 +182,7 @@ class GradReducer:
             for hf, _, _ in e.views:
                 if hf in trainable:
                     group_has_trainable[e.group] = True
-        elem = 4 if self.allreduce_dtype == "fp32" else 2
+        elem = 2 if self.allreduce_dtype == "bf16" else 4
         buckets: List[Tuple[int, int, List[str]]] = []
         for g, s, e in self.store.group_ranges():
             if not group_has_trainable.get(g):
@@ -164,12 +192,21 @@ class GradReducer:
                 buckets[-1] = (bs, e, gs + [g])
             else:
                 buckets.append((s, e, [g]))
-        self.buckets = [Bucket(i, s, e, gs) for i, (s, e, gs) in enumerate(buckets)]
+        def bucket_dtype(gs):
+            if self.allreduce_dtype == "bf16" or (self.allreduce_dtype == "emb_bf16" and "embeddings" in gs):
+                return "bf16"
+            return "fp32"
+        self.buckets = [Bucket(i, s, e, gs, bucket_dtype(gs)) for i, (s, e, gs) in enumerate(buckets)]
         self.group_to_bucket = {g: b for b in self.buckets for g in b.groups}
-        if self.allreduce_dtype == "bf16" and self._native is not None and self.buckets:
-            n = max(b.numel for b in self.buckets)
+        if any(b.dtype == "bf16" for b in self.buckets) and self._native is not None:
             self._scratch = torch.empty(self.store.total, dtype=torch.bfloat16, device=self.store.device)
-        logger.info("grad buckets (MiB): " + ", ".join(f"{b.numel * elem / 2**20:.1f}" for b in self.buckets))
+        logger.info("grad buckets (MiB, dtype): " + ", ".join(
+            f"{b.numel * (2 if b.dtype == 'bf16' else 4) / 2**20:.1f} {b.dtype}" for b in self.buckets))
+
+    @property
+    def bytes_per_sync(self) -> int:
+        """Bytes one synchronising backward all-reduces (every bucket once, at its wire dtype)."""
+        return sum(b.numel * (2 if b.dtype == "bf16" else 4) for b in self.buckets)
 
     def broadcast_parameters(self):
         """Rank 0's weights to everyone (DDP constructor semantics)."""
@@ -195,6 +232,7 @@ class GradReducer:
 
     def prepare(self, sync: bool = True):
         self.active = sync and (self.world > 1 or self.force)
+        self._norm_ready = False
         for b in self.buckets:
             b.pending = len(b.groups)
             b.launched = False
@@ -216,7 +254,7 @@ class GradReducer:
         b.launched = True
         view = self.store.grad[b.start:b.end]
         self.stats["buckets_launched"] += 1
-        self.stats["bytes"] += b.numel * (2 if self.allreduce_dtype == "bf16" else 4)
+        self.stats["bytes"] += b.numel * (2 if b.dtype == "bf16" else 4)
         self._seq_hash = (self._seq_hash * 1_000_003 + b.index * 65_537 + b.numel) & 0x7FFFFFFFFFFFFFFF
         side = getattr(self.model, "grad_side_stream", None)
         if self._native is not None:
@@ -233,10 +271,13 @@ class GradReducer:
                     part = self._probes[b.index] = torch.empty(self._PROBE_PARTS, dtype=torch.float32,
                                                                device=self.store.device)
                 self._native.probe_f32(view.data_ptr(), b.numel, part.data_ptr(), self._PROBE_PARTS, stream)
-            if self.allreduce_dtype == "bf16":
+            if b.dtype == "bf16":
                 self._native.allreduce_bf16(view.data_ptr(), self._scratch[b.start:b.end].data_ptr(), b.numel, stream)
             else:
                 self._native.allreduce_f32(view.data_ptr(), b.numel, stream)
+            c0, c1 = self._bucket_chunks[b.index]
+            self._native.sq_norm_chunks(self.store.grad.data_ptr(), self._norm_chunks.data_ptr(), c0, c1,
+                                        self._norm_parts.data_ptr())
         else:
             if side is not None:
                 torch.cuda.current_stream().wait_stream(side)
@@ -262,6 +303,9 @@ class GradReducer:
                 self._tev.append((self._first_ev, done_bwd, done_comm))
                 self._first_ev = None
             self._native.wait(torch.cuda.current_stream().cuda_stream)
+            for c0, c1 in self._uncovered:
+                kernels().sq_norm_chunks(self.store.grad, self._norm_chunks, c0, c1, self._norm_parts)
+            self._norm_ready = True
         else:
             scale = None if dist.get_backend(self.group) == "nccl" else 1.0 / self.world
             for b in self.buckets:
@@ -270,6 +314,10 @@ class GradReducer:
                     if scale is not None:
                         self.store.grad[b.start:b.end].mul_(scale)
         self.active = False
+
+    def norm_partials(self) -> Optional[torch.Tensor]:
+        """The complete grad-norm partials of the step just finalized (native path), else None (full pass)."""
+        return self._norm_parts if self._norm_ready else None
 
     _PROBE_PARTS = 256
 

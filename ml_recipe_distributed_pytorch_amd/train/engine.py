@@ -329,7 +329,8 @@ class TrainEngine:
         if self.reducer is not None:
             self.reducer.finalize()
         timer.mark("comm_wait")
-        norm, coef = grad_norm_and_clip(self.model.store, self.max_grad_norm)
+        parts = self.reducer.norm_partials() if self.reducer is not None else None
+        norm, coef = grad_norm_and_clip(self.model.store, self.max_grad_norm, partials=parts)
         lr = self.optimizer.param_groups[0]["lr"]
         self.optimizer.step(clip_coef=coef)
         self.optimizer.zero_grad()

@@ -205,12 +205,19 @@ class FusedAdaMod(_ArenaOptimizer):
         return loss
 
 
-def grad_norm_and_clip(store: ParamStore, max_norm: float):
+def grad_norm_and_clip(store: ParamStore, max_norm: float, partials: Optional[torch.Tensor] = None):
     """Global L2 norm of the grad arena + clip coefficient, both as device scalars (no host sync).
-    Matches ``torch.nn.utils.clip_grad_norm_`` (coef = max_norm / (norm + 1e-6), clamped to 1)."""
+    Matches ``torch.nn.utils.clip_grad_norm_`` (coef = max_norm / (norm + 1e-6), clamped to 1).
+    GPU: one Σg² partial per chunk of ``store.norm_chunks()`` then a fixed-order fold; ``partials`` = a complete
+    vector already written (the gradient reducer's comm stream computes each bucket's partials right after its
+    all-reduce, so the step tail is only the fold) — bitwise the same result as the full pass."""
     g = store.grad
     if g.is_cuda:
-        norm, coef = kernels().grad_norm(g, float(max_norm))
+        if partials is None:
+            chunks, _ = store.norm_chunks()
+            partials = torch.empty(chunks.shape[0], dtype=torch.float32, device=g.device)
+            kernels().sq_norm_chunks(g, chunks, 0, chunks.shape[0], partials)
+        norm, coef = kernels().clip_from_partials(partials, float(max_norm))
         return norm, (coef if max_norm > 0 else None)
     norm = g.float().norm()
     coef = torch.clamp(max_norm / (norm + 1e-6), max=1.0) if max_norm > 0 else None

@@ -164,8 +164,9 @@ def get_trainer_parser() -> ArgumentParser:
     # --- MI355X additions -------------------------------------------------------------------
     parser.add_argument("--bucket_cap_mb", type=float, default=32.0,
                         help="Gradient bucket size (MiB of reduced dtype); sized for 7 xGMI links per GPU.")
-    parser.add_argument("--allreduce_dtype", type=str, default="fp32", choices=["fp32", "bf16"],
-                        help="Dtype of the gradient all-reduce payload.")
+    parser.add_argument("--allreduce_dtype", type=str, default="fp32", choices=["fp32", "bf16", "emb_bf16"],
+                        help="Dtype of the gradient all-reduce payload: fp32, bf16 (every bucket), or emb_bf16 (only "
+                             "the embeddings bucket, the exposed tail of the step, in bf16).")
     parser.add_argument("--no_sync_accum", type=cast2(int), default=1,
                         help="1: all-reduce only at the accumulation boundary (fix of D1); 0: every micro-batch.")
     parser.add_argument("--dist_timeout", type=float, default=1800.0, help="Process-group timeout in seconds.")

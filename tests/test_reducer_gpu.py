@@ -183,3 +183,33 @@ def test_gloo_rehearsal_two_ranks_share_one_gpu(cuda, tmp_path):
     assert rec["process_group"] == "gloo" and rec["world_size"] == 2, rec
     assert rec["hw_queues"] == 4, rec   # not raised: the two ranks share cuda:0
     assert rec["value"] > 0, rec
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "emb_bf16"])
+def test_comm_stream_norm_partials_equal_full_pass(cuda, dtype):
+    """The reducer's comm stream writes each bucket's grad-norm partials right after its all-reduce; folded, they
+    must give BITWISE the norm / clip coefficient of the full pass over the same final gradients (the 8-GPU step
+    tail then holds one fold instead of a 418 MiB pass).  emb_bf16: the embeddings bucket travels as bf16 — its
+    partials are taken after the cast back, i.e. over the gradients the optimizer reads."""
+    from ml_recipe_distributed_pytorch_amd._native import kernels
+    from ml_recipe_distributed_pytorch_amd.train.optim import grad_norm_and_clip
+    model, red, eng = _engine(cuda, dict(bucket_cap_mb=32.0, allreduce_dtype=dtype))
+    assert any(b.dtype == ("bf16" if dtype == "emb_bf16" else "fp32") for b in red.buckets)
+    if dtype == "emb_bf16":
+        assert [b.dtype for b in red.buckets if "embeddings" in b.groups] == ["bf16"]
+        assert all(b.dtype == "fp32" for b in red.buckets if "embeddings" not in b.groups)
+    inputs, labels = _batches(cuda, n=1)[0]
+    red.prepare(sync=True)
+    eng.loss_fn(model(**inputs), labels).backward()
+    red.finalize()
+    parts = red.norm_partials()
+    assert parts is not None
+    n1, c1 = grad_norm_and_clip(model.store, 1.0, partials=parts)
+    n2, c2 = grad_norm_and_clip(model.store, 1.0)
+    torch.cuda.synchronize()
+    assert torch.equal(n1, n2) and torch.equal(c1, c2), (n1.item(), n2.item())
+    ref = float(model.store.grad.double().norm())
+    assert abs(n1.item() - ref) <= 1e-5 * ref
+    red.prepare(sync=False)          # an accumulation micro-step: no partials, the engine takes the full pass
+    assert red.norm_partials() is None
+    red.close()
