@@ -91,3 +91,78 @@ def test_attention_repeatable(cuda):
         outs.append((ctx, lse, bits, dq))
     torch.cuda.synchronize()
     _same(outs, "attention")
+
+
+@pytest.mark.gpu
+def test_gemm_nt_v2_repeatable(cuda):
+    """The K = 3072 FFN2 forward at seq 512 (M = 131072: a whole number of tile waves, no half-tile tail) runs the
+    non-persistent v2 kernel, whose LDS-DMA pipeline was reworked in round 4 like the persistent one's."""
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(17)
+    Tm = 256 * 512
+    x = _bf((Tm, F), g, cuda, 0.5)
+    w = _bf((H, F), g, cuda, 0.05)
+    bias = torch.randn(H, device=cuda, generator=g) * 0.1
+    outs = [(k.gemm_nt(x, w, EPI_BIAS, bias=bias),) for _ in range(REPS)]
+    torch.cuda.synchronize()
+    _same(outs, "ffn2 fwd v2 (seq 512)")
+
+
+@pytest.mark.gpu
+def test_gemm_nt_cross_epilogue_exact(cuda):
+    """Exact guard against a store that writes the wrong register: the epilogues share the mainloop and its
+    accumulation order, so GELU's stored P (pre-activation) must equal BIAS's C bit for bit, and GELUD's C (act,
+    packed-FMA GELU) GELU's C (scalar GELU, same operations) bit for bit — at the headline FFN1 shape."""
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(23)
+    x = _bf((T, H), g, cuda, 0.5)
+    w = _bf((F, H), g, cuda, 0.05)
+    bias = torch.randn(F, device=cuda, generator=g) * 0.1
+    c_bias = k.gemm_nt(x, w, EPI_BIAS, bias=bias)
+    pre = torch.empty(T, F, device=cuda, dtype=torch.bfloat16)
+    c_gelu = k.gemm_nt(x, w, EPI_GELU, bias=bias, pre=pre)
+    gd = torch.empty(T, F, device=cuda, dtype=torch.bfloat16)
+    c_gelud = k.gemm_nt(x, w, EPI_GELUD, bias=bias, pre=gd)
+    torch.cuda.synchronize()
+    _same([(c_bias,), (pre,)], "GELU P vs BIAS C")
+    _same([(c_gelu,), (c_gelud,)], "GELUD C vs GELU C")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["fwd_bias", "fwd_gelud", "dgrad_none", "dgrad_dmul", "dgrad_resid"])
+def test_gemm_fp8_repeatable(cuda, name):
+    """The fp8 GEMMs (gemm_fp8.hip: e4m3 forward, e5m2-gradient dgrads) share the LDS-DMA / epilogue structure of
+    the bf16 kernels: repeated launches at the headline shapes must agree bit for bit."""
+    k = _native.kernels()
+    g = torch.Generator(device=cuda).manual_seed(29)
+    fwd = name.startswith("fwd")
+    n_out, k_in = {"fwd_bias": (3 * H, H), "fwd_gelud": (F, H), "dgrad_none": (H, F), "dgrad_dmul": (F, H),
+                   "dgrad_resid": (H, 3 * H)}[name]
+    A8 = (torch.randn(T, k_in, device=cuda, generator=g) * 2).to(torch.float8_e4m3fn if fwd else torch.float8_e5m2)
+    B8 = (torch.randn(n_out, k_in, device=cuda, generator=g) * 2).to(torch.float8_e4m3fn)
+    sa = torch.full((1,), 0.01, device=cuda)
+    sb = torch.full((1,), 0.02, device=cuda)
+    bias = torch.randn(n_out, device=cuda, generator=g) * 0.1
+    aux = _bf((T, n_out), torch.Generator(device=cuda).manual_seed(31), cuda)
+    outs = []
+    for _ in range(REPS):
+        if name == "fwd_bias":
+            outs.append((k.gemm_fp8(A8, B8, EPI_BIAS, bias, sa, sb),))
+        elif name == "fwd_gelud":
+            gd = torch.empty(T, n_out, device=cuda, dtype=torch.bfloat16)
+            act8 = torch.empty(T, n_out, device=cuda, dtype=torch.float8_e4m3fn)
+            state = torch.tensor([1.0, 1.0, 1.0, 0.01], device=cuda)
+            c = k.gemm_fp8(A8, B8, EPI_GELUD, bias, sa, sb, pre=gd, out8=act8, state=state, phase=0)
+            outs.append((c, gd, act8.view(torch.uint8)))
+        elif name == "dgrad_none":
+            outs.append((k.gemm_fp8(A8, B8, EPI_NONE, None, sa, sb),))
+        elif name == "dgrad_dmul":
+            part = torch.zeros(T // 256, n_out, device=cuda)
+            out8 = torch.empty(T, n_out, device=cuda, dtype=torch.float8_e5m2)
+            state = torch.tensor([1.0, 1.0, 1.0, 0.01], device=cuda)
+            c = k.gemm_fp8(A8, B8, EPI_DMUL, None, sa, sb, pre=aux, out8=out8, state=state, phase=0, part=part)
+            outs.append((c, part, out8.view(torch.uint8)))
+        else:
+            outs.append((k.gemm_fp8(A8, B8, EPI_RESID, None, sa, sb, resid=aux),))
+    torch.cuda.synchronize()
+    _same(outs, f"gemm_fp8 {name}")

@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """Run one NT GEMM shape repeatedly (for PMC collection): python tools/gemm_one.py T N K epi
-(HQ_GEMM_VARIANT=1 selects the v1 kernel)."""
+(optional 5th argument: kernel variant for gemm_set_variant, e.g. 1 = v1)."""
 import os
 import sys
 
@@ -11,7 +11,7 @@ from ml_recipe_distributed_pytorch_amd import _native  # noqa: E402
 
 T, N, K, epi = (int(x) for x in sys.argv[1:5])
 k = _native.kernels()
-k.gemm_set_variant(int(os.environ.get("HQ_GEMM_VARIANT", "0")))
+k.gemm_set_variant(int(sys.argv[5]) if len(sys.argv) > 5 else 0)
 dev = torch.device("cuda")
 A = (torch.rand(T, K, device=dev) * 2 - 1).bfloat16()
 B = (torch.rand(N, K, device=dev) * 2 - 1).bfloat16()
