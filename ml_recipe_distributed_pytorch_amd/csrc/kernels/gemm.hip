@@ -879,6 +879,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   static_assert(3 * QREG <= PANEL / 2 && 2 * QREG <= REGION && TAIL + 3 * QREG <= 160 * 1024, "LDS plan");
   constexpr bool kBiasE = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD || EPI == HQ_EPI_BDR;
   const bool ht_on = (stagger >> 16) & 1;   // kHalfTail
+  const bool quarter_on = (stagger >> 17) & 1;
   stagger &= 0xFF;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
 
@@ -1012,8 +1013,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
   // Phase offset for half of each XCD's workgroups (stagger × 8128 cycles): the tile seams of all CUs
   // otherwise coincide, and every epilogue's stores / aux loads hit HBM in one chip-wide burst that the
   // next K-tile's counted wait (vmcnt counts stores too) then stalls on.
-  if (stagger > 0 && ((bid >> 3) & 1))
-    for (int i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  // bit 17 of the flag word: four groups (offsets 0, 1, 2, 3 × stagger) instead of two (0, stagger)
+  const int sgroup = quarter_on ? ((bid >> 3) & 3) : ((bid >> 3) & 1);
+  for (int i = 0; i < stagger * sgroup; ++i) __builtin_amdgcn_s_sleep(127);
   __amdgpu_buffer_rsrc_t ca = rsrc_a(tile), cb = rsrc_b(tile);
   int p0 = 0;                   // LDS buffer of this tile's K-tile 0
   // prologue of the first tile: K-tile 0 (A0 B0 B1 A1) and K-tile 1's A0 B0 B1 (its A1 is staged in K-tile 0)
@@ -1071,7 +1073,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       // halves and the epilogue's E vm ops); K-tile t's A0 B0 B1 were retired by P23(t-1)'s wait
       // HQ_EPI_DIAG bit 3 (timing lab only, results WRONG): no vmcnt wait in K-tiles 1-7 of a following unit, i.e.
       // what the mainloop would cost if the previous epilogue's stores never held up the DMA waits
-      const bool relax = (HQ_EPI_DIAG & 8) && !first && t >= 1 && t < 8;
+      // bit 4: no vmcnt wait in ANY K-tile of a following unit (pure issue timing, results wrong)
+      const bool relax = ((HQ_EPI_DIAG & 8) && !first && t >= 1 && t < 8) || ((HQ_EPI_DIAG & 16) && !first);
       if (relax) {
       } else if (t == 0 && !first) {
         if (prev_half) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(6 + E / 2) : "memory");
@@ -1169,6 +1172,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       const u32x4_t v = {d.x, d.y, d.z, d.w};
 #if HQ_EPI_DIAG & 1
       asm volatile("" :: "v"(v));
+#elif HQ_EPI_DIAG & 32
+      // bit 5: every store goes to the tile's first 8 rows (L2-resident): issue cost without the HBM write traffic
+      __builtin_amdgcn_raw_buffer_store_b128(v, r, vo_lane & 0xFFFF, 0, 0);
 #else
       __builtin_amdgcn_raw_buffer_store_b128(v, r, vo_lane, so_of(rnd, it), 0);
 #endif
