@@ -842,6 +842,15 @@ typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 #ifndef HQ_EPI_DIAG
 #define HQ_EPI_DIAG 0
 #endif
+// Cache policy of the persistent kernel's epilogue stores (gfx950 CPol bits: 1 = sc0, 2 = nt, 16 = sc1).  NTS
+// kernels store with nt | sc1 — streamed past the caches: at K = 768 the output is a third of the kernel's work in
+// bytes and its default-policy write-back holds the next tiles' LDS-DMA operand loads up (the stores retire, in
+// vmcnt order, ahead of them); nt | sc1 made the K = 768 NONE / BIAS / GELU / GELUD GEMMs 6-11 % faster on one box
+// (profiles/r5_epi_diag/aux*.log), while the K = 2304 / 3072 shapes and the epilogues that load an operand (DMUL /
+// RESID) lost 0-3 %.  HQ_EPI_STORE_AUX (lab builds) forces the bits for every variant.
+#ifndef HQ_EPI_STORE_AUX
+#define HQ_EPI_STORE_AUX 0
+#endif
 template <int EPI>
 struct NT3Epi {
   static constexpr int kStores = (HQ_EPI_DIAG & 1) ? 0 : 16 * (1 + (EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD ? 1 : 0));
@@ -852,7 +861,7 @@ struct NT3Epi {
 // DYN: the per-XCD ticket schedule is compiled in (a launch with sched == nullptr runs the static one either
 // way).  The static-only build (DYN = false, the single-GPU default) has no ticket atomic, whose pending return
 // makes hipcc drain vmcnt(0) — the next tile's in-flight K-tile-0 DMA — at every tile's epilogue.
-template <int EPI, bool DYN>
+template <int EPI, bool DYN, bool NTS>
 __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
                                                                uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                                uint16_t* __restrict__ P, const uint16_t* __restrict__ R,
@@ -1176,7 +1185,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       // bit 5: every store goes to the tile's first 8 rows (L2-resident): issue cost without the HBM write traffic
       __builtin_amdgcn_raw_buffer_store_b128(v, r, vo_lane & 0xFFFF, 0, 0);
 #else
-      __builtin_amdgcn_raw_buffer_store_b128(v, r, vo_lane, so_of(rnd, it), 0);
+      __builtin_amdgcn_raw_buffer_store_b128(v, r, vo_lane, so_of(rnd, it), HQ_EPI_STORE_AUX | (NTS ? 18 : 0));
 #endif
       return v;
     };
@@ -1406,6 +1415,10 @@ int g_gemm_stagger = kHalfTail;
 
 // default static: uncontended the dynamic schedule costs ~0.9 % of the step (profiles/r2_sched); GradReducer
 // switches it on when an all-reduce overlaps the backward (world > 1); HQ_GEMM_SCHED overrides either way
+// epilogue store cache policy of the persistent kernel (see HQ_EPI_STORE_AUX): 1 = streamed stores for the
+// operand-free epilogues at K <= 768 (production), 0 = default policy everywhere, 2 = streamed at any K (A/B only)
+int g_store_policy = 1;
+
 int g_gemm_sched = [] {
   const char* e = getenv("HQ_GEMM_SCHED");
   return e ? atoi(e) : 0;
@@ -1523,18 +1536,26 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
       int dev = 0, n = 0;
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-      (void)hipFuncSetAttribute((const void*)gemm_nt3_kernel<EPI, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      (void)hipFuncSetAttribute((const void*)gemm_nt3_kernel<EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      for (const void* f : {(const void*)gemm_nt3_kernel<EPI, false, false>, (const void*)gemm_nt3_kernel<EPI, true, false>,
+                            (const void*)gemm_nt3_kernel<EPI, false, true>, (const void*)gemm_nt3_kernel<EPI, true, true>})
+        (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       return n > 0 ? n : 256;
     }();
     const int nwg = std::min(grid, ncu);
     unsigned* sched = (g_gemm_sched && grid > 2 * nwg) ? nt3_sched_slot(s) : nullptr;
-    if (sched)
-      hipLaunchKernelGGL((gemm_nt3_kernel<EPI, true>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, R, part,
-                         M, N, K, lda, ldb, ldc, g_gemm_stagger, sched, dr);
-    else
-      hipLaunchKernelGGL((gemm_nt3_kernel<EPI, false>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, R, part,
-                         M, N, K, lda, ldb, ldc, g_gemm_stagger, nullptr, dr);
+    // streamed (nt | sc1) epilogue stores: epilogues without an operand load, K <= 768 (g_store_policy 1), or at any K
+    // (2, A/B only), or never (0)
+    constexpr bool kNoAux = EPI == HQ_EPI_NONE || EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD;
+    const bool nts = kNoAux && (g_store_policy == 2 || (g_store_policy == 1 && K <= 768));
+    auto go = [&](auto kern, unsigned* sc) {
+      hipLaunchKernelGGL(kern, dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, R, part, M, N, K, lda, ldb, ldc,
+                         g_gemm_stagger, sc, dr);
+    };
+    if (sched) {
+      if (nts) go(gemm_nt3_kernel<EPI, true, true>, sched); else go(gemm_nt3_kernel<EPI, true, false>, sched);
+    } else {
+      if (nts) go(gemm_nt3_kernel<EPI, false, true>, nullptr); else go(gemm_nt3_kernel<EPI, false, false>, nullptr);
+    }
   } else if (bn == 256 && (g_gemm_variant == 0 || g_gemm_variant == 2 || g_gemm_variant == 3) && K >= 2 * BK && srd_ok) {
     // production v2: buffer_load…lds staging (+8-12 % over global_load_lds on the BERT shapes,
     // tools/gemm_lab); grouped 8-row-panel tile order only for wide N (+15 % at 8192², neutral at
@@ -1581,6 +1602,7 @@ void launch_epi(const uint16_t* A, const uint16_t* B, uint16_t* C, const float* 
 }  // namespace
 
 void hq_gemm_set_variant(int v) { g_gemm_variant = v; }
+void hq_gemm_set_store_policy(int v) { g_store_policy = v; }
 void hq_gemm_set_stagger(int v) { g_gemm_stagger = v; }
 int hq_gemm_get_sched() { return g_gemm_sched; }
 void hq_gemm_set_sched(int v) {

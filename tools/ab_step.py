@@ -43,6 +43,10 @@ def set_toggle(name, on):
         _native.kernels().gemm_set_variant(2 if on else 0)
     elif name == "halftail":   # on: v2 / v3 half-tile tail (+ v3 at K = 3072 when it applies); off: neither
         _native.kernels().gemm_set_stagger((1 << 16) if on else 0)
+    elif name == "store_nt":   # on: streamed epilogue stores at K <= 768 (production); off: default policy
+        _native.kernels().gemm_set_store_policy(1 if on else 0)
+    elif name == "store_nt_all":   # on: streamed epilogue stores at every K; off: only at K <= 768 (production)
+        _native.kernels().gemm_set_store_policy(2 if on else 1)
     elif name == "input_pipeline":
         pass
     else:
@@ -57,6 +61,8 @@ def main():
     ap.add_argument("--model", default="bert-base-uncased")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=8)
+    ap.add_argument("--only", choices=["off", "on"], default=None,
+                    help="run one arm only (for a kernel-trace profile of that arm)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg = get_config(a.model)
@@ -91,7 +97,7 @@ def main():
         return piped() if (a.toggle == "input_pipeline" and on) else (inputs, labels)
     res = {False: [], True: []}
     for r in range(a.rounds + 1):
-        for on in (False, True):
+        for on in ((False, True) if a.only is None else ((a.only == "on"),)):
             set_toggle(a.toggle, on)
             eng.step([batch_for(on)])
             torch.cuda.synchronize()
@@ -101,6 +107,9 @@ def main():
             torch.cuda.synchronize()
             if r > 0:  # round 0 = warm-up of both arms
                 res[on].append((time.perf_counter() - t0) / a.steps * 1e3)
+    if a.only is not None:
+        print(json.dumps({"toggle": a.toggle, "arm": a.only, "ms": round(statistics.median(res[a.only == "on"]), 3)}))
+        return
     out = {"toggle": a.toggle, "batch": a.batch, "off_ms": round(statistics.median(res[False]), 3),
            "on_ms": round(statistics.median(res[True]), 3), "off_all": [round(x, 2) for x in res[False]],
            "on_all": [round(x, 2) for x in res[True]]}

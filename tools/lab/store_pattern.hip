@@ -52,6 +52,32 @@ __global__ __launch_bounds__(512, 1) void store_tiles(uint16_t* __restrict__ C, 
   }
 }
 
+// retirement latency: each wave stores its 16 KB per tile (nt3 map), then waits vmcnt(0); the cycles that wait
+// takes (s_memtime) are summed per workgroup into lat[blockIdx.x] (wave 0's view)
+__global__ __launch_bounds__(512, 1) void store_tiles_lat(uint16_t* __restrict__ C, int M, int N,
+                                                          unsigned long long* __restrict__ lat) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int tiles_n = N / 256, ntiles = (M / 256) * tiles_n;
+  uint4 v = make_uint4(lane, wave, blockIdx.x, 0x3f803f80u);
+  unsigned long long tot = 0;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int m0 = (t / tiles_n) * 256, n0 = (t % tiles_n) * 256;
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int seg = lane & 7, rsub = lane >> 3;
+      const int row = m0 + wm * 128 + it * 8 + rsub;
+      const int col = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;
+      v.w += 1;
+      *reinterpret_cast<uint4*>(C + (size_t)row * N + col) = v;
+    }
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    tot += __builtin_amdgcn_s_memtime() - t0;
+  }
+  if (threadIdx.x == 0) lat[blockIdx.x] = tot;
+}
+
 int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 98304;
   const int N = argc > 2 ? atoi(argv[2]) : 3072;
@@ -86,6 +112,26 @@ int main(int argc, char** argv) {
       printf("M=%d N=%d grid=%d %-26s %8.1f us  %7.1f GB/s\n", M, N, grid, names[pat], ts[3] * 1e3,
              bytes / (ts[3] * 1e-3) / 1e9);
     }
+  {
+    unsigned long long* lat = nullptr;
+    CK(hipMalloc(&lat, grid * sizeof(unsigned long long)));
+    store_tiles_lat<<<grid, 512>>>(C, M, N, lat);
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a));
+    store_tiles_lat<<<grid, 512>>>(C, M, N, lat);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    std::vector<unsigned long long> h(grid);
+    CK(hipMemcpy(h.data(), lat, grid * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    const int tiles = (M / 256) * (N / 256);
+    double s = 0;
+    for (auto x : h) s += (double)x;
+    printf("M=%d N=%d grid=%d store+vmcnt(0) per tile: %8.1f us total, mean wait %.0f cycles per tile-epilogue\n", M, N,
+           grid, ms * 1e3, s / tiles);
+    CK(hipFree(lat));
+  }
   CK(hipFree(C));
   return 0;
 }
