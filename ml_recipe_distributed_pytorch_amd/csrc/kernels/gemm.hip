@@ -669,8 +669,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
   asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   bar();
 
-  // the wave row one barrier behind (every wave waits when the rows run unstaggered: the ABL & 4 ablation)
-  const bool row1 = (ABL & 4) != 0 || __builtin_amdgcn_readfirstlane(wm) != 0;
   // One K-tile = 2 phases of 32 MFMAs (stage / wait table and hazard argument: gemm_nt3_kernel below);
   // `G1` = the staggered group (one barrier behind).
   auto ktile = [&](int t) {
@@ -685,11 +683,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
     mma(0, 0, bf0);
     mma(0, 1, bf1);
     bar();
-    // P23 (1,1) (1,0): K-tile t+1's A0 B0 B1 for the other wave row; younger: this P01's A1 (wave row 1 only:
-    // row 0 reads one interval earlier, so its own P01 wait precedes row 1's reads)
-    if (row1) {
-      if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // P23 (1,1) (1,0): K-tile t+1's A0 B0 B1, read by BOTH wave rows in their next P01 (rows of a half come from
+    // all 8 waves); younger: this P01's A1.  Both rows wait here, two barriers ahead of the reads.
+    if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (!half) readA(t, 1);
     if (more2) { stA(0, t + 2); stB(0, t + 2); stB(1, t + 2); }
     bar();
@@ -1064,11 +1060,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     //   P01: reads B(nh 0), A(mh 0), B(nh 1); stages A1 of K-tile t+1   | MFMAs (0,0) (0,1)
     //   P23: reads A(mh 1); stages A0, B0, B1 of K-tile t+2              | MFMAs (1,1) (1,0)
     // Every half is staged by all 8 waves (16 rows each) and read 4-6 barrier intervals later; each wave's
-    // counted wait retires its own rows one interval before the OTHER wave row reads them.  A half is
+    // counted wait retires its own rows at least one barrier before ANY wave reads them.  A half is
     // re-staged only after both rows have read it (A1 of buffer b1 two intervals after its last read, the
     // others one).  Past this tile's end the stages come from the next tile's K-tile 0 (t+1 == nt,
     // t+2 == nt); its K-tile-1 A0 B0 B1 (t+2 == nt+1) go into buffer bl right after the last K-tile.
-    const bool row1 = __builtin_amdgcn_readfirstlane(wm) != 0;   // the wave row one barrier behind
     auto ktile = [&](int t) {
       const bool more1 = t + 1 < nt || !last;                    // P01 stages A1 of K-tile t+1
       const bool more2 = t + 2 < nt || (t + 2 == nt && !last);    // P23 stages K-tile t+2 (A0 B0 B1)
@@ -1102,11 +1097,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       mma(0, 0, bf0);
       mma(0, 1, bf1);
       bar();
-      // P23: K-tile t+1's A0 B0 B1 (read by the other wave row in its next P01) — younger: this P01's A1 and,
+      // P23: K-tile t+1's A0 B0 B1 (read by both wave rows in their next P01) — younger: this P01's A1 and,
       // at t = 0 of a following unit, the previous unit's epilogue (E vm ops, E / 2 after a half tile), which was
-      // issued after K-tile 1.  Only wave row 1 needs this wait: row 0 reads a K-tile one interval BEFORE row 1,
-      // so its own P01 wait (which retires everything older than its A1 stage) already precedes row 1's reads.
-      if (!row1 || relax) {
+      // issued after K-tile 1.  BOTH rows wait: each half's rows are staged by all 8 waves, so a wave of row 0
+      // reads rows of the other row-0 waves, whose P01 wait is in the same barrier interval as that read (round
+      // 4's schedule let row 0 skip this wait and relied on the DMA landing within the 6 intervals since issue).
+      if (relax) {
       } else if (t == 0 && !first) {
         if (prev_half) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 + E / 2) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 + E) : "memory");

@@ -212,7 +212,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
   asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   bar();
   // two 32-MFMA phases per K-tile; stage / wait table and hazard argument: gemm.hip, gemm_nt3_kernel
-  const bool row1 = __builtin_amdgcn_readfirstlane(wm) != 0;
   auto ktile = [&](int t) {
     const bool more1 = t + 1 < nt, more2 = t + 2 < nt;
     if (t == 0 || more1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -224,9 +223,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
     mma(0, 0, bf0);
     mma(0, 1, bf1);
     bar();
-    if (row1) {   // only the trailing wave row (gemm.hip, gemm_nt3_kernel)
-      if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // both wave rows (gemm.hip, gemm_nt3_kernel P23)
+    if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readA(t, 1);
     if (more2) { stA(0, t + 2); stB(0, t + 2); stB(1, t + 2); }
     bar();
@@ -442,7 +440,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* _
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     // two 32-MFMA phases per K-tile; stage / wait table and hazard argument: gemm.hip gemm_nt3_kernel
-    const bool row1 = __builtin_amdgcn_readfirstlane(wm) != 0;
     auto ktile = [&](int t) {
       const bool more1 = t + 1 < nt || !last;
       const bool more2 = t + 2 < nt || (t + 2 == nt && !last);
@@ -467,10 +464,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* _
       mma(0, 0, bf0);
       mma(0, 1, bf1);
       bar();
-      if (row1) {   // only the trailing wave row (gemm.hip, gemm_nt3_kernel)
-        if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      // both wave rows (gemm.hip, gemm_nt3_kernel P23); at t = 0 of a following unit the epilogue's E vm ops
+      // are younger too
+      if (t == 0 && !first) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 + E) : "memory");
+      else if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       readA(b0, 1);
       if (more2) { stA(a2, 0, k2, b0); stB(b2r, 0, k2, b0); stB(b2r, 1, k2, b0); }
       bar();

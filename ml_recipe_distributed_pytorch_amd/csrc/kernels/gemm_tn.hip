@@ -197,7 +197,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const uint16_t* __
   asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   bar();
 
-  const bool row1 = __builtin_amdgcn_readfirstlane(wm) != 0;   // the wave row one barrier behind
   // two phases of 32 MFMAs per K-tile (schedule, waits and hazard argument: gemm.hip, gemm_nt3_kernel):
   //   P01: reads B(0) A(0) B(1), stages A1 of t+1 | (0,0) (0,1);   P23: reads A(1), stages A0 B0 B1 of t+2 | (1,1) (1,0)
   auto ktile = [&](int t) {
@@ -212,11 +211,9 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const uint16_t* __
     mma(0, 0, bf0);
     mma(0, 1, bf1);
     bar();
-    // A0 B0 B1 of t+1 (read by the other wave row next): younger is this P01's A1 stage.  Wave row 0 reads one
-    // interval before row 1, so only row 1 needs this wait (row 0's own P01 wait precedes row 1's reads)
-    if (row1) {
-      if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // A0 B0 B1 of t+1 (read by both wave rows in their next P01): younger is this P01's A1 stage.  Both rows
+    // wait (gemm.hip, gemm_nt3_kernel P23: each half's rows come from all 8 waves)
+    if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readA(t, 1);
     if (more2) { stA(0, t + 2); stB(0, t + 2); stB(1, t + 2); }
     bar();
@@ -369,7 +366,6 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn8_kernel(const uint8_t* __
   };
 
   // prologue, schedule and waits: identical to gemm_tn_kernel (2 DMA instructions per wave per half)
-  const bool row1 = __builtin_amdgcn_readfirstlane(wm) != 0;
   stA(0, 0); stB(0, 0); stB(1, 0); stA(1, 0); stA(0, 1); stB(0, 1); stB(1, 1);
   asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   bar();
@@ -384,9 +380,8 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn8_kernel(const uint8_t* __
     mma(0, 0, bf0);
     mma(0, 1, bf1);
     bar();
-    if (row1) {   // only the trailing wave row (gemm.hip, gemm_nt3_kernel)
-      if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // both wave rows (gemm.hip, gemm_nt3_kernel P23)
+    if (more1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     readA(t, 1);
     if (more2) { stA(0, t + 2); stB(0, t + 2); stB(1, t + 2); }
     bar();
