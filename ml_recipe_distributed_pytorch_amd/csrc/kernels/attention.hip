@@ -233,7 +233,17 @@ __device__ __forceinline__ float dpp_f(float x, int ctrl_sel) {
   }
   return __int_as_float(r);
 }
+// lanes in the (compile-time) EXEC-shaped `mask` take a, the others b: one v_cndmask_b32 on an SGPR-pair constant.
+// Written as asm because hipcc rewrites the butterfly's `up ? v[i] : v[i + k]` (up = a lane bit) into a
+// lane-dependent array index and lowers every such read to a 16-way v_cmp / v_cndmask chain (profiled: the
+// MODE 2 dK/dV epilogue was 2,500 VALU + 750 s_nop per wave, +83 µs per layer at B = 256, L = 384)
+__device__ __forceinline__ float lane_sel(uint64_t mask, float a, float b) {
+  float r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(mask));
+  return r;
+}
 __device__ __forceinline__ float colsum16(const f32x16_t& a, float mul, bool valid, int lane) {
+  (void)lane;
   float v[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = valid ? a[r] * mul : 0.f;
@@ -246,12 +256,13 @@ __device__ __forceinline__ float colsum16(const f32x16_t& a, float mul, bool val
   // bits 3, 2, 1: keep the half selected by the lane bit, add the partner's copy of it
 #pragma unroll
   for (int lvl = 0; lvl < 3; ++lvl) {
-    const int k = 4 >> lvl, bit = 8 >> lvl;
-    const bool up = (lane & bit) != 0;
+    const int k = 4 >> lvl;
+    // lanes with bit (8 >> lvl) set: 0xFF00…, 0xF0F0…, 0xCCCC…
+    const uint64_t up = lvl == 0 ? 0xFF00FF00FF00FF00ull : lvl == 1 ? 0xF0F0F0F0F0F0F0F0ull : 0xCCCCCCCCCCCCCCCCull;
 #pragma unroll
     for (int i = 0; i < k; ++i) {
-      const float send = up ? v[i] : v[i + k];
-      const float keep = up ? v[i + k] : v[i];
+      const float send = lane_sel(up, v[i], v[i + k]);
+      const float keep = lane_sel(up, v[i + k], v[i]);
       v[i] = keep + dpp_f(send, lvl);
     }
   }
