@@ -80,13 +80,22 @@ void embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tenso
   }
   const int nb = hq_embed_bwd_partials((int)T, (int)seq_len);
   auto part = at::empty({nb, 4 * H}, gamma.options());
+  const int V = (int)ww.size(0);
+  const HqEmbScratchSizes zs = hq_embed_bwd_scratch((int)T, V, (int)seq_len);
+  auto pairs = at::empty({4, T}, ids.options().dtype(at::kInt));
+  auto sort_tmp = at::empty({(int64_t)std::max<size_t>(zs.sort_bytes, 1)}, ids.options().dtype(at::kByte));
+  auto carry = at::empty({(int64_t)zs.chunks * 2, H}, gamma.options());
+  auto ppart = at::empty({std::max<int64_t>(zs.pos_rows, 1), H}, gamma.options());
+  int32_t* pr = pairs.data_ptr<int32_t>();
+  const HqEmbScratch sc{pr, pr + T, pr + 2 * T, pr + 3 * T, sort_tmp.data_ptr(), zs.sort_bytes, ptr<float>(carry),
+                        ptr<float>(ppart)};
   float* t0 = ptr<float>(g_type);
   HqOuts o = outs4(ptr<float>(g_gamma), ptr<float>(g_beta), n_types <= 2 ? t0 : nullptr,
                    n_types == 2 ? t0 + H : nullptr);
   hq_embed_bwd(ptr<uint16_t>(dy), ptr<int64_t>(ids), ptr<int64_t>(pids), ptr<int64_t>(tids), ptr<uint16_t>(ww),
                ptr<uint16_t>(wp), ptr<uint16_t>(wt), ptr<float>(gamma), ptr<float>(mean), ptr<float>(rstd),
                ptr<float>(g_word), ptr<float>(g_pos), t0, ptr<float>(part), o, (int)T, (int)H, n_types, (int)pad_word,
-               (int)pad_pos, (float)p, u32(seed), u32(opid), accumulate, (int)ww.size(0), (int)wp.size(0), (int)seq_len, s);
+               (int)pad_pos, (float)p, u32(seed), u32(opid), accumulate, V, (int)wp.size(0), (int)seq_len, sc, s);
 }
 
 // ------------------------------------------------------------------ residual + dropout + LayerNorm

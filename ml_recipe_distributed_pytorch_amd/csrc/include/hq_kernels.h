@@ -34,11 +34,24 @@ void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const
 void hq_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww, const uint16_t* wp,
                   const uint16_t* wt, const float* gamma, const float* beta, uint16_t* y, float* mean, float* rstd, int T,
                   int H, float eps, float p, uint32_t seed, uint32_t opid, int V, int P, int NTY, hipStream_t s);
+// deterministic embedding backward scratch (norm.hip: id sort, word-run carries, position partials)
+struct HqEmbScratch {
+  int32_t *keys, *rows, *skeys, *srows;   // [T] each: (id, row) pairs and their id-sorted copies
+  void* sort_tmp;                          // hipcub radix-sort temp storage, sort_bytes
+  size_t sort_bytes;
+  float* carry;                            // [chunks][2][H]
+  float* ppart;                            // [pos_rows][H] (unused when pos_rows == 0)
+};
+struct HqEmbScratchSizes {
+  size_t sort_bytes;
+  int chunks, pos_rows;
+};
+HqEmbScratchSizes hq_embed_bwd_scratch(int T, int V, int L);
 void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww,
                   const uint16_t* wp, const uint16_t* wt, const float* gamma, const float* mean, const float* rstd,
                   float* g_word, float* g_pos, float* g_type, float* part, HqOuts outs, int T, int H, int n_types,
                   int pad_word, int pad_pos, float p, uint32_t seed, uint32_t opid, bool accumulate, int V, int P,
-                  int L, hipStream_t s);
+                  int L, const HqEmbScratch& sc, hipStream_t s);
 // partial-sum rows embed_bwd needs for T tokens laid out as [T / L][L] (L <= 0: one sequence)
 int hq_embed_bwd_partials(int T, int L);
 void hq_gelu_fwd(const uint16_t* pre, uint16_t* out, size_t n, hipStream_t s);

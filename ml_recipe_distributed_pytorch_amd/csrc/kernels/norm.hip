@@ -3,15 +3,17 @@
 //   ln_fwd   : z = dropout(a) + resid (rounded to bf16, as HF under autocast) ; y = LN(z)
 //   ln_bwd   : dz = LN_bwd(dy [+ dy2]) ; da = dropout_bwd(dz) ; per-block partial Σ(g·x̂), Σg, Σda
 //   embed_fwd: y = dropout(LN(word[id] + pos[pid] + type[tid]))
-//   embed_bwd: recompute x̂, LN_bwd, f32 atomics into the word grads (256-B contiguous per wave
-//              instruction via an LDS transpose), position grads summed per wave over the batch
-//              (position-major walk) then one atomic flush, type/γ/β grads through deterministic partials
+//   embed_bwd: recompute x̂, LN_bwd; word grads summed per id over the id-sorted rows (no atomics),
+//              position grads summed per wave over the batch (position-major walk) into partial rows,
+//              type/γ/β grads through deterministic partials
 //   gelu_fwd / gelu_bwd(+bias grad partials), bias_grad partials, colsum finalize
 //
 // Layout: one wave per row; lane owns 4 consecutive columns per 256-column chunk (8-byte bf16
 // vector access), NCH = ceil(H/256) chunks.  Column partial sums are reduced per block through
 // LDS and finished by hq_colsum (one 1024-thread block per 64 columns), so every gradient is
-// bitwise deterministic except the word/position embedding scatter (float atomics).
+// bitwise deterministic (position ids other than 0 … L-1 fall back to float atomics for the position rows).
+#include <hipcub/hipcub.hpp>
+
 #include "hq_common.h"
 #include "hq_kernels.h"
 
@@ -441,16 +443,28 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
   if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
 }
 
+// Deterministic embedding backward (no float atomics at the default position ids):
+//   1. sort: the token rows by word id (hipcub radix sort of (id, row) pairs — stable, so each id's rows stay
+//      in token order);
+//   2. embed_bwd_kernel (position-major): recompute x̂ and the LayerNorm backward per row; γ / β / type
+//      gradients as per-block partials, the position gradient summed per wave over its kEmbNB batch rows and
+//      stored as that wave's partial row [blockIdx.y][l] (folded by colsum in a fixed order);
+//   3. embed_word_kernel (id-major): the same per-row recompute over the SORTED rows, kEmbCH per wave, summing
+//      each id's run in registers; a run inside the chunk is stored straight into its gradient row, the
+//      pieces of a run that crosses chunk boundaries go to two carry rows per chunk;
+//   4. embed_carry_kernel: the chunk where a crossing run starts adds its pieces in chunk order.
+// Every sum has a fixed order, so the result is bitwise reproducible (the round-4 kernel scattered 75 M f32
+// atomics into the word gradients: 316 µs at T = 98304 and run-to-run different low bits).
+// Position ids other than l (RoBERTa's l + 2, user-supplied ids) fall back to f32 atomics for those rows.
+//
 // part layout per block: [gamma | beta | type0 | type1] × H
 //
 // Position-major traversal: wave w of block (x, y) owns sequence position l = x·4 + w and walks the
-// kEmbNB batch rows b = y·kEmbNB … (row = b·L + l).  With the default position ids (pid = l for every
-// b) the wave sums the position gradient in registers and flushes it with ONE set of atomics per wave
-// (a flush also runs whenever the pid changes, so arbitrary position ids stay exact) — the old
-// row-major walk issued 768 position atomics per token, all 256 tokens of a position contending on
-// the same 3 KB.  The next row's dy / embedding rows / statistics are loaded while the current row
-// is reduced (one dependent HBM round trip per row otherwise).
-constexpr int kEmbNB = 16;
+// kEmbNB batch rows b = y·kEmbNB … (row = b·L + l).  The next row's dy / embedding rows / statistics are
+// loaded while the current row is reduced (one dependent HBM round trip per row otherwise).
+constexpr int kEmbNB = 16;       // batch rows per wave in the position pass (<= 64, as kEmbCH)
+constexpr int kEmbCH = 16;       // sorted rows per wave in the word pass (<= 64: one row's metadata per lane)
+constexpr int kEmbMaxL = 4096;   // position partials [T / L / kEmbNB][L][H] only for real sequence layouts
 
 template <int NCH>
 struct EmbRow {
@@ -479,16 +493,100 @@ __device__ __forceinline__ void emb_load(EmbRow<NCH>& r, size_t row, const uint1
   }
 }
 
+// Row metadata of up to 64 rows, one row per lane (ids, position / type ids, LayerNorm statistics), loaded once
+// up front: the per-row loop then reads them with v_readlane and issues only the row-data loads — no dependent
+// index → row round trip inside the loop.
+struct EmbMeta {
+  int id, pid, tid;
+  float mu, rs;
+};
+__device__ __forceinline__ EmbMeta emb_meta_load(int64_t row, bool ok, const int64_t* __restrict__ ids,
+                                                 const int64_t* __restrict__ pids, const int64_t* __restrict__ tids,
+                                                 const float* __restrict__ mean, const float* __restrict__ rstd) {
+  EmbMeta m{0, 0, 0, 0.f, 0.f};
+  if (ok) { m.id = (int)ids[row]; m.pid = (int)pids[row]; m.tid = (int)tids[row]; m.mu = mean[row]; m.rs = rstd[row]; }
+  return m;
+}
+// row data of the row whose metadata lane k holds
+template <int NCH>
+__device__ __forceinline__ void emb_load_k(EmbRow<NCH>& r, const EmbMeta& m, int k, size_t row, const uint16_t* __restrict__ dy,
+                                           const uint16_t* __restrict__ ww, const uint16_t* __restrict__ wp,
+                                           const uint16_t* __restrict__ wt, int H, int lane) {
+  r.id = __builtin_amdgcn_readlane(m.id, k);
+  r.pid = __builtin_amdgcn_readlane(m.pid, k);
+  r.tid = __builtin_amdgcn_readlane(m.tid, k);
+  r.mu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m.mu), k));
+  r.rs = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m.rs), k));
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    if (col < H) {
+      r.w[c] = *reinterpret_cast<const uint2*>(ww + (size_t)r.id * H + col);
+      r.p[c] = *reinterpret_cast<const uint2*>(wp + (size_t)r.pid * H + col);
+      r.t[c] = *reinterpret_cast<const uint2*>(wt + (size_t)r.tid * H + col);
+      r.d[c] = *reinterpret_cast<const uint2*>(dy + row * H + col);
+    }
+  }
+}
+
+// One row's LayerNorm backward from the recomputed x̂: g = dropout-masked dy, x̂, and dx = ∂/∂(word+pos+type).
+template <int NCH>
+__device__ __forceinline__ void emb_row_grad(const EmbRow<NCH>& cur, size_t base, const float (&gam)[NCH][4],
+                                             uint32_t key, uint32_t thr, float kscale, int H, int lane,
+                                             float (&g)[NCH][4], float (&xh)[NCH][4], float (&dx)[NCH][4]) {
+  const float mu = cur.mu, rs = cur.rs;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    if (col < H) {
+      float f1[4], f2[4], f3[4], m[4] = {1.f, 1.f, 1.f, 1.f};
+      hq_unpack4(cur.w[c], f1);
+      hq_unpack4(cur.p[c], f2);
+      hq_unpack4(cur.t[c], f3);
+      hq_unpack4(cur.d[c], g[c]);
+      if (thr) hq_keep4((uint32_t)(base + col), key, thr, kscale, m);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        g[c][i] *= m[i];
+        xh[c][i] = (f1[i] + f2[i] + f3[i] - mu) * rs;
+        const float dxh = g[c][i] * gam[c][i];
+        s1 += dxh;
+        s2 += dxh * xh[c][i];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { g[c][i] = 0.f; xh[c][i] = 0.f; }
+    }
+  }
+  s1 = hq_wave_sum(s1) / H;
+  s2 = hq_wave_sum(s2) / H;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dx[c][i] = c * 256 + lane * 4 < H ? rs * (g[c][i] * gam[c][i] - s1 - xh[c][i] * s2) : 0.f;
+}
+
+template <int NCH>
+__device__ __forceinline__ void emb_gamma(const float* __restrict__ gamma, int H, int lane, float (&gam)[NCH][4]) {
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int col = c * 256 + lane * 4;
+    const float4 g = col < H ? *reinterpret_cast<const float4*>(gamma + col) : make_float4(0.f, 0.f, 0.f, 0.f);
+    gam[c][0] = g.x; gam[c][1] = g.y; gam[c][2] = g.z; gam[c][3] = g.w;
+  }
+}
+
 template <int NCH>
 __global__ __launch_bounds__(256) void embed_bwd_kernel(
     const uint16_t* __restrict__ dy, const int64_t* __restrict__ ids, const int64_t* __restrict__ pids,
     const int64_t* __restrict__ tids, const uint16_t* __restrict__ ww, const uint16_t* __restrict__ wp,
     const uint16_t* __restrict__ wt, const float* __restrict__ gamma, const float* __restrict__ mean,
-    const float* __restrict__ rstd, float* __restrict__ g_word, float* __restrict__ g_pos, float* __restrict__ g_type,
-    float* __restrict__ part, int T, int H, int n_types, int pad_word, int pad_pos, HqDropKey kd_, uint32_t thr,
-    float kscale, int V, int P, int B, int L) {
+    const float* __restrict__ rstd, float* __restrict__ g_pos, float* __restrict__ g_type, float* __restrict__ ppart,
+    float* __restrict__ part, int T, int H, int n_types, int pad_pos, HqDropKey kd_, uint32_t thr, float kscale, int V,
+    int P, int B, int L) {
   const uint32_t key = kd_.get();
-  extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][H] reduction scratch, reused as dx rows
+  extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][H] block-partial scratch
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   float acc[4][NCH][4];
 #pragma unroll
@@ -498,109 +596,248 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc[q][c][i] = 0.f;
   float gam[NCH][4], pacc[NCH][4];
+  emb_gamma<NCH>(gamma, H, lane, gam);
 #pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int col = c * 256 + lane * 4;
-    float4 g = col < H ? *reinterpret_cast<const float4*>(gamma + col) : make_float4(0.f, 0.f, 0.f, 0.f);
-    gam[c][0] = g.x; gam[c][1] = g.y; gam[c][2] = g.z; gam[c][3] = g.w;
+  for (int c = 0; c < NCH; ++c)
 #pragma unroll
     for (int i = 0; i < 4; ++i) pacc[c][i] = 0.f;
-  }
+  const int l = blockIdx.x * kWaves + wave;
+  // this wave's position-partial row (ppart = null: every position flush is atomic)
+  float* prow = (ppart != nullptr && l < L) ? ppart + ((size_t)blockIdx.y * L + l) * H : nullptr;
+  bool pstored = false;
   int pcur = -1;
   auto flush_pos = [&]() {
     if (pcur >= 0 && pcur != pad_pos) {
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         const int col = c * 256 + lane * 4;
-        if (col < H)
+        if (col < H) {
+          if (prow != nullptr && pcur == l) {   // the default ids: the wave's own partial row, plain stores
+            float4 v = make_float4(pacc[c][0], pacc[c][1], pacc[c][2], pacc[c][3]);
+            if (pstored) {
+              const float4 o = *reinterpret_cast<const float4*>(prow + col);
+              v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+            }
+            *reinterpret_cast<float4*>(prow + col) = v;
+          } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) atomicAdd(g_pos + (size_t)pcur * H + col + i, pacc[c][i]);
+            for (int i = 0; i < 4; ++i) atomicAdd(g_pos + (size_t)pcur * H + col + i, pacc[c][i]);
+          }
+        }
       }
+      if (prow != nullptr && pcur == l) pstored = true;
     }
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int i = 0; i < 4; ++i) pacc[c][i] = 0.f;
   };
-  float* myrow = lds + wave * H;
-  const int l = blockIdx.x * kWaves + wave;
-  const int b0 = blockIdx.y * kEmbNB, b1 = min(B, b0 + kEmbNB);
+  const int b0 = blockIdx.y * kEmbNB, b1 = l < L ? min(B, b0 + kEmbNB) : b0;
+  // rows two ahead in a ring of three (compile-time slots in the unrolled loop: a rotation by copies would wait
+  // for the newest loads at every copy)
+  const EmbMeta meta = emb_meta_load((int64_t)(b0 + lane) * L + l, lane < b1 - b0, ids, pids, tids, mean, rstd);
   EmbRow<NCH> cur, nxt;
-  if (l < L && b0 < b1) emb_load<NCH>(nxt, (size_t)b0 * L + l, dy, ids, pids, tids, ww, wp, wt, mean, rstd, H, lane);
-  for (int b = b0; l < L && b < b1; ++b) {
+  if (b0 < b1) emb_load_k<NCH>(nxt, meta, 0, (size_t)b0 * L + l, dy, ww, wp, wt, H, lane);
+#pragma unroll 1
+  for (int b = b0; b < b1; ++b) {
     const size_t row = (size_t)b * L + l;
     cur = nxt;
-    if (b + 1 < b1) emb_load<NCH>(nxt, row + L, dy, ids, pids, tids, ww, wp, wt, mean, rstd, H, lane);
-    const int64_t id = cur.id, pid = cur.pid, tid = cur.tid;
-    HQ_DASSERT(id >= 0 && id < V && pid >= 0 && pid < P && tid >= 0 && tid < n_types);
-    const size_t base = row * H;
-    const float mu = cur.mu, rs = cur.rs;
-    float g[NCH][4], xh[NCH][4];
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int col = c * 256 + lane * 4;
-      if (col < H) {
-        float f1[4], f2[4], f3[4], m[4] = {1.f, 1.f, 1.f, 1.f};
-        hq_unpack4(cur.w[c], f1);
-        hq_unpack4(cur.p[c], f2);
-        hq_unpack4(cur.t[c], f3);
-        hq_unpack4(cur.d[c], g[c]);
-        if (thr) hq_keep4((uint32_t)(base + col), key, thr, kscale, m);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          g[c][i] *= m[i];
-          xh[c][i] = (f1[i] + f2[i] + f3[i] - mu) * rs;
-          acc[0][c][i] += g[c][i] * xh[c][i];
-          acc[1][c][i] += g[c][i];
-          const float dxh = g[c][i] * gam[c][i];
-          s1 += dxh;
-          s2 += dxh * xh[c][i];
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { g[c][i] = 0.f; xh[c][i] = 0.f; }
-      }
-    }
-    s1 = hq_wave_sum(s1) / H;
-    s2 = hq_wave_sum(s2) / H;
+    if (b + 1 < b1) emb_load_k<NCH>(nxt, meta, b + 1 - b0, row + L, dy, ww, wp, wt, H, lane);
+    const int64_t pid = cur.pid, tid = cur.tid;
+    HQ_DASSERT(cur.id >= 0 && cur.id < V && pid >= 0 && pid < P && tid >= 0 && tid < n_types);
+    float g[NCH][4], xh[NCH][4], dx[NCH][4];
+    emb_row_grad<NCH>(cur, row * H, gam, key, thr, kscale, H, lane, g, xh, dx);
     if ((int)pid != pcur) {  // wave-uniform: the running position sum belongs to another position
       flush_pos();
       pcur = (int)pid;
     }
+    const bool t1 = (tid & 1) != 0;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int col = c * 256 + lane * 4;
       if (col < H) {
-        float dx[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          dx[i] = rs * (g[c][i] * gam[c][i] - s1 - xh[c][i] * s2);
-          pacc[c][i] += dx[i];
+          acc[0][c][i] += g[c][i] * xh[c][i];
+          acc[1][c][i] += g[c][i];
+          pacc[c][i] += dx[c][i];
         }
         if (n_types <= 2) {  // static indices only: acc[2 + (tid & 1)] put the whole array in scratch memory
-          const bool t1 = (tid & 1) != 0;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            acc[2][c][i] += t1 ? 0.f : dx[i];
-            acc[3][c][i] += t1 ? dx[i] : 0.f;
+            acc[2][c][i] += t1 ? 0.f : dx[c][i];
+            acc[3][c][i] += t1 ? dx[c][i] : 0.f;
           }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) atomicAdd(g_type + (size_t)tid * H + col + i, dx[c][i]);
         }
-        *reinterpret_cast<float4*>(myrow + col) = make_float4(dx[0], dx[1], dx[2], dx[3]);
       }
-    }
-    // wave-private LDS row, re-read lane-contiguous so each atomic wave-instruction is 256 B contiguous
-    // (LDS ops of one wave complete in issue order; the aliasing stores keep the compiler order)
-    const bool do_word = (int)id != pad_word;
-    for (int col = lane; col < H; col += 64) {
-      const float d = myrow[col];
-      if (do_word) atomicAdd(g_word + (size_t)id * H + col, d);
-      if (n_types > 2) atomicAdd(g_type + (size_t)tid * H + col, d);
     }
   }
   flush_pos();
+  if (prow != nullptr && !pstored) {   // no row at position l in this batch slice: a zero partial
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int col = c * 256 + lane * 4;
+      if (col < H) *reinterpret_cast<float4*>(prow + col) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
   __syncthreads();
   block_partials<NCH, 4>(acc, lds, part, H);
+}
+
+// (id, row) pairs for the sort: the int64 ids as int32 keys, rows 0 … T-1 as values
+__global__ __launch_bounds__(256) void embed_keys_kernel(const int64_t* __restrict__ ids, int32_t* __restrict__ keys,
+                                                         int32_t* __restrict__ rows, int T) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t < T) { keys[t] = (int32_t)ids[t]; rows[t] = t; }
+}
+
+// Word gradients over the id-sorted rows.  Wave c owns sorted positions [c·kEmbCH, …); the run of one id is
+// summed in token order.  Run kinds: inside the chunk → stored into g_word[id] (fresh: =, accumulate: +=);
+// the chunk's FIRST run when it continues from chunk c-1 → carry slot 0 of c; the chunk's LAST run when it
+// continues into chunk c+1 and began in this chunk → carry slot 1 of c (a run covering the whole chunk from
+// both sides is slot 0).  embed_carry_kernel completes the crossing runs.  Padding ids get no gradient.
+template <int NCH>
+__global__ __launch_bounds__(256) void embed_word_kernel(
+    const int32_t* __restrict__ skeys, const int32_t* __restrict__ srows, const uint16_t* __restrict__ dy,
+    const int64_t* __restrict__ ids, const int64_t* __restrict__ pids, const int64_t* __restrict__ tids,
+    const uint16_t* __restrict__ ww, const uint16_t* __restrict__ wp, const uint16_t* __restrict__ wt,
+    const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ rstd,
+    float* __restrict__ g_word, float* __restrict__ carry, int T, int H, int pad_word, int accumulate, HqDropKey kd_,
+    uint32_t thr, float kscale) {
+  const uint32_t key = kd_.get();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int c = blockIdx.x * kWaves + wave;
+  const int j0 = c * kEmbCH;
+  if (j0 >= T) return;
+  const int j1 = min(T, j0 + kEmbCH);
+  float gam[NCH][4], acc[NCH][4];
+  emb_gamma<NCH>(gamma, H, lane, gam);
+#pragma unroll
+  for (int q = 0; q < NCH; ++q)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[q][i] = 0.f;
+  const int first = __builtin_amdgcn_readfirstlane(skeys[j0]);
+  const bool head_cont = c > 0 && __builtin_amdgcn_readfirstlane(skeys[j0 - 1]) == first;
+  const int after = j1 < T ? __builtin_amdgcn_readfirstlane(skeys[j1]) : -1;
+  auto flush = [&](int id, int kind) {   // kind 0: carry slot 0, 1: carry slot 1, 2: the gradient row
+    if (id != pad_word) {
+      float* dst = kind == 2 ? g_word + (size_t)id * H : carry + ((size_t)c * 2 + kind) * H;
+#pragma unroll
+      for (int q = 0; q < NCH; ++q) {
+        const int col = q * 256 + lane * 4;
+        if (col < H) {
+          float4 v = make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]);
+          if (kind == 2 && accumulate) {
+            const float4 o = *reinterpret_cast<const float4*>(dst + col);
+            v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+          }
+          *reinterpret_cast<float4*>(dst + col) = v;
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NCH; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[q][i] = 0.f;
+  };
+  int seg = first;
+  bool seg_first = true;
+  // the chunk's sorted rows and their metadata, one per lane (kEmbCH <= 64)
+  const int myrow = lane < j1 - j0 ? srows[j0 + lane] : 0;
+  const EmbMeta meta = emb_meta_load(myrow, lane < j1 - j0, ids, pids, tids, mean, rstd);
+  EmbRow<NCH> cur, nxt;
+  emb_load_k<NCH>(nxt, meta, 0, (size_t)__builtin_amdgcn_readlane(myrow, 0), dy, ww, wp, wt, H, lane);
+#pragma unroll 1
+  for (int j = j0; j < j1; ++j) {
+    const size_t row = (size_t)__builtin_amdgcn_readlane(myrow, j - j0);
+    cur = nxt;
+    if (j + 1 < j1)
+      emb_load_k<NCH>(nxt, meta, j + 1 - j0, (size_t)__builtin_amdgcn_readlane(myrow, j + 1 - j0), dy, ww, wp, wt, H, lane);
+    const int id = (int)cur.id;
+    if (id != seg) {
+      flush(seg, seg_first && head_cont ? 0 : 2);
+      seg = id;
+      seg_first = false;
+    }
+    float g[NCH][4], xh[NCH][4], dx[NCH][4];
+    emb_row_grad<NCH>(cur, row * H, gam, key, thr, kscale, H, lane, g, xh, dx);
+#pragma unroll
+    for (int q = 0; q < NCH; ++q)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[q][i] += dx[q][i];
+  }
+  const bool from_prev = seg_first && head_cont;
+  flush(seg, from_prev ? 0 : (after == seg ? 1 : 2));
+}
+
+// Runs that cross chunk boundaries: the chunk holding a run's start piece (carry slot 1) adds the following
+// chunks' slot-0 pieces in chunk order and stores the gradient row.
+template <int NCH>
+__global__ __launch_bounds__(256) void embed_carry_kernel(const int32_t* __restrict__ skeys, const float* __restrict__ carry,
+                                                          float* __restrict__ g_word, int T, int H, int pad_word,
+                                                          int accumulate) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int c = blockIdx.x * kWaves + wave;
+  const int j0 = c * kEmbCH;
+  if (j0 >= T) return;
+  const int j1 = min(T, j0 + kEmbCH);
+  const int last = __builtin_amdgcn_readfirstlane(skeys[j1 - 1]);
+  if (j1 >= T || skeys[j1] != last || last == pad_word) return;                  // the last run ends here
+  if (skeys[j0] == last && c > 0 && skeys[j0 - 1] == last) return;               // ... or began before
+  // end of the run: the first sorted position past j1 whose key differs, by a 64-ary search over the sorted keys
+  int lo = j1, hi = T;   // skeys[lo] == last; the end lies in (lo, hi]
+  while (hi - lo > 1) {
+    const int step = (hi - lo + 63) / 64;
+    const int q = lo + lane * step;
+    const bool in = q < hi && skeys[q] == last;
+    const uint64_t m = __ballot(in);   // a prefix of the lanes (sorted keys)
+    const int k = 63 - __builtin_clzll(m);
+    lo = lo + k * step;
+    hi = min(hi, lo + step);
+  }
+  const int ce = (hi - 1) / kEmbCH;   // the last chunk holding rows of the run: pieces of chunks c+1 … ce
+  float acc[NCH][4];
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    const int col = q * 256 + lane * 4;
+    const float4 v = col < H ? *reinterpret_cast<const float4*>(carry + ((size_t)c * 2 + 1) * H + col)
+                             : make_float4(0.f, 0.f, 0.f, 0.f);
+    acc[q][0] = v.x; acc[q][1] = v.y; acc[q][2] = v.z; acc[q][3] = v.w;
+  }
+  for (int cc = c + 1; cc <= ce; cc += 8) {   // 8 pieces in flight, added in chunk order
+    float4 v[8][NCH];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int q = 0; q < NCH; ++q) {
+        const int col = q * 256 + lane * 4;
+        v[u][q] = (cc + u <= ce && col < H) ? *reinterpret_cast<const float4*>(carry + ((size_t)(cc + u) * 2) * H + col)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (cc + u <= ce)
+#pragma unroll
+        for (int q = 0; q < NCH; ++q) {
+          acc[q][0] += v[u][q].x; acc[q][1] += v[u][q].y; acc[q][2] += v[u][q].z; acc[q][3] += v[u][q].w;
+        }
+  }
+  float* dst = g_word + (size_t)last * H;
+#pragma unroll
+  for (int q = 0; q < NCH; ++q) {
+    const int col = q * 256 + lane * 4;
+    if (col < H) {
+      float4 v = make_float4(acc[q][0], acc[q][1], acc[q][2], acc[q][3]);
+      if (accumulate) {
+        const float4 o = *reinterpret_cast<const float4*>(dst + col);
+        v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+      }
+      *reinterpret_cast<float4*>(dst + col) = v;
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void gelu_fwd_kernel(const uint16_t* __restrict__ pre, uint16_t* __restrict__ out, size_t n8) {
@@ -827,11 +1064,28 @@ void hq_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, 
   });
 }
 
+static void emb_sort_check(hipError_t e) {
+  if (e != hipSuccess) { fprintf(stderr, "hq_embed_bwd: id sort failed: %s\n", hipGetErrorString(e)); abort(); }
+}
+static int emb_sort_bits(int V) { return V > 1 ? 32 - __builtin_clz((unsigned)(V - 1)) : 1; }
+
+HqEmbScratchSizes hq_embed_bwd_scratch(int T, int V, int L) {
+  HqEmbScratchSizes z{};
+  size_t bytes = 0;
+  emb_sort_check(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                                    (const int32_t*)nullptr, (int32_t*)nullptr, T, 0, emb_sort_bits(V)));
+  z.sort_bytes = bytes;
+  z.chunks = (T + kEmbCH - 1) / kEmbCH;
+  if (L <= 0 || T % L) L = T;
+  z.pos_rows = L <= kEmbMaxL ? ((T / L + kEmbNB - 1) / kEmbNB) * L : 0;
+  return z;
+}
+
 void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww,
                   const uint16_t* wp, const uint16_t* wt, const float* gamma, const float* mean, const float* rstd,
                   float* g_word, float* g_pos, float* g_type, float* part, HqOuts outs, int T, int H,
                   int n_types, int pad_word, int pad_pos, float p, uint32_t seed, uint32_t opid, bool accumulate,
-                  int V, int P, int L, hipStream_t s) {
+                  int V, int P, int L, const HqEmbScratch& sc, hipStream_t s) {
   const uint32_t thr = p > 0.f ? hq_threshold(p) : 0u;
   const HqDropKey key = hq_drop_key(seed, opid);
   const float ks = hq_keep_scale(thr);
@@ -839,13 +1093,28 @@ void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, c
   const int B = T / L;
   const dim3 grid((L + kWaves - 1) / kWaves, (B + kEmbNB - 1) / kEmbNB);
   const int nb = hq_embed_bwd_partials(T, L);
+  const HqEmbScratchSizes z = hq_embed_bwd_scratch(T, V, L);
+  float* ppart = z.pos_rows > 0 ? sc.ppart : nullptr;
+  // (id, row) sort: stable, so every id's rows stay in token order
+  hipLaunchKernelGGL(embed_keys_kernel, dim3((T + 255) / 256), dim3(256), 0, s, ids, sc.keys, sc.rows, T);
+  size_t bytes = sc.sort_bytes;
+  emb_sort_check(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp, bytes, sc.keys, sc.skeys, sc.rows, sc.srows, T, 0,
+                                                    emb_sort_bits(V), s));
+  const int nwb = (z.chunks + kWaves - 1) / kWaves;
   dispatch_nch(H, [&](auto nch) {
-    hipLaunchKernelGGL(embed_bwd_kernel<decltype(nch)::value>, grid, dim3(256), 4 * H * sizeof(float), s, dy, ids,
-                       pids, tids, ww, wp, wt, gamma, mean, rstd, g_word, g_pos, g_type, part, T, H, n_types, pad_word,
-                       pad_pos, key, thr, ks, V, P, B, L);
+    constexpr int C = decltype(nch)::value;
+    hipLaunchKernelGGL(embed_bwd_kernel<C>, grid, dim3(256), 4 * H * sizeof(float), s, dy, ids, pids, tids, ww, wp, wt,
+                       gamma, mean, rstd, g_pos, g_type, ppart, part, T, H, n_types, pad_pos, key, thr, ks, V, P, B, L);
+    hipLaunchKernelGGL(embed_word_kernel<C>, dim3(nwb), dim3(256), 0, s, sc.skeys, sc.srows, dy, ids, pids, tids, ww,
+                       wp, wt, gamma, mean, rstd, g_word, sc.carry, T, H, pad_word, accumulate ? 1 : 0, key, thr, ks);
+    hipLaunchKernelGGL(embed_carry_kernel<C>, dim3(nwb), dim3(256), 0, s, sc.skeys, sc.carry, g_word, T, H, pad_word,
+                       accumulate ? 1 : 0);
   });
   // outs: gamma, beta, type0, type1 (type rows only when n_types <= 2)
   colsum(part, nb, 4 * H, outs, H, accumulate, s);
+  // position partials [B / kEmbNB][L][H] -> rows 0 … L-1 of g_pos, on top of its zeroed (or accumulated) rows and
+  // the atomic flushes of non-default position ids
+  if (ppart) colsum(ppart, (B + kEmbNB - 1) / kEmbNB, L * H, HqOuts{{g_pos, nullptr, nullptr, nullptr}}, L * H, true, s);
 }
 
 void hq_gelu_fwd(const uint16_t* pre, uint16_t* out, size_t n, hipStream_t s) {

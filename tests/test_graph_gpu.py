@@ -1,6 +1,6 @@
 """HIP-graph replay of the training step (TrainEngine(graph=True)) against the eager step: same batches,
 same dropout seeds (host-drawn, written to the model's device seed word before each replay), so losses and
-weights must agree (bitwise except the float-atomic embedding-gradient scatter).  Covered: one micro-batch
+weights must agree bit for bit.  Covered: one micro-batch
 per step; gradient accumulation (first / middle / last micro-batch graphs); the native RCCL reducer's bucket
 all-reduces captured inside the boundary graph (forced 1-rank communicator); and the reference-heads path,
 which must stay eager (its classifier dropout key is drawn on the host)."""
@@ -52,14 +52,12 @@ def _run(cuda, graph, steps=5, B=2, L=512, split=1, reducer=False, lengths=None,
 
 
 def _same(model, le, me, lg, mg):
+    """Every kernel of the step is deterministic (the embedding backward sums each word's rows in a fixed order
+    since round 5): graph replay and eager must agree bit for bit."""
     for a, b in zip(le, lg):
-        assert a == pytest.approx(b, rel=1e-5, abs=1e-6)
-    atomic = torch.zeros_like(me, dtype=torch.bool)
-    for e in model.store.entries:
-        if "word_embeddings" in e.key or "position_embeddings" in e.key:
-            atomic[e.offset:e.offset + e.numel] = True
-    assert torch.equal(mg[~atomic], me[~atomic]) or torch.allclose(mg, me, rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(mg[atomic], me[atomic], rtol=1e-4, atol=1e-6)
+        assert a == b, (a, b)
+    diff = int((mg != me).sum())
+    assert diff == 0, f"{diff} of {me.numel()} master weights differ between graph replay and eager"
 
 
 def test_graph_replay_matches_eager(cuda):

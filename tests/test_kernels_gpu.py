@@ -163,6 +163,45 @@ def test_embedding(cuda, H, ntypes, p, layout):
     assert out[0][0].abs().max().item() == 0.0, "padding row must get no gradient"
 
 
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_embedding_bwd_sorted_runs(cuda, accumulate):
+    """The id-sorted word-gradient pass: runs of one id that stay inside a 16-row chunk, end exactly on a chunk
+    boundary, or cross many chunks (id 5: 100 rows -> start piece, middle pieces, end piece), the padding id
+    (no gradient) and single rows, in both the fresh and the accumulating mode, vs the fp32 oracle."""
+    k = _native.kernels()
+    torch.manual_seed(4)
+    V, P, B, L, H = 300, 64, 8, 64, 768
+    T = B * L
+    ww, wp, wt = _bf(torch.randn(V, H) * 0.05), _bf(torch.randn(P, H) * 0.05), _bf(torch.randn(2, H) * 0.05)
+    gamma = torch.randn(H) * 0.3 + 1
+    ids = torch.randint(8, V, (T,))
+    perm = torch.randperm(T)
+    ids[perm[:100]] = 5      # a long run
+    ids[perm[100:116]] = 7   # exactly one chunk's worth
+    ids[perm[116:156]] = 0   # padding
+    ids[perm[156:173]] = 3   # 17 rows
+    pids = torch.arange(L).repeat(B)
+    tids = torch.randint(0, 2, (T,))
+    dev = lambda t: t.to(cuda)  # noqa: E731
+    _, m, rs = k.embed_fwd(dev(ids), dev(pids), dev(tids), dev(ww), dev(wp), dev(wt), dev(gamma), dev(torch.zeros(H)),
+                           1e-12, 0.1, 7, 0)
+    dy = _bf(torch.randn(T, H))
+    init = [torch.randn(V, H) if accumulate else torch.zeros(V, H), torch.randn(P, H) if accumulate else torch.zeros(P, H),
+            torch.zeros(2, H), torch.zeros(H), torch.zeros(H)]
+    out = [dev(t.clone()) for t in init]
+    refs = [t.clone() for t in init]
+    k.embed_bwd(dev(dy), dev(ids), dev(pids), dev(tids), dev(ww), dev(wp), dev(wt), dev(gamma), m, rs, 0.1, 7, 0, *out,
+                accumulate, 0, -1, L)
+    ref.embed_bwd(dy, ids, pids, tids, ww, wp, wt, gamma, m.cpu(), rs.cpu(), 0.1, 7, 0, *refs, accumulate, 0, -1)
+    for a, b, n in zip(out, refs, ["word", "pos", "type", "gamma", "beta"]):
+        _close(a, b, 5e-2, 2e-2, n)
+    assert torch.equal(out[0][0].cpu(), init[0][0]), "padding row must get no gradient"
+    # rows of ids that never occur keep their initial value exactly
+    absent = torch.ones(V, dtype=torch.bool)
+    absent[ids.unique()] = False
+    assert torch.equal(out[0][absent.to(cuda)].cpu(), init[0][absent])
+
+
 def test_gelu_and_bias_grad(cuda):
     k = _native.kernels()
     torch.manual_seed(2)

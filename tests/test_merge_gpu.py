@@ -103,11 +103,6 @@ def test_merged_graph_replay_matches_eager_merged(cuda):
     eg.release_graph()
     assert replays >= 1 and keys == 2, (replays, keys)
     for a, b in zip(le, lg):
-        assert a == pytest.approx(b, rel=1e-5, abs=1e-6)
+        assert a == b, (a, b)
     me, mg = me_model.store.master, mg_model.store.master
-    atomic = torch.zeros_like(me, dtype=torch.bool)
-    for e in me_model.store.entries:
-        if "word_embeddings" in e.key or "position_embeddings" in e.key:
-            atomic[e.offset:e.offset + e.numel] = True
-    assert torch.equal(mg[~atomic], me[~atomic]) or torch.allclose(mg, me, rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(mg[atomic], me[atomic], rtol=1e-4, atol=1e-6)
+    assert int((mg != me).sum()) == 0   # every kernel deterministic: graph replay == eager bit for bit

@@ -166,3 +166,29 @@ def test_gemm_fp8_repeatable(cuda, name):
             outs.append((k.gemm_fp8(A8, B8, EPI_RESID, None, sa, sb, resid=aux),))
     torch.cuda.synchronize()
     _same(outs, f"gemm_fp8 {name}")
+
+
+@pytest.mark.gpu
+def test_embedding_bwd_repeatable(cuda):
+    """The embedding backward sorts rows by id and sums each id's rows in a fixed order (no float atomics at the
+    default position ids): word / position / type / γ / β gradients bitwise equal across launches at the headline
+    shape (V = 30522, 10 % padding)."""
+    k = _native.kernels()
+    B, L, V = 256, 384, 30522
+    g = torch.Generator(device=cuda).manual_seed(37)
+    ids = torch.randint(1, V, (B * L,), device=cuda, generator=g)
+    ids[torch.rand(B * L, device=cuda, generator=g) < 0.1] = 0
+    pids = torch.arange(L, device=cuda).repeat(B)
+    tids = torch.randint(0, 2, (B * L,), device=cuda, generator=g)
+    ww, wp, wt = _bf((V, H), g, cuda, 0.05), _bf((512, H), g, cuda, 0.05), _bf((2, H), g, cuda, 0.05)
+    gamma, beta = torch.ones(H, device=cuda), torch.zeros(H, device=cuda)
+    _, m, rs = k.embed_fwd(ids, pids, tids, ww, wp, wt, gamma, beta, 1e-12, 0.1, 41, 0)
+    dy = _bf((B * L, H), g, cuda)
+    outs = []
+    for _ in range(REPS):
+        o = [torch.empty(V, H, device=cuda), torch.empty(512, H, device=cuda), torch.empty(2, H, device=cuda),
+             torch.empty(H, device=cuda), torch.empty(H, device=cuda)]
+        k.embed_bwd(dy, ids, pids, tids, ww, wp, wt, gamma, m, rs, 0.1, 41, 0, *o, False, 0, -1, L)
+        outs.append(tuple(o))
+    torch.cuda.synchronize()
+    _same(outs, "embed_bwd")
