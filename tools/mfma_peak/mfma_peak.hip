@@ -31,6 +31,27 @@ __global__ __launch_bounds__(256) void peak(float* out, int iters) {
     const f32x4 t = ((c0 + c1) + (c2 + c3)) + ((c4 + c5) + (c6 + c7));
     const float s = t[0] + t[1] + t[2] + t[3];
     if (s == 1.2345f) out[threadIdx.x] = s;
+  } else if constexpr (SHAPE == 17) {
+    // 16x16x32 through inline asm: eight independent accumulators hipcc cannot rotate (the builtin form above
+    // compiles to accvgpr moves between the MFMAs)
+    f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, c2 = c0, c3 = c0, c4 = c0, c5 = c0, c6 = c0, c7 = c0;
+    for (int it = 0; it < iters; ++it) {
+      asm volatile(
+          "v_mfma_f32_16x16x32_bf16 %0, %8, %9, %0\n\t"
+          "v_mfma_f32_16x16x32_bf16 %1, %8, %9, %1\n\t"
+          "v_mfma_f32_16x16x32_bf16 %2, %8, %9, %2\n\t"
+          "v_mfma_f32_16x16x32_bf16 %3, %8, %9, %3\n\t"
+          "v_mfma_f32_16x16x32_bf16 %4, %8, %9, %4\n\t"
+          "v_mfma_f32_16x16x32_bf16 %5, %8, %9, %5\n\t"
+          "v_mfma_f32_16x16x32_bf16 %6, %8, %9, %6\n\t"
+          "v_mfma_f32_16x16x32_bf16 %7, %8, %9, %7"
+          : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4), "+v"(c5), "+v"(c6), "+v"(c7)
+          : "v"(a), "v"(b));
+    }
+    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");
+    const f32x4 t = ((c0 + c1) + (c2 + c3)) + ((c4 + c5) + (c6 + c7));
+    const float s = t[0] + t[1] + t[2] + t[3];
+    if (s == 1.2345f) out[threadIdx.x] = s;
   } else {
     f32x16 c[4];
     for (int j = 0; j < 4; ++j)
@@ -64,14 +85,15 @@ void run(int waves_per_simd) {
   (void)hipEventSynchronize(e1);
   float ms = 0.f;
   (void)hipEventElapsedTime(&ms, e0, e1);
-  const double per = SHAPE == 16 ? 16.0 * 16 * 32 * 2 * 8 : 32.0 * 32 * 16 * 2 * 4;   // flop per wave-iteration
+  const double per = SHAPE != 32 ? 16.0 * 16 * 32 * 2 * 8 : 32.0 * 32 * 16 * 2 * 4;   // flop per wave-iteration
   const double flop = per * iters * blocks * 4;
-  printf("mfma %dx%d  waves/SIMD %d  %.3f ms  %.0f TFLOP/s\n", SHAPE, SHAPE, waves_per_simd, ms, flop / ms / 1e9);
+  printf("mfma %s  waves/SIMD %d  %.3f ms  %.0f TFLOP/s\n", SHAPE == 16 ? "16x16x32" : SHAPE == 17 ? "16x16x32 asm" : "32x32x16", waves_per_simd, ms, flop / ms / 1e9);
   (void)hipFree(out);
 }
 
 int main() {
   for (int w : {1, 2, 4}) run<16>(w);
+  for (int w : {1, 2, 4}) run<17>(w);
   for (int w : {1, 2, 4}) run<32>(w);
   return 0;
 }
