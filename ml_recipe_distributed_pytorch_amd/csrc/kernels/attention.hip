@@ -956,8 +956,9 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
     st.bits = 0;
     if constexpr (DROP) st.bits = mbits[(((size_t)bh * n32 + t) * n32 + min(ks_idx, n32 - 1)) * 64 + lane];
   };
+  auto slot_of = [&](int t) { return (t & 1) * SLOT; };
   auto commit = [&](int t, const Stage& st) {
-    char* slot = reinterpret_cast<char*>(smem) + (t & 1) * SLOT;
+    char* slot = reinterpret_cast<char*>(smem) + slot_of(t);
     uint16_t* sq = reinterpret_cast<uint16_t*>(slot);
     uint16_t* so = sq + 32 * D;
     float f[8];
@@ -976,23 +977,6 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
     }
     if constexpr (DROP) reinterpret_cast<uint16_t*>(slot + 2 * RTILE + 640)[wave * 64 + lane] = st.bits;
   };
-  // Tile t lives in register set st[t % 3] (compile-time index in the unrolled NT > 0 loop: a rotation by
-  // copies would make hipcc wait for the NEWER tile's loads before each copy); the rolled NT = 0 loop
-  // rotates by copies (one tile less lookahead).
-  Stage st[3];
-  issue(0, st[0]);
-  if (n32 > 1) issue(1, st[1]);
-  if (n32 > 2) issue(2, st[2]);
-  commit(0, st[0]);
-  __syncthreads();
-  if constexpr (NT > 0) {
-    if (n32 > 3) issue(3, st[0]);
-  } else {
-    st[0] = st[1];
-    st[1] = st[2];
-    if (n32 > 3) issue(3, st[2]);
-  }
-
   LdsOffsets lo_;
   lo_.init(lane);
   const f32x16_t zero16 = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -1002,82 +986,130 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
   const int r_f = kbit((krel & 3) + 4 * (krel >> 3));   // bit position in the forward's keep word
   const float ksc = DROP ? kscale : 1.f;
   const f2_t ksc2 = {ksc, ksc};
-  constexpr int UNR = NT > 0 ? NT : 1;
-#pragma unroll UNR
-  for (int t = 0; t < n32; ++t) {
-    const char* slot = reinterpret_cast<const char*>(smem) + (t & 1) * SLOT;
+  // S = Q'·Kᵀ (+ bias_k − lse_q through the A'/B' words) and dP = dO·Vᵀ of tile t.  All eight operand reads are
+  // issued before the first MFMA (sched_barrier): left to itself hipcc reads each operand just before its
+  // MFMA and waits lgkmcnt(0) there, exposing the LDS latency once per MFMA.
+  auto scores = [&](int t, f32x16_t& s_acc, f32x16_t& p_acc) {
+    const char* slot = reinterpret_cast<const char*>(smem) + slot_of(t);
     const uint16_t* tq = reinterpret_cast<const uint16_t*>(slot);
     const uint16_t* to = tq + 32 * D;
-    if (active) {
-      const uint4 aw = reinterpret_cast<const uint4*>(slot + 2 * RTILE)[hh ? 0 : krel];
-      const bf16x8_t qa = hh ? bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0} : __builtin_bit_cast(bf16x8_t, u32x4{aw.x, aw.y, aw.z, aw.w});
-      f32x16_t s_acc = mfma32(row8(tq, 0, lo_, 0), kf[0], zero16);
+    bf16x8_t fq[4], fo[4];
 #pragma unroll
-      for (int s = 1; s < 4; ++s) s_acc = mfma32(row8(tq, 0, lo_, s), kf[s], s_acc);
-      s_acc = mfma32(qa, kaug, s_acc);                   // + bias_k − lse_q
-      f32x16_t p_acc = mfma32(row8(to, 0, lo_, 0), vf[0], zero16);
+    for (int s = 0; s < 4; ++s) {
+      fq[s] = row8(tq, 0, lo_, s);
+      fo[s] = row8(to, 0, lo_, s);
+    }
+    const uint4 aw = reinterpret_cast<const uint4*>(slot + 2 * RTILE)[hh ? 0 : krel];
+    __builtin_amdgcn_sched_barrier(0);
+    const bf16x8_t qa = hh ? bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0} : __builtin_bit_cast(bf16x8_t, u32x4{aw.x, aw.y, aw.z, aw.w});
+    s_acc = mfma32(fq[0], kf[0], zero16);
+    p_acc = mfma32(fo[0], vf[0], zero16);
 #pragma unroll
-      for (int s = 1; s < 4; ++s) p_acc = mfma32(row8(to, 0, lo_, s), vf[s], p_acc);
-      // mask: the forward word of fwd-lane l' = q + 32·hh' holds bit r' for key acc_row(r', hh'); this lane
-      // (key krel) needs, for query rows acc_row(r, hh) = 8g + 4hh + i, bit r_f of the words of fwd-lanes
-      // 8g + 4hh + i + 32·hh_f: four consecutive words per g, one 8-byte LDS read per g
-      const uint16_t* wsrc = reinterpret_cast<const uint16_t*>(slot + 2 * RTILE + 640) + wave * 64 + 4 * hh + 32 * hh_f;
-      const float* sdl = reinterpret_cast<const float*>(slot + 2 * RTILE + 512);
+    for (int s = 1; s < 4; ++s) {
+      s_acc = mfma32(fq[s], kf[s], s_acc);
+      p_acc = mfma32(fo[s], vf[s], p_acc);
+    }
+    s_acc = mfma32(qa, kaug, s_acc);                   // + bias_k − lse_q
+  };
+  // P, dS of tile t from its accumulators, then dVᵀ += dOᵀ·(P∘mask), dKᵀ += Q'ᵀ·dS
+  auto grads = [&](int t, const f32x16_t& s_acc, const f32x16_t& p_acc) {
+    const char* slot = reinterpret_cast<const char*>(smem) + slot_of(t);
+    const uint16_t* tq = reinterpret_cast<const uint16_t*>(slot);
+    const uint16_t* to = tq + 32 * D;
+    // mask: the forward word of fwd-lane l' = q + 32·hh' holds bit r' for key acc_row(r', hh'); this lane
+    // (key krel) needs, for query rows acc_row(r, hh) = 8g + 4hh + i, bit r_f of the words of fwd-lanes
+    // 8g + 4hh + i + 32·hh_f: four consecutive words per g, one 8-byte LDS read per g
+    const uint16_t* wsrc = reinterpret_cast<const uint16_t*>(slot + 2 * RTILE + 640) + wave * 64 + 4 * hh + 32 * hh_f;
+    const float* sdl = reinterpret_cast<const float*>(slot + 2 * RTILE + 512);
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        float pd[8], dsv[8];
+    for (int s = 0; s < 2; ++s) {
+      // this half's dV / dK operands read ahead of the exp / mask VALU that produces the other operand
+      bf16x8_t ov[2], oq[2];
 #pragma unroll
-        for (int gg = 0; gg < 2; ++gg) {
-          const int g = 2 * s + gg;
-          const float4 d4 = *reinterpret_cast<const float4*>(sdl + 8 * g + 4 * hh);
-          const f2_t dl[2] = {f2_t{d4.x, d4.y}, f2_t{d4.z, d4.w}};
-          float P[4], dp[4];
+      for (int d = 0; d < 2; ++d) {
+        ov[d] = tr8(to, 0, lo_, s, d);
+        oq[d] = tr8(tq, 0, lo_, s, d);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      float pd[8], dsv[8];
+#pragma unroll
+      for (int gg = 0; gg < 2; ++gg) {
+        const int g = 2 * s + gg;
+        const float4 d4 = *reinterpret_cast<const float4*>(sdl + 8 * g + 4 * hh);
+        const f2_t dl[2] = {f2_t{d4.x, d4.y}, f2_t{d4.z, d4.w}};
+        float P[4], dp[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          P[i] = __builtin_amdgcn_exp2f(s_acc[4 * g + i]);
+          dp[i] = p_acc[4 * g + i];
+        }
+        // keep bits as AND masks: pd = P·mask (kscale is applied once, at the dV store), dS = P·(dP·mask·ksc − δ)
+        float pm[4] = {P[0], P[1], P[2], P[3]};
+        if constexpr (DROP) {
+          const uint64_t w = *reinterpret_cast<const uint64_t*>(wsrc + 8 * g);
+          const uint32_t wl = (uint32_t)w, wh = (uint32_t)(w >> 32);
+          const int pos[4] = {r_f, r_f + 16, r_f, r_f + 16};
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            P[i] = __builtin_amdgcn_exp2f(s_acc[4 * g + i]);
-            dp[i] = p_acc[4 * g + i];
-          }
-          // keep bits as AND masks: pd = P·mask (kscale is applied once, at the dV store), dS = P·(dP·mask·ksc − δ)
-          float pm[4] = {P[0], P[1], P[2], P[3]};
-          if constexpr (DROP) {
-            const uint64_t w = *reinterpret_cast<const uint64_t*>(wsrc + 8 * g);
-            const uint32_t wl = (uint32_t)w, wh = (uint32_t)(w >> 32);
-            const int pos[4] = {r_f, r_f + 16, r_f, r_f + 16};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              pm[i] = keep_and(P[i], i < 2 ? wl : wh, pos[i]);
-              dp[i] = keep_and(dp[i], i < 2 ? wl : wh, pos[i]);
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const f2_t Pj = {P[2 * j], P[2 * j + 1]}, dpj = {dp[2 * j], dp[2 * j + 1]};
-            const f2_t v = (dpj * ksc2 - dl[j]) * Pj;
-            pd[4 * gg + 2 * j] = pm[2 * j];
-            pd[4 * gg + 2 * j + 1] = pm[2 * j + 1];
-            dsv[4 * gg + 2 * j] = v.x;
-            dsv[4 * gg + 2 * j + 1] = v.y;
+            pm[i] = keep_and(P[i], i < 2 ? wl : wh, pos[i]);
+            dp[i] = keep_and(dp[i], i < 2 ? wl : wh, pos[i]);
           }
         }
-        const bf16x8_t pb = pack_b(pd, 0), sb = pack_b(dsv, 0);
 #pragma unroll
-        for (int d = 0; d < 2; ++d) {
-          dv[d] = mfma32(tr8(to, 0, lo_, s, d), pb, dv[d]);
-          dk[d] = mfma32(tr8(tq, 0, lo_, s, d), sb, dk[d]);
+        for (int j = 0; j < 2; ++j) {
+          const f2_t Pj = {P[2 * j], P[2 * j + 1]}, dpj = {dp[2 * j], dp[2 * j + 1]};
+          const f2_t v = (dpj * ksc2 - dl[j]) * Pj;
+          pd[4 * gg + 2 * j] = pm[2 * j];
+          pd[4 * gg + 2 * j + 1] = pm[2 * j + 1];
+          dsv[4 * gg + 2 * j] = v.x;
+          dsv[4 * gg + 2 * j + 1] = v.y;
         }
       }
+      const bf16x8_t pb = pack_b(pd, 0), sb = pack_b(dsv, 0);
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        dv[d] = mfma32(ov[d], pb, dv[d]);
+        dk[d] = mfma32(oq[d], sb, dk[d]);
+      }
     }
-    if (t + 1 < n32) {                                  // the other slot: last read before this barrier
-      if constexpr (NT > 0) {
-        commit(t + 1, st[(t + 1) % 3]);
-        __syncthreads();
-        if (t + 4 < n32) issue(t + 4, st[(t + 1) % 3]);
-      } else {
-        commit(t + 1, st[0]);
-        __syncthreads();
-        st[0] = st[1];
-        st[1] = st[2];
-        if (t + 4 < n32) issue(t + 4, st[2]);
+  };
+  // Tile t lives in register set st[t % 3] (compile-time index in the unrolled NT > 0 loop: a rotation by
+  // copies would make hipcc wait for the NEWER tile's loads before each copy); the rolled NT = 0 loop
+  // rotates by copies (one tile less lookahead).
+  Stage st[3];
+  issue(0, st[0]);
+  if (n32 > 1) issue(1, st[1]);
+  if (n32 > 2) issue(2, st[2]);
+  constexpr int UNR = NT > 0 ? NT : 1;
+  {
+    commit(0, st[0]);
+    __syncthreads();
+    if constexpr (NT > 0) {
+      if (n32 > 3) issue(3, st[0]);
+    } else {
+      st[0] = st[1];
+      st[1] = st[2];
+      if (n32 > 3) issue(3, st[2]);
+    }
+#pragma unroll UNR
+    for (int t = 0; t < n32; ++t) {
+      if (active) {
+        f32x16_t s_acc, p_acc;
+        scores(t, s_acc, p_acc);
+        grads(t, s_acc, p_acc);
+      }
+      if (t + 1 < n32) {                                  // the other slot: last read before this barrier
+        if constexpr (NT > 0) {
+          commit(t + 1, st[(t + 1) % 3]);
+          __syncthreads();
+          if (t + 4 < n32) issue(t + 4, st[(t + 1) % 3]);
+        } else {
+          commit(t + 1, st[0]);
+          __syncthreads();
+          st[0] = st[1];
+          st[1] = st[2];
+          if (t + 4 < n32) issue(t + 4, st[2]);
+        }
       }
     }
   }
