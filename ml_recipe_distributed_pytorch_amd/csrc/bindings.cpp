@@ -81,7 +81,7 @@ void embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tenso
   const int nb = hq_embed_bwd_partials((int)T, (int)seq_len);
   auto part = at::empty({nb, 4 * H}, gamma.options());
   const int V = (int)ww.size(0);
-  const HqEmbScratchSizes zs = hq_embed_bwd_scratch((int)T, V, (int)seq_len);
+  const HqEmbScratchSizes zs = hq_embed_bwd_scratch((int)T, V, (int)seq_len, (int)wp.size(0));
   auto pairs = at::empty({4, T}, ids.options().dtype(at::kInt));
   auto sort_tmp = at::empty({(int64_t)std::max<size_t>(zs.sort_bytes, 1)}, ids.options().dtype(at::kByte));
   auto carry = at::empty({(int64_t)zs.chunks * 2, H}, gamma.options());

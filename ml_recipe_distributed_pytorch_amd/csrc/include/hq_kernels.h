@@ -46,7 +46,7 @@ struct HqEmbScratchSizes {
   size_t sort_bytes;
   int chunks, pos_rows;
 };
-HqEmbScratchSizes hq_embed_bwd_scratch(int T, int V, int L);
+HqEmbScratchSizes hq_embed_bwd_scratch(int T, int V, int L, int P);
 void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww,
                   const uint16_t* wp, const uint16_t* wt, const float* gamma, const float* mean, const float* rstd,
                   float* g_word, float* g_pos, float* g_type, float* part, HqOuts outs, int T, int H, int n_types,

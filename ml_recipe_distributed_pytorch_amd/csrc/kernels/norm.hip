@@ -584,7 +584,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
     const uint16_t* __restrict__ wt, const float* __restrict__ gamma, const float* __restrict__ mean,
     const float* __restrict__ rstd, float* __restrict__ g_pos, float* __restrict__ g_type, float* __restrict__ ppart,
     float* __restrict__ part, int T, int H, int n_types, int pad_pos, HqDropKey kd_, uint32_t thr, float kscale, int V,
-    int P, int B, int L) {
+    int P, int B, int L, int PL) {
   const uint32_t key = kd_.get();
   extern __shared__ __attribute__((aligned(16))) float lds[];  // [4][H] block-partial scratch
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -602,8 +602,9 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
 #pragma unroll
     for (int i = 0; i < 4; ++i) pacc[c][i] = 0.f;
   const int l = blockIdx.x * kWaves + wave;
-  // this wave's position-partial row (ppart = null: every position flush is atomic)
-  float* prow = (ppart != nullptr && l < L) ? ppart + ((size_t)blockIdx.y * L + l) * H : nullptr;
+  // this wave's position-partial row [blockIdx.y][l] (l < PL = min(L, P): pid == l needs l < P; ppart = null:
+  // every position flush is atomic)
+  float* prow = (ppart != nullptr && l < PL) ? ppart + ((size_t)blockIdx.y * PL + l) * H : nullptr;
   bool pstored = false;
   int pcur = -1;
   auto flush_pos = [&]() {
@@ -1069,7 +1070,7 @@ static void emb_sort_check(hipError_t e) {
 }
 static int emb_sort_bits(int V) { return V > 1 ? 32 - __builtin_clz((unsigned)(V - 1)) : 1; }
 
-HqEmbScratchSizes hq_embed_bwd_scratch(int T, int V, int L) {
+HqEmbScratchSizes hq_embed_bwd_scratch(int T, int V, int L, int P) {
   HqEmbScratchSizes z{};
   size_t bytes = 0;
   emb_sort_check(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
@@ -1077,7 +1078,8 @@ HqEmbScratchSizes hq_embed_bwd_scratch(int T, int V, int L) {
   z.sort_bytes = bytes;
   z.chunks = (T + kEmbCH - 1) / kEmbCH;
   if (L <= 0 || T % L) L = T;
-  z.pos_rows = L <= kEmbMaxL ? ((T / L + kEmbNB - 1) / kEmbNB) * L : 0;
+  // partial rows exist for the positions l < min(L, P) only: a row whose pid == l needs l < P
+  z.pos_rows = L <= kEmbMaxL ? ((T / L + kEmbNB - 1) / kEmbNB) * std::min(L, P) : 0;
   return z;
 }
 
@@ -1093,7 +1095,8 @@ void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, c
   const int B = T / L;
   const dim3 grid((L + kWaves - 1) / kWaves, (B + kEmbNB - 1) / kEmbNB);
   const int nb = hq_embed_bwd_partials(T, L);
-  const HqEmbScratchSizes z = hq_embed_bwd_scratch(T, V, L);
+  const HqEmbScratchSizes z = hq_embed_bwd_scratch(T, V, L, P);
+  const int PL = std::min(L, P);   // position-partial rows per batch slice
   float* ppart = z.pos_rows > 0 ? sc.ppart : nullptr;
   // (id, row) sort: stable, so every id's rows stay in token order
   hipLaunchKernelGGL(embed_keys_kernel, dim3((T + 255) / 256), dim3(256), 0, s, ids, sc.keys, sc.rows, T);
@@ -1104,7 +1107,8 @@ void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, c
   dispatch_nch(H, [&](auto nch) {
     constexpr int C = decltype(nch)::value;
     hipLaunchKernelGGL(embed_bwd_kernel<C>, grid, dim3(256), 4 * H * sizeof(float), s, dy, ids, pids, tids, ww, wp, wt,
-                       gamma, mean, rstd, g_pos, g_type, ppart, part, T, H, n_types, pad_pos, key, thr, ks, V, P, B, L);
+                       gamma, mean, rstd, g_pos, g_type, ppart, part, T, H, n_types, pad_pos, key, thr, ks, V, P, B, L,
+                       PL);
     hipLaunchKernelGGL(embed_word_kernel<C>, dim3(nwb), dim3(256), 0, s, sc.skeys, sc.srows, dy, ids, pids, tids, ww,
                        wp, wt, gamma, mean, rstd, g_word, sc.carry, T, H, pad_word, accumulate ? 1 : 0, key, thr, ks);
     hipLaunchKernelGGL(embed_carry_kernel<C>, dim3(nwb), dim3(256), 0, s, sc.skeys, sc.carry, g_word, T, H, pad_word,
@@ -1112,9 +1116,9 @@ void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, c
   });
   // outs: gamma, beta, type0, type1 (type rows only when n_types <= 2)
   colsum(part, nb, 4 * H, outs, H, accumulate, s);
-  // position partials [B / kEmbNB][L][H] -> rows 0 … L-1 of g_pos, on top of its zeroed (or accumulated) rows and
-  // the atomic flushes of non-default position ids
-  if (ppart) colsum(ppart, (B + kEmbNB - 1) / kEmbNB, L * H, HqOuts{{g_pos, nullptr, nullptr, nullptr}}, L * H, true, s);
+  // position partials [B / kEmbNB][min(L, P)][H] -> rows 0 … min(L, P)-1 of g_pos, on top of its zeroed (or
+  // accumulated) rows and the atomic flushes of non-default position ids
+  if (ppart) colsum(ppart, (B + kEmbNB - 1) / kEmbNB, PL * H, HqOuts{{g_pos, nullptr, nullptr, nullptr}}, PL * H, true, s);
 }
 
 void hq_gelu_fwd(const uint16_t* pre, uint16_t* out, size_t n, hipStream_t s) {
