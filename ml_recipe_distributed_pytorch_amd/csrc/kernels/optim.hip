@@ -87,6 +87,20 @@ __device__ __forceinline__ void adamw_elem(float& p, float& m, float& v, float g
   if (wd > 0.f) p = p - (lr * wd) * p;
 }
 
+__device__ __forceinline__ void st_nt4(float* dst, const float4& v) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __builtin_nontemporal_store(f4{v.x, v.y, v.z, v.w}, reinterpret_cast<f4*>(dst));
+}
+__device__ __forceinline__ float4 ld_nt4(const float* src) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_nt2(uint16_t* dst, const uint2& v) {
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  __builtin_nontemporal_store(u2{v.x, v.y}, reinterpret_cast<u2*>(dst));
+}
+
 __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, uint16_t* __restrict__ compute,
                                                     const float* __restrict__ grad, float* __restrict__ exp_avg,
                                                     float* __restrict__ exp_avg_sq, const HqOptChunk* __restrict__ chunks,
@@ -105,21 +119,23 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ master, 
       adamw_elem(p.y, m.y, v.y, g.y * cc, lr, wd, a);
       adamw_elem(p.z, m.z, v.z, g.z * cc, lr, wd, a);
       adamw_elem(p.w, m.w, v.w, g.w * cc, lr, wd, a);
-      *reinterpret_cast<float4*>(master + o) = p;
-      *reinterpret_cast<float4*>(exp_avg + o) = m;
-      *reinterpret_cast<float4*>(exp_avg_sq + o) = v;
+      // streaming (non-temporal) loads and stores: every state word is read and written once per step, so
+      // nothing is gained by allocating it in L2
+      st_nt4(master + o, p);
+      st_nt4(exp_avg + o, m);
+      st_nt4(exp_avg_sq + o, v);
       if (compute) {
         const float pf[4] = {p.x, p.y, p.z, p.w};
-        *reinterpret_cast<uint2*>(compute + o) = hq_pack4(pf);
+        st_nt2(compute + o, hq_pack4(pf));
       }
     };
     int i = threadIdx.x;
     for (; i + 256 < n4; i += 512) {
       const int64_t o0 = s0 + 4 * (int64_t)i, o1 = o0 + 4 * 256;
-      float4 p0 = *reinterpret_cast<float4*>(master + o0), p1 = *reinterpret_cast<float4*>(master + o1);
-      float4 m0 = *reinterpret_cast<float4*>(exp_avg + o0), m1 = *reinterpret_cast<float4*>(exp_avg + o1);
-      float4 v0 = *reinterpret_cast<float4*>(exp_avg_sq + o0), v1 = *reinterpret_cast<float4*>(exp_avg_sq + o1);
-      const float4 g0 = *reinterpret_cast<const float4*>(grad + o0), g1 = *reinterpret_cast<const float4*>(grad + o1);
+      float4 p0 = ld_nt4(master + o0), p1 = ld_nt4(master + o1);
+      float4 m0 = ld_nt4(exp_avg + o0), m1 = ld_nt4(exp_avg + o1);
+      float4 v0 = ld_nt4(exp_avg_sq + o0), v1 = ld_nt4(exp_avg_sq + o1);
+      const float4 g0 = ld_nt4(grad + o0), g1 = ld_nt4(grad + o1);
       step4(o0, p0, m0, v0, g0);
       step4(o1, p1, m1, v1, g1);
     }
