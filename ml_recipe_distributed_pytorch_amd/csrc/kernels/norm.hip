@@ -464,7 +464,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
 // loaded while the current row is reduced (one dependent HBM round trip per row otherwise).
 constexpr int kEmbNB = 16;       // batch rows per wave in the position pass (<= 64, as kEmbCH)
 constexpr int kEmbCH = 16;       // sorted rows per wave in the word pass (<= 64: one row's metadata per lane)
-constexpr int kEmbMaxL = 4096;   // position partials [T / L / kEmbNB][L][H] only for real sequence layouts
+constexpr int kEmbMaxL = 4096;   // position partials [T / L / kEmbNB][min(L, P)][H] only for real sequence layouts
 
 template <int NCH>
 struct EmbRow {
@@ -472,26 +472,6 @@ struct EmbRow {
   float mu, rs;
   uint2 w[NCH], p[NCH], t[NCH], d[NCH];
 };
-
-template <int NCH>
-__device__ __forceinline__ void emb_load(EmbRow<NCH>& r, size_t row, const uint16_t* __restrict__ dy,
-                                         const int64_t* __restrict__ ids, const int64_t* __restrict__ pids,
-                                         const int64_t* __restrict__ tids, const uint16_t* __restrict__ ww,
-                                         const uint16_t* __restrict__ wp, const uint16_t* __restrict__ wt,
-                                         const float* __restrict__ mean, const float* __restrict__ rstd, int H, int lane) {
-  r.id = ids[row]; r.pid = pids[row]; r.tid = tids[row];
-  r.mu = mean[row]; r.rs = rstd[row];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    const int col = c * 256 + lane * 4;
-    if (col < H) {
-      r.w[c] = *reinterpret_cast<const uint2*>(ww + (size_t)r.id * H + col);
-      r.p[c] = *reinterpret_cast<const uint2*>(wp + (size_t)r.pid * H + col);
-      r.t[c] = *reinterpret_cast<const uint2*>(wt + (size_t)r.tid * H + col);
-      r.d[c] = *reinterpret_cast<const uint2*>(dy + row * H + col);
-    }
-  }
-}
 
 // Row metadata of up to 64 rows, one row per lane (ids, position / type ids, LayerNorm statistics), loaded once
 // up front: the per-row loop then reads them with v_readlane and issues only the row-data loads — no dependent
