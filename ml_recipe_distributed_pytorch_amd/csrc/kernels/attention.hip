@@ -1093,6 +1093,14 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
     }
 #pragma unroll UNR
     for (int t = 0; t < n32; ++t) {
+      if constexpr (NT > 0) {
+        // tile t+1 into the other slot BEFORE this tile's work, so its LDS writes overlap the MFMA chains: that
+        // slot's last reader (tile t-1) finished before the previous barrier
+        if (t + 1 < n32) {
+          commit(t + 1, st[(t + 1) % 3]);
+          if (t + 4 < n32) issue(t + 4, st[(t + 1) % 3]);
+        }
+      }
       if (active) {
         f32x16_t s_acc, p_acc;
         scores(t, s_acc, p_acc);
@@ -1100,9 +1108,7 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
       }
       if (t + 1 < n32) {                                  // the other slot: last read before this barrier
         if constexpr (NT > 0) {
-          commit(t + 1, st[(t + 1) % 3]);
           __syncthreads();
-          if (t + 4 < n32) issue(t + 4, st[(t + 1) % 3]);
         } else {
           commit(t + 1, st[0]);
           __syncthreads();
