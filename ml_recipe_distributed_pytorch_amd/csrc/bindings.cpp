@@ -377,9 +377,16 @@ Tensor gemm_fp8(Tensor A8, Tensor B8, int64_t epi, c10::optional<Tensor> bias, T
   }
   if (epi == HQ_EPI_GELUD || epi == HQ_EPI_DMUL) {
     TORCH_CHECK(pre.has_value() && pre->defined(), "gemm_fp8: GELUD / DMUL need `pre` (gelu')");
-    check(*pre, BF16, "pre");
+    // with out8 (the fp8 forward / fp8 dgrad) gelu' travels as the 8-bit code (hq_gd_encode8), else as bf16
+    const bool code8 = out8.has_value() && out8->defined();
+    if (code8) {
+      TORCH_CHECK(pre->scalar_type() == at::kByte && pre->is_cuda() && pre->is_contiguous(),
+                  "gemm_fp8: with out8, `pre` is the uint8 gelu' code (gelud_code())");
+    } else {
+      check(*pre, BF16, "pre");
+    }
     TORCH_CHECK(pre->size(0) == M && pre->size(1) == N, "gemm_fp8: pre shape");
-    P = ptr<uint16_t>(*pre);
+    P = reinterpret_cast<uint16_t*>(pre->data_ptr());
     if (out8.has_value() && out8->defined()) {
       TORCH_CHECK(out8->scalar_type() == (fwd ? at::kFloat8_e4m3fn : at::kFloat8_e5m2),
                   "gemm_fp8: out8 must be float8_e4m3fn (GELUD) / float8_e5m2 (DMUL)");
@@ -828,6 +835,8 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("transpose_tiles", &transpose_tiles);
   m.def("transpose_tiles8", &transpose_tiles8);
   m.def("colsum_into", &colsum_into);
+  m.def("gelud_code", []() { return std::make_pair((double)kHqGdLo, (double)kHqGdStep); },
+        "(lo, step) of the fp8 path's 8-bit gelu' code: g = lo + q·step");
   m.def("fp8_quantize", &fp8_quantize);
   m.def("fp8_quant_delayed", &fp8_quant_delayed);
   m.def("fp8_quant_delayed_multi", &fp8_quant_delayed_multi);

@@ -7,6 +7,8 @@
 #include <hip/hip_bf16.h>
 #include <stdint.h>
 
+#include "hq_kernels.h"   // kHqGdLo / kHqGdStep
+
 #define HQ_WAVE 64
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // MFMA A/B fragment (4 VGPRs)
@@ -200,6 +202,26 @@ __device__ __forceinline__ void hq_keep4(uint32_t idx0, uint32_t key, uint32_t t
 // 30-binade exponent range affords the 5 binades that a 64× margin takes off its bottom.
 constexpr float kHqFp8Max = 448.f;      // OCP e4m3 (forward activations / weights)
 constexpr float kHqBf8Max = 57344.f;    // OCP e5m2 (backward activation gradients)
+
+// --precision fp8: the FFN1 epilogue stores gelu'(pre) for the FFN2 dgrad as an 8-bit linear code over its exact
+// range [−0.12890, 1.12890] (gelu'(∓√2)): q = rint((g − lo)·(1/step)) clamped to 0…255, g ≈ lo + q·step (absolute
+// error ≤ step/2 = 0.0025).  The dgrad's product is quantised to e5m2 (relative error up to 12.5 %) right after,
+// so bf16 precision on this operand bought nothing but 604 MB of extra traffic per FFN per step.
+// (kHqGdLo, kHqGdStep: hq_kernels.h, shared with the host bindings)
+__device__ __forceinline__ uint2 hq_gd_encode8(const float* g) {
+  constexpr float inv = 255.f / 1.2578125f;
+  uint32_t w[2] = {0u, 0u};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float q = fminf(fmaxf(rintf((g[e] - kHqGdLo) * inv), 0.f), 255.f);
+    w[e >> 2] |= (uint32_t)q << (8 * (e & 3));
+  }
+  return make_uint2(w[0], w[1]);
+}
+__device__ __forceinline__ void hq_gd_decode8(const uint2& c, float* g) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) g[e] = fmaf((float)(((e < 4 ? c.x : c.y) >> (8 * (e & 3))) & 0xFFu), kHqGdStep, kHqGdLo);
+}
 constexpr float kHqFp8Margin = 2.f;
 constexpr float kHqBf8Margin = 64.f;
 __device__ __forceinline__ float hq_fp8_delayed_scale(const float* st, int phase, float fmax = kHqFp8Max) {

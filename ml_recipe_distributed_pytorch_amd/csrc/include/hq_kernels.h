@@ -7,6 +7,11 @@
 #include <algorithm>
 #include <type_traits>
 
+// --precision fp8: 8-bit linear code of gelu'(pre) between the FFN1 forward and the FFN2 dgrad (hq_common.h,
+// hq_gd_encode8 / hq_gd_decode8): g = kHqGdLo + q·kHqGdStep over gelu''s exact range [−0.12890, 1.12890]
+constexpr float kHqGdLo = -0.12890625f;
+constexpr float kHqGdStep = 1.2578125f / 255.f;
+
 struct HqOuts {  // up to 4 fp32 column-sum destinations (null = skip), passed by value
   float* p[4];
 };

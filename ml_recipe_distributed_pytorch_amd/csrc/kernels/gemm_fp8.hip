@@ -87,6 +87,18 @@ constexpr bool grad_epi(int epi) { return epi == HQ_EPI_NONE || epi == HQ_EPI_DM
 // P (DMUL: gelu', RESID: residual) loaded ahead.  WC = false skips the bf16 output (GELUD / DMUL with Q8, once
 // every consumer reads the fp8 copy) — a template flag: a runtime test around the 16 unrolled stores made hipcc
 // spill the DMUL epilogue.
+// the epilogue operand piece at element offset goff: 8 bf16 (RESID's residual, bf16 DMUL's gelu') or, for the
+// fp8 DMUL (Q8), the 8-byte gelu' code the fp8 FFN1 forward stored (hq_gd_encode8)
+template <int EPI, bool Q8>
+__device__ __forceinline__ uint4 load_aux(const uint16_t* __restrict__ P, size_t goff) {
+  if constexpr (EPI == HQ_EPI_DMUL && Q8) {
+    const uint2 c = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(P) + goff);
+    return make_uint4(c.x, c.y, 0u, 0u);
+  } else {
+    return *reinterpret_cast<const uint4*>(P + goff);
+  }
+}
+
 template <int EPI, bool Q8, bool WC>
 __device__ __forceinline__ void epi_piece(uint4 piece, const uint4& aux, size_t goff, uint16_t* __restrict__ C,
                                           uint16_t* __restrict__ P, uint8_t* __restrict__ C8, float inv8, float& amax,
@@ -99,9 +111,13 @@ __device__ __forceinline__ void epi_piece(uint4 piece, const uint4& aux, size_t 
     for (int e = 0; e < 8; ++e) d[e] += rr[e];
     piece = hq_pack8(d);
   } else if constexpr (EPI == HQ_EPI_DMUL) {
+    // no fma contraction of d·gd into the column sum: hipcc contracted it in one kernel form and not the
+    // other, and the per-tile / persistent partials must agree bit for bit
+#pragma clang fp contract(off)
     float d[8], gd[8];
     hq_unpack8(piece, d);
-    hq_unpack8(aux, gd);
+    if constexpr (Q8) hq_gd_decode8(make_uint2(aux.x, aux.y), gd);   // the fp8 forward's 8-bit gelu' code
+    else hq_unpack8(aux, gd);
 #pragma unroll
     for (int e = 0; e < 8; ++e) { d[e] *= gd[e]; csum[e] += d[e]; }
     piece = hq_pack8(d);
@@ -115,7 +131,8 @@ __device__ __forceinline__ void epi_piece(uint4 piece, const uint4& aux, size_t 
     float x[8], g[8];
     hq_unpack8(piece, x);
     hq_gelu_grad8(x, g);   // g = gelu'(x), x = gelu(x)
-    *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
+    if constexpr (Q8) *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(P) + goff) = hq_gd_encode8(g);
+    else *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
     piece = hq_pack8(x);
     if constexpr (Q8) {
       float f[8];
@@ -277,7 +294,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
   float csum[8];
   if constexpr (kAux) {
 #pragma unroll
-    for (int it = 0; it < NIT; ++it) aux[it] = *reinterpret_cast<const uint4*>(P + (size_t)grow_of(it) * ldc + gcol);
+    for (int it = 0; it < NIT; ++it) aux[it] = load_aux<EPI, Q8>(P, (size_t)grow_of(it) * ldc + gcol);
   }
   if constexpr (EPI == HQ_EPI_DMUL) {
 #pragma unroll
@@ -520,7 +537,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* _
         uint4 aux[kAux ? AB : 1];
         if constexpr (kAux) {
 #pragma unroll
-          for (int it = 0; it < AB; ++it) aux[it] = *reinterpret_cast<const uint4*>(P + goff_of(h + it));
+          for (int it = 0; it < AB; ++it) aux[it] = load_aux<EPI, Q8>(P, goff_of(h + it));
         }
 #pragma unroll
         for (int it = 0; it < AB; ++it) {

@@ -270,20 +270,39 @@ def linear_fwd_fp8_own(x8, x_state: Fp8DelayedState, w8s, b32):
     return _k().gemm_fp8(x8, w8, _EPI_BIAS, b32, x_state.scale, sw.reshape(1).float())
 
 
+def gelud_code():
+    """(lo, step) of the fp8 path's 8-bit gelu' code (hq_kernels.h kHqGdLo / kHqGdStep): g ≈ lo + q·step."""
+    return _k().gelud_code()
+
+
+def gelud_encode(g: torch.Tensor) -> torch.Tensor:
+    """gelu' → the 8-bit code, as the fp8 FFN1 epilogue writes it (hq_gd_encode8: fp32 (g − lo)·(1/step), round
+    half to even, clamp 0…255)."""
+    lo, step = gelud_code()
+    inv = torch.tensor(255.0 / 1.2578125, dtype=torch.float32)
+    q = torch.round((g.float() - torch.tensor(lo, dtype=torch.float32)) * inv.to(g.device))
+    return q.clamp_(0, 255).to(torch.uint8)
+
+
+def gelud_decode(q: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
+    lo, step = gelud_code()
+    return (q.float() * step + lo).to(dtype)
+
+
 def linear_gelu_fwd_fp8(x, w8s, b32, in_state: Fp8DelayedState, out_state: Fp8DelayedState, x8=None,
                         need_act: bool = True):
-    """FFN1 in fp8 on the own block-scaled MFMA kernel (gemm_fp8.hip): returns (gelu'(pre), act, act8)
-    — act in bf16 (for a bf16 FFN2 weight gradient; ``need_act=False`` skips it and returns None when the
-    fp8 weight gradient will read act8) and in e4m3 under ``out_state``'s delayed scale for the FFN2 fp8
-    GEMM; None when the shape does not tile (caller falls back).  ``x8``: the input already in e4m3 under
-    ``in_state`` (LN forward's fp8 output), else it is quantised here."""
+    """FFN1 in fp8 on the own block-scaled MFMA kernel (gemm_fp8.hip): returns (gelu'(pre) as the 8-bit code of
+    ``gelud_code()``, act, act8) — act in bf16 (for a bf16 FFN2 weight gradient; ``need_act=False`` skips it and
+    returns None when the fp8 weight gradient will read act8) and in e4m3 under ``out_state``'s delayed scale for
+    the FFN2 fp8 GEMM; None when the shape does not tile (caller falls back).  ``x8``: the input already in e4m3
+    under ``in_state`` (LN forward's fp8 output), else it is quantised here."""
     M, K, N = x.shape[0], x.shape[1], w8s[0].shape[0]
     if not _k().gemm_fp8_supported(M, N, K):
         return None
     if x8 is None:
         x8 = in_state.quantize(x)
     w8, sw = w8s
-    gd = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    gd = torch.empty(M, N, dtype=torch.uint8, device=x.device)
     act8 = torch.empty(M, N, dtype=torch.float8_e4m3fn, device=x.device)
     act = _k().gemm_fp8(x8, w8, _EPI_GELUD, b32, in_state.scale, sw.reshape(1).float(), pre=gd, out8=act8,
                         state=out_state.buf, phase=out_state.next_phase(), write_out=bool(need_act))
@@ -307,10 +326,13 @@ def linear_dgrad_add_fp8(dy8, dy_state: Fp8DelayedState, wt8s, resid):
 
 def linear_dgrad_gelu_fp8(dy8, dy_state: Fp8DelayedState, wt8s, gd, g_bias, accumulate, out_state: Fp8DelayedState,
                           need_bf16: bool = True):
-    """FFN2 dgrad in fp8: dpre = (dy·W) ⊙ gelu'(pre) (``gd``: the gelu' stored by the forward), the FFN1 bias
-    gradient from the epilogue's column sums, and dpre also in e5m2 under ``out_state`` for the FFN1 dgrad:
-    (dpre, dpre8); ``need_bf16=False`` (every consumer reads dpre8) skips the bf16 dpre (returned as None)."""
+    """FFN2 dgrad in fp8: dpre = (dy·W) ⊙ gelu'(pre) (``gd``: the gelu' code stored by the fp8 forward; a bf16
+    gelu' from a bf16 forward is encoded first), the FFN1 bias gradient from the epilogue's column sums, and dpre
+    also in e5m2 under ``out_state`` for the FFN1 dgrad: (dpre, dpre8); ``need_bf16=False`` (every consumer reads
+    dpre8) skips the bf16 dpre (returned as None)."""
     wt8, sw = wt8s
+    if gd.dtype != torch.uint8:
+        gd = gelud_encode(gd)
     M, N = dy8.shape[0], wt8.shape[0]
     part = torch.empty(M // 256, N, dtype=torch.float32, device=dy8.device)
     dpre8 = torch.empty(M, N, dtype=torch.float8_e5m2, device=dy8.device)
@@ -364,6 +386,8 @@ def linear_dgrad_gelu_d(dy, w, saved, is_deriv, g_bias, accumulate, wt=None):
     M, N = dy.shape[0], w.shape[1]
     assert wt is not None, "stored-derivative GELU backward needs the Wᵀ working copy"
     _check_nt(M, N, dy.shape[1], "linear_dgrad_gelu_d")
+    if saved.dtype == torch.uint8:   # the fp8 forward's gelu' code, while the fp8 dgrad is still uncalibrated
+        saved = gelud_decode(saved)
     part = _part(M, N, dy.shape[1], dy.device)
     dpre = _k().gemm_nt(dy, wt, _EPI_DMUL, pre=saved, part=part)
     if g_bias is not None:

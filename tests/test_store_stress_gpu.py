@@ -144,12 +144,14 @@ def test_gemm_fp8_repeatable(cuda, name):
     sb = torch.full((1,), 0.02, device=cuda)
     bias = torch.randn(n_out, device=cuda, generator=g) * 0.1
     aux = _bf((T, n_out), torch.Generator(device=cuda).manual_seed(31), cuda)
+    code = torch.randint(0, 256, (T, n_out), device=cuda, dtype=torch.uint8,
+                         generator=torch.Generator(device=cuda).manual_seed(37))   # gelu' code for the fp8 DMUL
     outs = []
     for _ in range(REPS):
         if name == "fwd_bias":
             outs.append((k.gemm_fp8(A8, B8, EPI_BIAS, bias, sa, sb),))
         elif name == "fwd_gelud":
-            gd = torch.empty(T, n_out, device=cuda, dtype=torch.bfloat16)
+            gd = torch.empty(T, n_out, device=cuda, dtype=torch.uint8)   # the 8-bit gelu' code
             act8 = torch.empty(T, n_out, device=cuda, dtype=torch.float8_e4m3fn)
             state = torch.tensor([1.0, 1.0, 1.0, 0.01], device=cuda)
             c = k.gemm_fp8(A8, B8, EPI_GELUD, bias, sa, sb, pre=gd, out8=act8, state=state, phase=0)
@@ -160,7 +162,7 @@ def test_gemm_fp8_repeatable(cuda, name):
             part = torch.zeros(T // 256, n_out, device=cuda)
             out8 = torch.empty(T, n_out, device=cuda, dtype=torch.float8_e5m2)
             state = torch.tensor([1.0, 1.0, 1.0, 0.01], device=cuda)
-            c = k.gemm_fp8(A8, B8, EPI_DMUL, None, sa, sb, pre=aux, out8=out8, state=state, phase=0, part=part)
+            c = k.gemm_fp8(A8, B8, EPI_DMUL, None, sa, sb, pre=code, out8=out8, state=state, phase=0, part=part)
             outs.append((c, part, out8.view(torch.uint8)))
         else:
             outs.append((k.gemm_fp8(A8, B8, EPI_RESID, None, sa, sb, resid=aux),))
