@@ -209,13 +209,11 @@ constexpr float kHqBf8Max = 57344.f;    // OCP e5m2 (backward activation gradien
 // so bf16 precision on this operand bought nothing but 604 MB of extra traffic per FFN per step.
 // (kHqGdLo, kHqGdStep: hq_kernels.h, shared with the host bindings)
 __device__ __forceinline__ uint2 hq_gd_encode8(const float* g) {
-  constexpr float inv = 255.f / 1.2578125f;
+  // q = (g − lo)/step as one FMA, then v_cvt_pk_u8_f32 (round to nearest, saturate to 0…255) packs it into its byte
+  constexpr float inv = 255.f / 1.2578125f, off = -kHqGdLo * inv;
   uint32_t w[2] = {0u, 0u};
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float q = fminf(fmaxf(rintf((g[e] - kHqGdLo) * inv), 0.f), 255.f);
-    w[e >> 2] |= (uint32_t)q << (8 * (e & 3));
-  }
+  for (int e = 0; e < 8; ++e) w[e >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(fmaf(g[e], inv, off), e & 3, w[e >> 2]);
   return make_uint2(w[0], w[1]);
 }
 __device__ __forceinline__ void hq_gd_decode8(const uint2& c, float* g) {

@@ -276,11 +276,11 @@ def gelud_code():
 
 
 def gelud_encode(g: torch.Tensor) -> torch.Tensor:
-    """gelu' → the 8-bit code, as the fp8 FFN1 epilogue writes it (hq_gd_encode8: fp32 (g − lo)·(1/step), round
-    half to even, clamp 0…255)."""
+    """gelu' → the 8-bit code, as the fp8 FFN1 epilogue writes it (hq_gd_encode8: fp32 g·(1/step) − lo/step, round
+    to nearest, clamp 0…255)."""
     lo, step = gelud_code()
     inv = torch.tensor(255.0 / 1.2578125, dtype=torch.float32)
-    q = torch.round((g.float() - torch.tensor(lo, dtype=torch.float32)) * inv.to(g.device))
+    q = torch.round(g.float() * inv.to(g.device) - inv.to(g.device) * lo)
     return q.clamp_(0, 255).to(torch.uint8)
 
 

@@ -82,6 +82,8 @@ def test_gemm_fp8_gelud_delayed_q8(cuda, variant):
         torch.testing.assert_close(act.float(), y.detach(), atol=2e-2, rtol=2e-2)
         # the code's half step plus the bf16 pre the reference differentiates at
         torch.testing.assert_close(ops.gelud_decode(gd, torch.float32), x.grad, atol=step / 2 + 1e-2, rtol=0)
+        # rounded to nearest, not truncated: no systematic offset of half a step
+        assert abs((ops.gelud_decode(gd, torch.float32) - x.grad).mean().item()) < step / 8
         assert int(gd.min()) >= 0 and int(gd.max()) <= 255
         s = state[3].item()
         assert s == (1.0 if phase == 0 else pytest.approx(2 * act.float().abs().max().item() / 448, rel=1e-3))
