@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from ml_recipe_distributed_pytorch_amd import _native  # noqa: E402
 
 SHAPES = (("qkv", 2304, 768, (4, 6, 8, 9, 12, 18)), ("out", 768, 768, (14, 16, 20, 24, 28, 32, 56)),
-          ("ffn1", 3072, 768, (4, 6, 7, 8, 14)), ("ffn2", 768, 3072, (4, 6, 7, 8, 14)))
+          ("ffn1", 3072, 768, (4, 6, 7, 8, 10, 14)), ("ffn2", 768, 3072, (4, 6, 7, 8, 10, 14)))
 
 
 def main():
