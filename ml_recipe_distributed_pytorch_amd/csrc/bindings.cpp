@@ -823,6 +823,7 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("gemm_set_variant", [](int64_t v) { hq_gemm_set_variant((int)v); });
   m.def("gemm_set_store_policy", [](int64_t v) { hq_gemm_set_store_policy((int)v); });
   m.def("gemm_set_stagger", [](int64_t v) { hq_gemm_set_stagger((int)v); });
+  m.def("gemm_tn_set_variant", [](int64_t v) { hq_gemm_tn_set_variant((int)v); });
   m.def("gemm_set_sched", [](int64_t v) { hq_gemm_set_sched((int)v); });
   m.def("gemm_get_sched", []() { return (int64_t)hq_gemm_get_sched(); });
   m.def("gemm_tn", &gemm_tn, py::arg("dy"), py::arg("x"), py::arg("out"), py::arg("accumulate") = false,

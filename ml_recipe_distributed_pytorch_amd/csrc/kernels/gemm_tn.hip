@@ -28,6 +28,8 @@
 // fragment (12.5 % more MFMAs in a third of the waves of a third of the blocks) and write fp32 partials
 // [S][N] that the same reduce kernel folds in — replacing a separate 450 MB column-sum pass.
 #include <algorithm>
+#include <type_traits>
+#include <utility>
 #include <cstdlib>
 
 #include "hq_common.h"
@@ -47,6 +49,9 @@ __device__ __forceinline__ f32x4_t mfma16(const bf16x8_t& a, const bf16x8_t& b, 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 __device__ __forceinline__ int tswz(int t) { return (t & 3) | (((t >> 3) & 1) << 2); }
+// f(integral_constant<int, n>) for n = 0 … N-1, fully unrolled in order
+template <typename F, int... n>
+__device__ __forceinline__ void unroll_n(F&& f, std::integer_sequence<int, n...>) { (f(std::integral_constant<int, n>{}), ...); }
 
 // Fragment of 8 consecutive tokens (ks·32 + 8g … +7) of column `cblk`·16 + (lane & 15) from a half
 // image at LDS byte address `img`.  `roff` = (8g + q)·256 + 8p and `sw` = f(8g + q) are per-lane
@@ -254,6 +259,182 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn_kernel(const uint16_t* __
   }
 }
 
+// ------------------------------------------------------------------ lockstep form (no bias)
+// gemm_tn_kernel alternates its two wave rows (one row's MFMAs under the other's fragment reads), so at any
+// time ONE wave per SIMD issues MFMAs, and a K-tile has four barriers.  Here all 8 waves run in lockstep, BOTH
+// waves of a SIMD issue MFMAs all the time, and each wave hides its own fragment reads with two register
+// sets: a K-tile is two sub-steps of 32 tokens (ks 0, ks 1), each with its operands in one set (A0 A1: 16
+// VGPRs each, B0 B1: 8), and a sub-step first issues the 24 reads of the NEXT sub-step into the other set,
+// then its own 32 MFMAs — every read has a whole sub-step to land.  One barrier per K-tile, at the start of
+// ks 1: lgkmcnt(0) (every read of this K-tile's buffer has returned) + vmcnt(0) (this wave's share of K-tile
+// t+1 has landed) → barrier → K-tile t+2 is staged into this K-tile's buffer and K-tile t+1's ks-0 operands
+// are read.  Per accumulator the MFMAs run in gemm_tn_kernel's K order (ks 0, ks 1 per K-tile): bitwise equal.
+template <int LAB>   // lab switches (results wrong): bit 0 no vmcnt wait, bit 1 no fragment reads in the loop
+__global__ __launch_bounds__(kThreads, 1) void gemm_tn2_kernel(const uint16_t* __restrict__ A, const uint16_t* __restrict__ B,
+                                                               float* __restrict__ part, int T, int N, int K, int S,
+                                                               int tiles_k) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tiles = nwg / S;
+  const int split = id / tiles, tile = id % tiles;
+  const int n0 = (tile / tiles_k) * 256, k0 = (tile % tiles_k) * 256;
+  const int nkt = (T + BT - 1) / BT;
+  const int kt0 = (int)((long)split * nkt / S), kt1 = (int)((long)(split + 1) * nkt / S);
+  const int nt = kt1 - kt0;
+  const int rows = min(nt * BT, T - kt0 * BT);
+  HQ_DASSERT(n0 + 128 <= N && k0 + 128 <= K && nt >= 2 && rows > 0);
+
+  const uint16_t* Ab = A + (size_t)kt0 * BT * N + n0;
+  const uint16_t* Bb = B + (size_t)kt0 * BT * K + k0;
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, rows * N * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, rows * K * 2, 0x00020000);
+  int voA[2], voB[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 4 + (lane >> 4);
+    const int pos = lane & 15;
+    const int c16 = ((((pos >> 1) ^ tswz(row))) << 1) | (pos & 1);
+    voA[i] = (row * N + c16 * 8) * 2;
+    voB[i] = (row * K + c16 * 8) * 2;
+  }
+  auto stage = [&](const __amdgpu_buffer_rsrc_t& rs, const int (&vo)[2], int ld, int half, int t, char* img) {
+    char* dst = img + wave_u * 2048;
+    const int so = half * 256 + t * BT * ld * 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_void*)(dst + i * 1024), 16, vo[i], so, 0, 0);
+  };
+  auto stage_all = [&](int t) {   // 8 DMA instructions per wave
+    char* img = smem + (t & 1) * STAGE;
+    stage(rA, voA, N, 0, t, img);
+    stage(rA, voA, N, 1, t, img + HALF);
+    stage(rB, voB, K, 0, t, img + 2 * HALF);
+    stage(rB, voB, K, 1, t, img + 3 * HALF);
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int roff = (8 * g + qq) * 256 + 8 * pp;
+  const int sw = tswz(8 * g + qq);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  // per-lane read bases of this K-tile's stage (cA, cB) and of the next one's (nA, nB), swapped every K-tile:
+  // half, ks and second-read offsets are compile-time and go in the instruction's 16-bit offset field
+  uint32_t cA[4], cB[2], nA[4], nB[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    cA[i] = lds0 + roff + (((wm * 4 + i) ^ sw) << 5);
+    nA[i] = cA[i] + STAGE;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    cB[j] = lds0 + roff + (((wn * 2 + j) ^ sw) << 5);
+    nB[j] = cB[j] + STAGE;
+  }
+  bf16x8_t fa[2][2][4], fb[2][2][2];   // [set][half][fragment]
+  auto frag = [&](uint32_t base, auto off_c) {
+    constexpr int OFF = decltype(off_c)::value;
+    typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+    u32x2 lo, hi;
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(lo) : "v"(base), "i"(OFF) : "memory");
+    asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(base), "i"(OFF + 1024) : "memory");
+    typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+    const u32x4 u = {lo[0], lo[1], hi[0], hi[1]};
+    return __builtin_bit_cast(bf16x8_t, u);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  auto bar = []() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  // one of the 8 DMA instructions of K-tile t: A half 0/1, B half 0/1, two 1-KiB rows blocks each
+  auto stage_one = [&](auto pc_c, int t) {
+    constexpr int PC = decltype(pc_c)::value, W = PC >> 1, I = PC & 1;
+    char* dst = smem + (t & 1) * STAGE + W * HALF + wave_u * 2048 + I * 1024;
+    if constexpr (W < 2)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)dst, 16, voA[I], (W & 1) * 256 + t * BT * N * 2, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)dst, 16, voB[I], (W & 1) * 256 + t * BT * K * 2, 0, 0);
+  };
+  // fragment f (0 … 11) of a set: A0[0..3] B0[0..1] A1[0..3] B1[0..1] — the order in which the previous
+  // sub-step last read the registers it overwrites (its MFMAs run (mh, nh, i, j) with mh outermost)
+  auto read_frag = [&](auto q_c, auto f_c, const uint32_t (&ba)[4], const uint32_t (&bb)[2], auto ks_c) {
+    constexpr int Q = decltype(q_c)::value, f = decltype(f_c)::value, KO = decltype(ks_c)::value * 32 * 256;
+    if constexpr (f < 4) fa[Q][0][f] = frag(ba[f], std::integral_constant<int, KO>{});
+    else if constexpr (f < 6) fb[Q][0][f - 4] = frag(bb[f - 4], std::integral_constant<int, 2 * HALF + KO>{});
+    else if constexpr (f < 10) fa[Q][1][f - 6] = frag(ba[f - 6], std::integral_constant<int, HALF + KO>{});
+    else fb[Q][1][f - 10] = frag(bb[f - 10], std::integral_constant<int, 3 * HALF + KO>{});
+  };
+  // one sub-step: the 32 MFMAs of set P with the next sub-step's 12 fragments (24 ds_reads) into the other set
+  // after MFMAs 1, 3, …, 23 (hipcc spreads the pairs to one read per MFMA) and, with DMA, K-tile tdma's 8 staging
+  // instructions after MFMAs 2, 6, …, 30 — so that neither wave of a SIMD stalls its MFMA issue on an LDS or DMA
+  // burst.  (Measured slower: the 24 reads in one burst before the MFMAs; a second barrier mid-sub-step that
+  // let the next K-tile's DMA land later, with the reads packed into the second half.)
+  auto substep = [&](auto p_c, auto dma_c, const uint32_t (&ba)[4], const uint32_t (&bb)[2], auto rks_c, int tdma) {
+    constexpr int P = decltype(p_c)::value, Q = 1 - P;
+    __builtin_amdgcn_sched_barrier(0);
+    unroll_n([&](auto n_c) {
+      constexpr int n = decltype(n_c)::value;
+      constexpr int mh = n >> 4, nh = (n >> 3) & 1, ii = (n >> 1) & 3, jj = n & 1;
+      acc[mh * 4 + ii][nh * 2 + jj] = mfma16(fb[P][nh][jj], fa[P][mh][ii], acc[mh * 4 + ii][nh * 2 + jj]);
+      if constexpr ((n & 1) && (n >> 1) < 12) read_frag(std::integral_constant<int, Q>{}, std::integral_constant<int, (n >> 1)>{}, ba, bb, rks_c);
+      if constexpr (decltype(dma_c)::value && (n & 3) == 2) stage_one(std::integral_constant<int, (n >> 2)>{}, tdma);
+      __builtin_amdgcn_sched_barrier(0);
+    }, std::make_integer_sequence<int, 32>{});
+  };
+
+  // prologue: K-tiles 0 and 1 staged; K-tile 0's ks-0 fragments into set 0
+  stage_all(0);
+  stage_all(1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  bar();
+  unroll_n([&](auto f_c) { read_frag(I0{}, f_c, cA, cB, I0{}); }, std::make_integer_sequence<int, 12>{});
+  // Every K-tile stages K-tile t+2 and reads ahead unconditionally: past the split's last K-tile the DMA
+  // reads zeros (outside the buffer descriptor) into the consumed buffer and the reads fetch an idle image —
+  // a conditional would make hipcc hold two values of a register set across a branch.
+  for (int t = 0; t < nt; ++t) {
+    // ks 0 (set 0), reading ks 1 of this K-tile into set 1
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    substep(I0{}, std::false_type{}, cA, cB, I1{}, 0);
+    // ks 1 (set 1): sync, then K-tile t+2's staging and K-tile t+1's ks 0 (into set 0) under the MFMAs
+    if constexpr (LAB & 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_waitcnt vmcnt(0)" ::: "memory");
+    bar();
+    substep(I1{}, std::true_type{}, nA, nB, I0{}, t + 2);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { const uint32_t x = cA[i]; cA[i] = nA[i]; nA[i] = x; }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) { const uint32_t x = cB[j]; cB[j] = nB[j]; nB[j] = x; }
+  }
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");   // the trailing zero stages / reads
+
+  // epilogue: fp32 slab, straight from the accumulators (as gemm_tn_kernel)
+  float* out = part + (size_t)split * N * K;
+  const int fr = lane & 15, fq = lane >> 4;
+  const bool n_full = n0 + 256 <= N, k_full = k0 + 256 <= K;
+#pragma unroll
+  for (int I = 0; I < 8; ++I) {
+    const int row = n0 + (I >> 2) * 128 + wm * 64 + (I & 3) * 16 + fr;
+    if (!n_full && (I >> 2) == 1) continue;
+#pragma unroll
+    for (int J = 0; J < 4; ++J) {
+      if (!k_full && (J >> 1) == 1) continue;
+      const int col = k0 + (J >> 1) * 128 + wn * 32 + (J & 1) * 16 + fq * 4;
+      *reinterpret_cast<float4*>(out + (size_t)row * K + col) = make_float4(acc[I][J][0], acc[I][J][1], acc[I][J][2], acc[I][J][3]);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ fp8 (e5m2 dy × e4m3 x)
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 constexpr int BT8 = 128;   // tokens (bytes) per K-tile
@@ -454,12 +635,20 @@ int hq_gemm_tn_splits(int T, int N, int K) {
   return S;
 }
 
+// bias-free weight gradients: 0 = gemm_tn_kernel (alternating wave rows), 1 = gemm_tn2_kernel (lockstep)
+int g_tn_variant = 0;
+void hq_gemm_tn_set_variant(int v) { g_tn_variant = v; }
+
 void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, float* bpart, float* bout, int T, int N, int K,
                 int S, bool accumulate, hipStream_t s) {
   constexpr size_t lds = 2 * STAGE;
   static bool init = [] {
     (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<0, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     (void)hipFuncSetAttribute((const void*)gemm_tn_kernel<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm_tn2_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm_tn2_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm_tn2_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm_tn2_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     return true;
   }();
   (void)init;
@@ -467,6 +656,11 @@ void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, f
   if (bout)
     hipLaunchKernelGGL((gemm_tn_kernel<0, true>), dim3(tiles * S), dim3(kThreads), lds, s, A, B, part, bpart, T, N, K, S,
                        tiles_k);
+  else if (g_tn_variant >= 1 && g_tn_variant <= 4) {
+    auto k2 = g_tn_variant == 1 ? gemm_tn2_kernel<0> : g_tn_variant == 2 ? gemm_tn2_kernel<1>
+            : g_tn_variant == 3 ? gemm_tn2_kernel<2> : gemm_tn2_kernel<3>;
+    hipLaunchKernelGGL(k2, dim3(tiles * S), dim3(kThreads), lds, s, A, B, part, T, N, K, S, tiles_k);
+  }
   else
     hipLaunchKernelGGL((gemm_tn_kernel<0, false>), dim3(tiles * S), dim3(kThreads), lds, s, A, B, part, bpart, T, N, K, S,
                        tiles_k);

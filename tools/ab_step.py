@@ -4,7 +4,7 @@ per-step differences are not swamped by box-to-box variance.  Rounds alternate A
 median ms/step of each.
 
     python tools/ab_step.py --toggle gelu_deriv [--batch 256] [--rounds 4] [--steps 8]
-toggles: gemm_v1 (NT kernel v2 vs v1), halftail (GEMM half-tile tail on / off),
+toggles: tn_lockstep (weight-gradient kernel: lockstep vs alternating rows), gemm_v1 (NT kernel v2 vs v1), halftail (GEMM half-tile tail on / off),
          input_pipeline (on: bench.py's per-step host synthesis + pinned H2D; off: one resident batch)
 """
 import argparse
@@ -37,6 +37,8 @@ def set_toggle(name, on):
         if on and getattr(m, "_ab_side", None) is None:
             m._ab_side = torch.cuda.Stream(device=torch.device("cuda", 0))
         m.grad_side_stream = m._ab_side if on else None
+    elif name == "tn_lockstep":   # on: lockstep weight-gradient kernel (gemm_tn_set_variant(1)); off: alternating rows
+        _native.kernels().gemm_tn_set_variant(1 if on else 0)
     elif name == "gemm_v1":
         _native.kernels().gemm_set_variant(1 if on else 0)
     elif name == "gemm_v2":   # on: per-tile v2 everywhere; off: auto (persistent v3 for K <= 2304)
