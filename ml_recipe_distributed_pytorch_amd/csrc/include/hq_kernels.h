@@ -152,7 +152,7 @@ void hq_gemm_f32(const float* A, const float* B, float* C, const float* bias, co
 // also the fused bias gradient bout[N] (+)= Σ_t A[t, n] through slabs bpart[S][N].
 // hq_gemm_tn_splits: the split count for this shape, 0 = unsupported (need N%256, K%256 == 0, T >= 128;
 // a token tail T % 64 != 0 stages zero rows through the buffer descriptors' bounds).
-void hq_gemm_tn_set_variant(int v);   // bias-free wgrad kernel: 0 alternating rows, 1 lockstep (A/B, tests)
+void hq_gemm_tn_set_variant(int v);   // bias-free wgrad kernel: 0 auto, 1 lockstep, 5 alternating rows (A/B, tests)
 int hq_gemm_tn_splits(int T, int N, int K);
 void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, float* bpart, float* bout, int T, int N, int K,
                 int S, bool accumulate, hipStream_t s);

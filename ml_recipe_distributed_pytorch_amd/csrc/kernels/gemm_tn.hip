@@ -635,7 +635,10 @@ int hq_gemm_tn_splits(int T, int N, int K) {
   return S;
 }
 
-// bias-free weight gradients: 0 = gemm_tn_kernel (alternating wave rows), 1 = gemm_tn2_kernel (lockstep)
+// bias-free weight gradients: 0 = auto — gemm_tn2_kernel (lockstep) for N >= 2304 at K <= 768, where it measured
+// 5 % faster inside the training step (the FFN1 weight gradient; profiles/r5_tn_lockstep), gemm_tn_kernel
+// (alternating wave rows) elsewhere (the out-projection's was 11 % slower lockstep, FFN2's even); 1 = always
+// lockstep, 5 = always alternating rows; 2-4 lockstep lab builds (tests, tools/tn_variant_bench.py)
 int g_tn_variant = 0;
 void hq_gemm_tn_set_variant(int v) { g_tn_variant = v; }
 
@@ -656,8 +659,8 @@ void hq_gemm_tn(const uint16_t* A, const uint16_t* B, float* part, float* out, f
   if (bout)
     hipLaunchKernelGGL((gemm_tn_kernel<0, true>), dim3(tiles * S), dim3(kThreads), lds, s, A, B, part, bpart, T, N, K, S,
                        tiles_k);
-  else if (g_tn_variant >= 1 && g_tn_variant <= 4) {
-    auto k2 = g_tn_variant == 1 ? gemm_tn2_kernel<0> : g_tn_variant == 2 ? gemm_tn2_kernel<1>
+  else if ((g_tn_variant >= 1 && g_tn_variant <= 4) || (g_tn_variant == 0 && N >= 2304 && K <= 768)) {
+    auto k2 = g_tn_variant <= 1 ? gemm_tn2_kernel<0> : g_tn_variant == 2 ? gemm_tn2_kernel<1>
             : g_tn_variant == 3 ? gemm_tn2_kernel<2> : gemm_tn2_kernel<3>;
     hipLaunchKernelGGL(k2, dim3(tiles * S), dim3(kThreads), lds, s, A, B, part, T, N, K, S, tiles_k);
   }

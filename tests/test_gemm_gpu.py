@@ -195,10 +195,12 @@ def test_gemm_tn_wgrad(cuda, T, N, K, variant):
 @pytest.mark.gpu
 @pytest.mark.parametrize("T,N,K", [(128, 256, 256), (4 * 317, 768, 768), (200, 256, 512), (24576 - 37, 3072, 768),
                                    (98304, 2304, 768), (98304, 768, 768), (98304, 3072, 768), (98304, 768, 3072)])
-def test_gemm_tn_lockstep_bitwise(cuda, T, N, K):
+def test_gemm_tn_lockstep_bitwise(cuda, T, N, K, variant):
     """The lockstep weight-gradient kernel (gemm_tn_set_variant(1): both waves of a SIMD on MFMAs, one
-    barrier per K-tile) against the alternating-row kernel: bitwise equal (same K order per accumulator) at
-    every split count tried, token tails included, repeatable over launches."""
+    barrier per K-tile) against the alternating-row kernel (5): bitwise equal (same K order per accumulator) at
+    every split count tried, token tails included, repeatable over launches; the automatic choice (0) equals both."""
+    if variant:
+        pytest.skip("TN kernel variants are selected below")
     k = _native.kernels()
     g = torch.Generator(device=cuda).manual_seed(T + 3 * N + K)
     dy = (torch.rand(T, N, device=cuda, generator=g) * 2 - 1).bfloat16()
@@ -208,7 +210,7 @@ def test_gemm_tn_lockstep_bitwise(cuda, T, N, K):
     try:
         for s in splits:
             outs = []
-            for v in (0, 1, 1):
+            for v in (5, 1, 1, 0):
                 k.gemm_tn_set_variant(v)
                 out = base.clone()
                 k.gemm_tn(dy, x, out, True, s)
@@ -216,6 +218,7 @@ def test_gemm_tn_lockstep_bitwise(cuda, T, N, K):
                 outs.append(out)
             assert torch.equal(outs[0], outs[1]), (s, (outs[0] - outs[1]).abs().max().item())
             assert torch.equal(outs[1], outs[2]), s
+            assert torch.equal(outs[0], outs[3]), s
     finally:
         k.gemm_tn_set_variant(0)
 

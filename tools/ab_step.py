@@ -37,8 +37,10 @@ def set_toggle(name, on):
         if on and getattr(m, "_ab_side", None) is None:
             m._ab_side = torch.cuda.Stream(device=torch.device("cuda", 0))
         m.grad_side_stream = m._ab_side if on else None
-    elif name == "tn_lockstep":   # on: lockstep weight-gradient kernel (gemm_tn_set_variant(1)); off: alternating rows
-        _native.kernels().gemm_tn_set_variant(1 if on else 0)
+    elif name == "tn_lockstep":   # on: lockstep weight-gradient kernel everywhere (1); off: alternating rows (5)
+        _native.kernels().gemm_tn_set_variant(1 if on else 5)
+    elif name == "tn_auto":   # on: automatic choice (0, production); off: alternating rows everywhere (5)
+        _native.kernels().gemm_tn_set_variant(0 if on else 5)
     elif name == "gemm_v1":
         _native.kernels().gemm_set_variant(1 if on else 0)
     elif name == "gemm_v2":   # on: per-tile v2 everywhere; off: auto (persistent v3 for K <= 2304)

@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""Weight-gradient TN GEMM: the alternating-row kernel (variant 0) vs the lockstep kernel (variant 1) on the
+"""Weight-gradient TN GEMM: the alternating-row kernel (variant 5) vs the lockstep kernel (variant 1) on the
 BERT-base b256 wgrad shapes, median of interleaved launches (split-K reduce included), outputs compared bitwise.
 
     python tools/tn_variant_bench.py [reps]
@@ -25,7 +25,7 @@ def main():
     for name, N, K in SHAPES:
         dy = (torch.randn(T, N, device=dev) * 0.1).bfloat16()
         x = torch.randn(T, K, device=dev).bfloat16()
-        vs = [int(v) for v in os.environ.get("TN_VARIANTS", "0,1").split(",")]
+        vs = [int(v) for v in os.environ.get("TN_VARIANTS", "5,1").split(",")]
         outs = {v: torch.empty(N, K, device=dev) for v in vs}
         res = {v: [] for v in vs}
         for _ in range(reps):
