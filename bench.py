@@ -262,6 +262,15 @@ def main():
     ar_bytes = ((reducer.stats["bytes"] - bytes0) / args.steps) if reducer is not None else 0
     final_loss = res.losses.to_floats().get("loss", float("nan"))
     comm = reducer.pop_timings() if reducer is not None else {}
+    # data-parallel self-check, AFTER the clock: one more (untimed) step fingerprints its reduced gradient arena,
+    # then every rank's fp32 master weights and that gradient are all-gathered and compared with rank 0's — a
+    # reducer bug must fail the run, not be reported as a fast number
+    replica = None
+    if reducer is not None:
+        reducer.snapshot_grads = True
+        one_step()
+        torch.cuda.synchronize()
+        replica = reducer.replica_check()
     ms = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
     H, F, NL = cfg.hidden_size, cfg.intermediate_size, cfg.num_hidden_layers
@@ -301,7 +310,14 @@ def main():
                           if reducer is not None and comm.get("comm_span_ms") else None),
            "mfu_bf16_dense": round(value * flops_per_sample / (world * 2.5e15), 4),
            "max_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2),
-           "final_loss": round(final_loss, 4)}
+           "final_loss": round(final_loss, 4),
+           # cross-rank replica check (null without a reducer): exact fingerprints of the fp32 master arena and of
+           # an untimed extra step's reduced gradients, every rank vs rank 0
+           "weights_equal_across_ranks": replica["weights_equal_across_ranks"] if replica else None,
+           "grads_equal_across_ranks": replica["grads_equal_across_ranks"] if replica else None,
+           "replica_mismatch_parts": replica["replica_mismatch_parts"] if replica else None,
+           "max_weight_partial_mismatch": replica["max_weight_partial_mismatch"] if replica else None,
+           "rccl_comm_ranks_ok": replica["rccl_comm_ranks_ok"] if replica else None}
     if args.profile:
         out["phase_ms"] = {k: round(v / args.steps, 3) for k, v in phase.items()}
     if rank == 0:
@@ -314,6 +330,10 @@ def main():
         reducer.close()
     if launched:
         hqdist.destroy()
+    if replica is not None and not replica["ok"]:
+        print(f"[bench] error: data-parallel replica check failed on rank {rank}: {replica}", file=sys.stderr,
+              flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -21,7 +21,7 @@ _lock = threading.Lock()
 _cache = {}
 
 
-_DEBUG_DIR = os.path.join(_PKG_DIR, "csrc", "build", "debug")
+_DEBUG_DIR = os.path.join(_PKG_DIR, "_debug")   # in-tree (travels to the GPU box; csrc/build/ does not)
 
 
 def _load(name: str, directory: str = _PKG_DIR):

@@ -363,6 +363,7 @@ Tensor gemm_fp8(Tensor A8, Tensor B8, int64_t epi, c10::optional<Tensor> bias, T
   uint8_t* C8 = nullptr;
   float* q8 = nullptr;
   float* pp = nullptr;
+  bool code8 = true;
   if (epi == HQ_EPI_DMUL) {
     TORCH_CHECK(part.has_value() && part->defined(), "gemm_fp8: DMUL needs `part` [M/256, N]");
     check(*part, F32, "part");
@@ -377,13 +378,18 @@ Tensor gemm_fp8(Tensor A8, Tensor B8, int64_t epi, c10::optional<Tensor> bias, T
   }
   if (epi == HQ_EPI_GELUD || epi == HQ_EPI_DMUL) {
     TORCH_CHECK(pre.has_value() && pre->defined(), "gemm_fp8: GELUD / DMUL need `pre` (gelu')");
-    // with out8 (the fp8 forward / fp8 dgrad) gelu' travels as the 8-bit code (hq_gd_encode8), else as bf16
-    const bool code8 = out8.has_value() && out8->defined();
+    // gelu' travels as the 8-bit code (hq_gd_encode8, a uint8 `pre`) between the fp8 FFN1 forward and the fp8
+    // FFN2 dgrad, else as bf16.  The fp8 DMUL reads only the code; the fp8 GELUD writes bf16 gelu' (beside its
+    // e4m3 act) only together with the bf16 act, i.e. when the backward will run the FFN2 dgrad in bf16.
+    const bool with8 = out8.has_value() && out8->defined();
+    code8 = pre->scalar_type() == at::kByte;
     if (code8) {
-      TORCH_CHECK(pre->scalar_type() == at::kByte && pre->is_cuda() && pre->is_contiguous(),
-                  "gemm_fp8: with out8, `pre` is the uint8 gelu' code (gelud_code())");
+      TORCH_CHECK(with8 && pre->is_cuda() && pre->is_contiguous(),
+                  "gemm_fp8: the uint8 gelu' code (gelud_code()) goes with out8");
     } else {
       check(*pre, BF16, "pre");
+      TORCH_CHECK(!with8 || (epi == HQ_EPI_GELUD && write_out),
+                  "gemm_fp8: a bf16 gelu' with out8 needs GELUD with write_out (fp8 DMUL reads the uint8 code)");
     }
     TORCH_CHECK(pre->size(0) == M && pre->size(1) == N, "gemm_fp8: pre shape");
     P = reinterpret_cast<uint16_t*>(pre->data_ptr());
@@ -402,7 +408,7 @@ Tensor gemm_fp8(Tensor A8, Tensor B8, int64_t epi, c10::optional<Tensor> bias, T
   hq_gemm_fp8(reinterpret_cast<const uint8_t*>(A8.data_ptr()), reinterpret_cast<const uint8_t*>(B8.data_ptr()),
               write_out ? ptr<uint16_t>(C) : nullptr,
               optr<float>(bias), P, ptr<float>(sa), ptr<float>(sb), C8, q8, (int)(phase % 3), (int)M, (int)N, (int)K,
-              (int)epi, cur_stream(), pp);
+              (int)epi, cur_stream(), pp, code8 ? 1 : 0);
   return C;
 }
 
@@ -836,8 +842,42 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("transpose_tiles", &transpose_tiles);
   m.def("transpose_tiles8", &transpose_tiles8);
   m.def("colsum_into", &colsum_into);
+  m.def("ln_guard", [](Tensor master, Tensor goff, Tensor boff, int64_t H, double ratio) {
+    check(master, F32, "master");
+    TORCH_CHECK(goff.is_cuda() && boff.is_cuda() && goff.scalar_type() == at::kLong && boff.scalar_type() == at::kLong &&
+                goff.numel() == boff.numel() && goff.is_contiguous() && boff.is_contiguous(), "ln_guard: offsets");
+    // (offsets are validated against the arena on the host when the caller builds them: no device read here)
+    c10::DeviceGuard g(master.device());
+    auto flags = at::empty({goff.numel()}, master.options().dtype(at::kBool));
+    hq_ln_guard(ptr<float>(master), goff.data_ptr<int64_t>(), boff.data_ptr<int64_t>(), (int)goff.numel(), (int)H,
+                (float)ratio, reinterpret_cast<uint8_t*>(flags.data_ptr()), cur_stream());
+    return flags;
+  });
+  m.def("sort_ids", [](Tensor ids, int64_t V) {   // the embedding backward's stable id sort (tests)
+    TORCH_CHECK(ids.is_cuda() && ids.scalar_type() == at::kLong && ids.is_contiguous() && ids.dim() == 1,
+                "sort_ids: ids must be a contiguous int64 GPU vector");
+    c10::DeviceGuard g(ids.device());
+    const int T = (int)ids.numel();
+    auto buf = at::empty({4, std::max(T, 1)}, ids.options().dtype(at::kInt));
+    auto hist = at::empty({(int64_t)std::max<size_t>(hq_sort_ids_bytes(T, (int)V), 4)}, ids.options().dtype(at::kByte));
+    int32_t* b = buf.data_ptr<int32_t>();
+    const int64_t stride = std::max(T, 1);
+    hq_sort_ids(ids.data_ptr<int64_t>(), T, (int)V, b, b + stride, b + 2 * stride, b + 3 * stride, hist.data_ptr(),
+                hist.numel(), cur_stream());
+    return std::make_pair(buf[2].narrow(0, 0, T), buf[3].narrow(0, 0, T));
+  });
   m.def("gelud_code", []() { return std::make_pair((double)kHqGdLo, (double)kHqGdStep); },
         "(lo, step) of the fp8 path's 8-bit gelu' code: g = lo + q·step");
+  m.def("gelud_code_enc", []() { return std::make_pair((double)kHqGdInv, (double)kHqGdOff); },
+        "(inv, off) of the encoder: q = round(fma(g, inv, off)), clamp 0..255 (fp32)");
+  m.def("gelud_encode8", [](Tensor g) {
+    check(g, BF16, "g");
+    TORCH_CHECK(g.numel() % 8 == 0, "gelud_encode8: numel must be a multiple of 8");
+    c10::DeviceGuard dg(g.device());
+    auto q = at::empty(g.sizes(), g.options().dtype(at::kByte));
+    hq_gelud_encode8(ptr<uint16_t>(g), q.data_ptr<uint8_t>(), g.numel(), cur_stream());
+    return q;
+  });
   m.def("fp8_quantize", &fp8_quantize);
   m.def("fp8_quant_delayed", &fp8_quant_delayed);
   m.def("fp8_quant_delayed_multi", &fp8_quant_delayed_multi);
@@ -885,6 +925,16 @@ PYBIND11_MODULE(_hq_kernels, m) {
     auto part = at::empty({nparts}, x.options());
     hq_sq_norm_partials(ptr<float>(x), x.numel(), ptr<float>(part), (int)nparts, cur_stream());
     return part;
+  });
+  m.def("fingerprint", [](Tensor x, int64_t nparts) {
+    check(x, F32, "x");
+    TORCH_CHECK(x.is_contiguous(), "x must be contiguous");
+    TORCH_CHECK(nparts > 0 && nparts <= 65535, "nparts out of range");
+    c10::DeviceGuard g(x.device());
+    auto out = at::empty({nparts}, x.options().dtype(at::kLong));
+    hq_fingerprint(ptr<float>(x), x.numel(), (int)nparts, reinterpret_cast<uint64_t*>(out.data_ptr<int64_t>()),
+                   cur_stream());
+    return out;
   });
   m.def("adamw", &adamw);
   m.def("adamod", &adamod);

@@ -21,7 +21,7 @@ from typing import List
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 BUILD = os.path.join(HERE, "build")
-DEBUG_DIR = os.path.join(BUILD, "debug")
+DEBUG_DIR = os.path.join(PKG, "_debug")   # HQ_KERNELS_DEBUG=1 loads it (_native); in-tree so it reaches the GPU box
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
@@ -67,18 +67,34 @@ def _torch_paths():
     return incs, libdir
 
 
-def build_kernels(jobs: int = 8, force: bool = False, verbose: bool = True, debug: bool = False) -> str:
+_PROD_PKG = PKG
+
+
+def build_kernels(jobs: int = 8, force: bool = False, verbose: bool = True, debug: bool = False,
+                  lab_defines: List[str] = ()) -> str:
     """Release build → ``<pkg>/_hq_kernels<ext>``.  ``debug=True`` adds ``-DHQ_DEBUG`` (device-side
-    ``HQ_DASSERT`` bounds checks, host line info) and writes ``csrc/build/debug/_hq_kernels<ext>``,
-    which ``_native`` loads instead when ``HQ_KERNELS_DEBUG=1``."""
+    ``HQ_DASSERT`` bounds checks, host line info) and writes ``<pkg>/_debug/_hq_kernels<ext>``,
+    which ``_native`` loads instead when ``HQ_KERNELS_DEBUG=1``.
+
+    ``lab_defines`` (``-D...``; tools/build_ab_lib.py only) are lab switches such as ``HQ_EPI_DIAG`` whose builds
+    give WRONG results by design: they are refused for the production library path, and nothing is read from
+    the environment, so a lab setting left in a shell can never reach the library training loads."""
+    if lab_defines and os.path.realpath(PKG) == os.path.realpath(_PROD_PKG):
+        raise RuntimeError(f"lab defines {list(lab_defines)} refused for the production kernel library {PKG}")
+    if os.environ.get("HQ_KERNEL_CFLAGS"):
+        print("[hq-build] note: HQ_KERNEL_CFLAGS is ignored (pass lab defines to tools/build_ab_lib.py)",
+              file=sys.stderr)
     incs, torch_lib = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-I" + os.path.join(HERE, "include"),
               "-D__HIP_PLATFORM_AMD__=1", "-Wno-unused-result"]
     if debug:
         common += ["-DHQ_DEBUG=1", "-g1"]
-    # lab / A-B builds only (tools/build_ab_lib.py): extra defines for the kernel sources, e.g. -DHQ_EPI_DIAG=1
-    common += [f for f in os.environ.get("HQ_KERNEL_CFLAGS", "").split() if f.startswith("-D")]
+    # lab / A-B builds only (tools/build_ab_lib.py, output outside the package): e.g. -DHQ_EPI_DIAG=1
+    bad = [f for f in lab_defines if not f.startswith("-D")]
+    if bad:
+        raise ValueError(f"lab_defines must be -D flags: {bad}")
+    common += list(lab_defines)
     kernel_srcs = sorted(os.path.join(HERE, "kernels", f) for f in os.listdir(os.path.join(HERE, "kernels"))
                          if f.endswith(".hip"))
     runtime_srcs = sorted(os.path.join(HERE, "runtime", f) for f in os.listdir(os.path.join(HERE, "runtime"))
@@ -156,7 +172,7 @@ def main(argv=None):
     ap.add_argument("--kernels", action="store_true")
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 1))
     ap.add_argument("--force", action="store_true")
-    ap.add_argument("--debug", action="store_true", help="kernels with HQ_DASSERT checks into csrc/build/debug/")
+    ap.add_argument("--debug", action="store_true", help="kernels with HQ_DASSERT checks into <pkg>/_debug/")
     a = ap.parse_args(argv)
     both = not a.host and not a.kernels
     if a.host or both:

@@ -210,7 +210,7 @@ constexpr float kHqBf8Max = 57344.f;    // OCP e5m2 (backward activation gradien
 // (kHqGdLo, kHqGdStep: hq_kernels.h, shared with the host bindings)
 __device__ __forceinline__ uint2 hq_gd_encode8(const float* g) {
   // q = (g − lo)/step as one FMA, then v_cvt_pk_u8_f32 (round to nearest, saturate to 0…255) packs it into its byte
-  constexpr float inv = 255.f / 1.2578125f, off = -kHqGdLo * inv;
+  constexpr float inv = kHqGdInv, off = kHqGdOff;
   uint32_t w[2] = {0u, 0u};
 #pragma unroll
   for (int e = 0; e < 8; ++e) w[e >> 2] = __builtin_amdgcn_cvt_pk_u8_f32(fmaf(g[e], inv, off), e & 3, w[e >> 2]);

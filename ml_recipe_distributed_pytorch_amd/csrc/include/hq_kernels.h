@@ -11,6 +11,9 @@
 // hq_gd_encode8 / hq_gd_decode8): g = kHqGdLo + q·kHqGdStep over gelu''s exact range [−0.12890, 1.12890]
 constexpr float kHqGdLo = -0.12890625f;
 constexpr float kHqGdStep = 1.2578125f / 255.f;
+constexpr float kHqGdInv = 255.f / 1.2578125f;       // encode: q = rne(fma(g, kHqGdInv, kHqGdOff)), clamp 0…255
+constexpr float kHqGdOff = -kHqGdLo * kHqGdInv;
+void hq_gelud_encode8(const uint16_t* g, uint8_t* q, size_t n, hipStream_t s);   // bf16 gelu' -> code (n % 8 == 0)
 
 struct HqOuts {  // up to 4 fp32 column-sum destinations (null = skip), passed by value
   float* p[4];
@@ -42,7 +45,7 @@ void hq_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, 
 // deterministic embedding backward scratch (norm.hip: id sort, word-run carries, position partials)
 struct HqEmbScratch {
   int32_t *keys, *rows, *skeys, *srows;   // [T] each: (id, row) pairs and their id-sorted copies
-  void* sort_tmp;                          // hipcub radix-sort temp storage, sort_bytes
+  void* sort_tmp;                          // radix-sort digit histograms (sort_bytes)
   size_t sort_bytes;
   float* carry;                            // [chunks][2][H]
   float* ppart;                            // [pos_rows][H] (unused when pos_rows == 0)
@@ -52,6 +55,9 @@ struct HqEmbScratchSizes {
   int chunks, pos_rows;
 };
 HqEmbScratchSizes hq_embed_bwd_scratch(int T, int V, int L, int P);
+size_t hq_sort_ids_bytes(int T, int V);
+void hq_sort_ids(const int64_t* ids, int T, int V, int32_t* keys, int32_t* rows, int32_t* skeys, int32_t* srows,
+                 void* hist, size_t hist_bytes, hipStream_t s);
 void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, const int64_t* tids, const uint16_t* ww,
                   const uint16_t* wp, const uint16_t* wt, const float* gamma, const float* mean, const float* rstd,
                   float* g_word, float* g_pos, float* g_type, float* part, HqOuts outs, int T, int H, int n_types,
@@ -60,6 +66,8 @@ void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, c
 // partial-sum rows embed_bwd needs for T tokens laid out as [T / L][L] (L <= 0: one sequence)
 int hq_embed_bwd_partials(int T, int L);
 void hq_gelu_fwd(const uint16_t* pre, uint16_t* out, size_t n, hipStream_t s);
+void hq_ln_guard(const float* master, const int64_t* goff, const int64_t* boff, int n, int H, float ratio, uint8_t* flags,
+                 hipStream_t s);
 void hq_gelu_bwd(const uint16_t* dout, const uint16_t* pre, uint16_t* dpre, float* part, HqOuts outs, int T, int N,
                  bool accumulate, hipStream_t s);
 void hq_bias_grad(const uint16_t* dy, float* part, HqOuts outs, int T, int N, bool accumulate, hipStream_t s);
@@ -92,6 +100,7 @@ struct HqOptGroups {
   float wd[kOptMaxGroups];
 };
 void hq_sq_norm_partials(const float* g, int64_t n, float* partials, int nparts, hipStream_t s);
+void hq_fingerprint(const float* x, int64_t n, int nparts, uint64_t* out, hipStream_t s);
 // Σg² of chunks c0 … c1-1 of the grad arena (chunks: int64 [C][2] = start, numel; numel <= kNormChunk, % 4 == 0)
 constexpr int64_t kNormChunk = 1 << 18;
 void hq_sq_norm_chunks(const float* g, const int64_t* chunks, int c0, int c1, float* partials, hipStream_t s);
@@ -170,7 +179,7 @@ int hq_gemm_fp8_supported(int M, int N, int K);
 void hq_gemm_fp8_set_variant(int v);   // 0 auto (persistent but the Q8 DMUL), 2 = per-tile v2, 3 = persistent
 void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, uint16_t* P, const float* sa,
                  const float* sb, uint8_t* C8, float* q8, int phase, int M, int N, int K, int epi, hipStream_t s,
-                 float* part = nullptr);
+                 float* part = nullptr, int gd8 = 1);
 // delayed-scaling e4m3 quantiser (one pass): y = x / s(prev amax), amax tracked in q8 (see gemm_fp8.hip)
 void hq_fp8_quant_delayed(const uint16_t* x, uint8_t* y, size_t n, float* q8, int phase, hipStream_t s);
 long long hq_fp8_quant_multi_blocks(long long n8);   // blocks of one segment of n8 8-element groups

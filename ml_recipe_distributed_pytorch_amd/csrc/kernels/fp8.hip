@@ -51,7 +51,25 @@ __global__ __launch_bounds__(256) void fp8_quant_kernel(const uint16_t* __restri
 
 int grid_for(size_t n8) { return (int)std::min<size_t>((n8 + 255) / 256, 256 * 8); }
 
+// bf16 gelu' -> the 8-bit code with the very encoder the fp8 FFN1 epilogue uses (hq_gd_encode8): for a bf16 gelu'
+// that must meet the fp8 FFN2 dgrad (ops.gelud_encode)
+__global__ __launch_bounds__(256) void gelud_encode8_kernel(const uint4* __restrict__ g, uint2* __restrict__ q, size_t n8) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float f[8];
+    hq_unpack8(g[i], f);
+    q[i] = hq_gd_encode8(f);
+  }
+}
+
 }  // namespace
+
+void hq_gelud_encode8(const uint16_t* g, uint8_t* q, size_t n, hipStream_t s) {
+  const size_t n8 = n / 8;
+  const int grid = std::max(1, (int)std::min<size_t>((n8 + 255) / 256, 4096));
+  hipLaunchKernelGGL(gelud_encode8_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<const uint4*>(g),
+                     reinterpret_cast<uint2*>(q), n8);
+}
 
 void hq_amax_bf16(const uint16_t* x, size_t n, unsigned* amax, hipStream_t s) {
   (void)hipMemsetAsync(amax, 0, sizeof(unsigned), s);

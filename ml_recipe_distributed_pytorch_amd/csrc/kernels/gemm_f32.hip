@@ -142,8 +142,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(F32Args a) {
 
   // C/D map of the 32×32 MFMA: col = lane & 31, row = (r & 3) + 8·(r >> 2) + 4·(lane >> 5)
   const int col_l = lane & 31, row_h = 4 * (lane >> 5);
+  HQ_DASSERT(split < a.ksplit && m0 < a.M && n0 < a.N);
   if (a.ksplit > 1) {
-    float* slab = a.ws + (long long)split * a.M * a.N;
+    HQ_DASSERT(a.ws != nullptr);
+    float* slab = a.ws + (long long)split * a.M * a.N;   // slab `split` of the [ksplit][M][N] workspace
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -153,7 +155,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(F32Args a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int gi = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + row_h;
-          if (gi < a.M) slab[(long long)gi * a.N + gj] = acc[i][j][r];
+          if (gi < a.M) {
+            HQ_DASSERT(gj < a.N);
+            slab[(long long)gi * a.N + gj] = acc[i][j][r];
+          }
         }
       }
     return;
@@ -172,6 +177,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(F32Args a) {
         const int gi = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + row_h;
         if (gi >= a.M) continue;
         float v = a.alpha * acc[i][j][r] + bj;
+        HQ_DASSERT(gj < a.N && gj < a.ldc && (R == nullptr || gj < a.ldr));
         if (R) v += R[(long long)gi * a.ldr + gj];
         C[(long long)gi * a.ldc + gj] = v;
       }

@@ -99,7 +99,7 @@ __device__ __forceinline__ uint4 load_aux(const uint16_t* __restrict__ P, size_t
   }
 }
 
-template <int EPI, bool Q8, bool WC>
+template <int EPI, bool Q8, bool WC, bool GD8>
 __device__ __forceinline__ void epi_piece(uint4 piece, const uint4& aux, size_t goff, uint16_t* __restrict__ C,
                                           uint16_t* __restrict__ P, uint8_t* __restrict__ C8, float inv8, float& amax,
                                           float (&csum)[8]) {
@@ -131,7 +131,8 @@ __device__ __forceinline__ void epi_piece(uint4 piece, const uint4& aux, size_t 
     float x[8], g[8];
     hq_unpack8(piece, x);
     hq_gelu_grad8(x, g);   // g = gelu'(x), x = gelu(x)
-    if constexpr (Q8) *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(P) + goff) = hq_gd_encode8(g);
+    // GD8: the 8-bit gelu' code, only when the fp8 FFN2 dgrad will read it; else gelu' in bf16
+    if constexpr (GD8) *reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(P) + goff) = hq_gd_encode8(g);
     else *reinterpret_cast<uint4*>(P + goff) = hq_pack8(g);
     piece = hq_pack8(x);
     if constexpr (Q8) {
@@ -145,7 +146,7 @@ __device__ __forceinline__ void epi_piece(uint4 piece, const uint4& aux, size_t 
   if constexpr (WC) *reinterpret_cast<uint4*>(C + goff) = piece;
 }
 
-template <int EPI, bool Q8, bool WC>
+template <int EPI, bool Q8, bool WC, bool GD8>
 __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                                uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                                uint16_t* __restrict__ P, const float* __restrict__ sa,
@@ -303,7 +304,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
   auto piece_out = [&](int it) {
     const int lr = it * ROWS_PER_IT + rsub;
     const uint4 piece = *reinterpret_cast<const uint4*>(wreg + lr * RS + seg * 16);
-    epi_piece<EPI, Q8, WC>(piece, aux[kAux ? it : 0], (size_t)grow_of(it) * ldc + gcol, C, P, C8, inv8, amax, csum);
+    epi_piece<EPI, Q8, WC, GD8>(piece, aux[kAux ? it : 0], (size_t)grow_of(it) * ldc + gcol, C, P, C8, inv8, amax, csum);
   };
   if constexpr (kAux) {   // fully unrolled: aux[] must stay in registers
 #pragma unroll
@@ -348,7 +349,7 @@ struct P8Epi {   // vm ops per lane per tile: C (WC), P (GELUD), C8 (Q8) stores,
   static_assert(6 + E <= 63, "vmcnt field");
 };
 
-template <int EPI, bool Q8, bool WC>
+template <int EPI, bool Q8, bool WC, bool GD8>
 __global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* __restrict__ A, const uint8_t* __restrict__ B,
                                                                 uint16_t* __restrict__ C, const float* __restrict__ bias,
                                                                 uint16_t* __restrict__ P, const float* __restrict__ sa,
@@ -543,7 +544,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* _
         for (int it = 0; it < AB; ++it) {
           const int lr = (h + it) * ROWS_PER_IT + rsub;
           const uint4 piece = *reinterpret_cast<const uint4*>(wreg + lr * RS + seg * 16);
-          epi_piece<EPI, Q8, WC>(piece, aux[kAux ? it : 0], goff_of(h + it), C, P, C8, inv8, amax, csum);
+          epi_piece<EPI, Q8, WC, GD8>(piece, aux[kAux ? it : 0], goff_of(h + it), C, P, C8, inv8, amax, csum);
         }
       }
     }
@@ -589,7 +590,7 @@ constexpr size_t lds_bytes() {
 // profiles/r3_fp8_bwd).
 int g_fp8_variant = 0;
 
-template <int EPI, bool Q8, bool WC = true>
+template <int EPI, bool Q8, bool WC = true, bool GD8 = Q8>
 void launch(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, uint16_t* P, const float* sa,
             const float* sb, uint8_t* C8, float* q8, float* part, int phase, int M, int N, int K, hipStream_t s) {
   const bool persist = g_fp8_variant == 3 || (g_fp8_variant == 0 && !(EPI == HQ_EPI_DMUL && Q8));
@@ -599,26 +600,26 @@ void launch(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, 
       int dev = 0, n = 0;
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-      (void)hipFuncSetAttribute((const void*)gemm_fp8p_kernel<EPI, Q8, WC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      (void)hipFuncSetAttribute((const void*)gemm_fp8p_kernel<EPI, Q8, WC, GD8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       return n > 0 ? n : 256;
     }();
     const int tiles = (M / BM) * (N / BN);
     const int nwg = std::min(tiles, ncu);   // every workgroup has at least one tile
     float* part8 = Q8 ? hq_fp8_amax_parts((size_t)nwg * (kThreads / 64)) : nullptr;
-    hipLaunchKernelGGL((gemm_fp8p_kernel<EPI, Q8, WC>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, sa, sb, C8, q8,
+    hipLaunchKernelGGL((gemm_fp8p_kernel<EPI, Q8, WC, GD8>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, sa, sb, C8, q8,
                        part8, part, phase, M, N, K);
     if (Q8) hq_fp8_amax_fold(part8, nwg * (kThreads / 64), q8, phase, s, EPI == HQ_EPI_DMUL ? kHqBf8Max : kHqFp8Max);
     return;
   }
   constexpr size_t lds = lds_bytes();
   static bool init = [] {
-    (void)hipFuncSetAttribute((const void*)gemm_fp8_kernel<EPI, Q8, WC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm_fp8_kernel<EPI, Q8, WC, GD8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     return true;
   }();
   (void)init;
   const int grid = (M / BM) * (N / BN);
   float* part8 = Q8 ? hq_fp8_amax_parts((size_t)grid * (kThreads / 64)) : nullptr;
-  hipLaunchKernelGGL((gemm_fp8_kernel<EPI, Q8, WC>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, sa, sb,
+  hipLaunchKernelGGL((gemm_fp8_kernel<EPI, Q8, WC, GD8>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, sa, sb,
                      C8, q8, part8, part, phase, M, N, K, K, K, N);
   if (Q8) hq_fp8_amax_fold(part8, grid * (kThreads / 64), q8, phase, s, EPI == HQ_EPI_DMUL ? kHqBf8Max : kHqFp8Max);
 }
@@ -783,10 +784,12 @@ int hq_gemm_fp8_supported(int M, int N, int K) {
 
 void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, uint16_t* P, const float* sa,
                  const float* sb, uint8_t* C8, float* q8, int phase, int M, int N, int K, int epi, hipStream_t s,
-                 float* part) {
+                 float* part, int gd8) {
   switch (epi) {
     case HQ_EPI_GELUD:
-      if (C8 && C) launch<HQ_EPI_GELUD, true>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
+      // gd8 = 0: gelu' in bf16 beside the e4m3 act (the FFN2 dgrad runs in bf16 and would otherwise decode the code)
+      if (C8 && C && !gd8) launch<HQ_EPI_GELUD, true, true, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
+      else if (C8 && C) launch<HQ_EPI_GELUD, true>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
       else if (C8) launch<HQ_EPI_GELUD, true, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
       else launch<HQ_EPI_GELUD, false>(A, B, C, bias, P, sa, sb, C8, q8, part, phase, M, N, K, s);
       break;

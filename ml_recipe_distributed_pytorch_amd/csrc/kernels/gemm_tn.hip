@@ -430,6 +430,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_tn2_kernel(const uint16_t* _
     for (int J = 0; J < 4; ++J) {
       if (!k_full && (J >> 1) == 1) continue;
       const int col = k0 + (J >> 1) * 128 + wn * 32 + (J & 1) * 16 + fq * 4;
+      HQ_DASSERT(split < S && row < N && col + 4 <= K);
       *reinterpret_cast<float4*>(out + (size_t)row * K + col) = make_float4(acc[I][J][0], acc[I][J][1], acc[I][J][2], acc[I][J][3]);
     }
   }

@@ -12,7 +12,6 @@
 // vector access), NCH = ceil(H/256) chunks.  Column partial sums are reduced per block through
 // LDS and finished by hq_colsum (one 1024-thread block per 64 columns), so every gradient is
 // bitwise deterministic (position ids other than 0 … L-1 fall back to float atomics for the position rows).
-#include <hipcub/hipcub.hpp>
 
 #include "hq_common.h"
 #include "hq_kernels.h"
@@ -444,8 +443,8 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
 }
 
 // Deterministic embedding backward (no float atomics at the default position ids):
-//   1. sort: the token rows by word id (hipcub radix sort of (id, row) pairs — stable, so each id's rows stay
-//      in token order);
+//   1. sort: the token rows by word id (hq_sort_ids: own LSD radix sort of (id, row) pairs — stable, so each
+//      id's rows stay in token order);
 //   2. embed_bwd_kernel (position-major): recompute x̂ and the LayerNorm backward per row; γ / β / type
 //      gradients as per-block partials, the position gradient summed per wave over its kEmbNB batch rows and
 //      stored as that wave's partial row [blockIdx.y][l] (folded by colsum in a fixed order);
@@ -585,6 +584,9 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
   // this wave's position-partial row [blockIdx.y][l] (l < PL = min(L, P): pid == l needs l < P; ppart = null:
   // every position flush is atomic)
   float* prow = (ppart != nullptr && l < PL) ? ppart + ((size_t)blockIdx.y * PL + l) * H : nullptr;
+  // the partial rows are [ceil(B / kEmbNB)][PL][H] with PL = min(L, P): row l exists only for l < PL (77ab202: the
+  // flat layout, L = T > P, once wrote rows past the buffer)
+  HQ_DASSERT(prow == nullptr || (l < PL && PL <= P && (int)blockIdx.y < (B + kEmbNB - 1) / kEmbNB));
   bool pstored = false;
   int pcur = -1;
   auto flush_pos = [&]() {
@@ -601,6 +603,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
             }
             *reinterpret_cast<float4*>(prow + col) = v;
           } else {
+            HQ_DASSERT(pcur >= 0 && pcur < P);
 #pragma unroll
             for (int i = 0; i < 4; ++i) atomicAdd(g_pos + (size_t)pcur * H + col + i, pacc[c][i]);
           }
@@ -668,11 +671,105 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(
   block_partials<NCH, 4>(acc, lds, part, H);
 }
 
-// (id, row) pairs for the sort: the int64 ids as int32 keys, rows 0 … T-1 as values
-__global__ __launch_bounds__(256) void embed_keys_kernel(const int64_t* __restrict__ ids, int32_t* __restrict__ keys,
-                                                         int32_t* __restrict__ rows, int T) {
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t < T) { keys[t] = (int32_t)ids[t]; rows[t] = t; }
+// ---- own stable LSD radix sort of the (word id, row) pairs: 8-bit digits, ceil(bits / 8) passes -------------
+// Each pass is a stable counting sort over 256 bins in tiles of kSortTile rows:
+//   sort_hist_kernel (first pass only): per-tile digit counts -> hist[digit][tile] (LDS integer atomics);
+//   sort_scan_kernel: one block, exclusive scan of hist in (digit, tile) order -> every tile's start per digit;
+//                     also zeroes the next pass's histogram;
+//   sort_scatter_kernel: each wave ranks its 64-row batches by digit with 8 ballots (the lanes holding the same
+//                     digit, in lane order), batch counts are scanned per digit in LDS, and every row goes to
+//                     tile start + earlier batches + rank — stable, so each id's rows keep token order.  It also
+//                     counts the NEXT pass's digits of the tile each row lands in (integer atomics).
+// Integer counts and fixed ranks: the output is the same permutation every run (no float, no order race).
+constexpr int kSortTile = 1024;   // 256 threads × 4 batches of 64
+
+__global__ __launch_bounds__(256) void sort_hist_kernel(const int64_t* __restrict__ ids, int T, int* __restrict__ hist,
+                                                        int ntiles) {
+  __shared__ int cnt[256];
+  cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const int t0 = blockIdx.x * kSortTile;
+  for (int i = threadIdx.x; i < kSortTile; i += 256)
+    if (t0 + i < T) atomicAdd(&cnt[(int)ids[t0 + i] & 255], 1);
+  __syncthreads();
+  hist[threadIdx.x * ntiles + blockIdx.x] = cnt[threadIdx.x];
+}
+
+__global__ __launch_bounds__(1024) void sort_scan_kernel(int* __restrict__ hist, int n, int* __restrict__ next_hist) {
+  __shared__ int sums[1024];
+  const int per = (n + 1023) / 1024;
+  const int a = min(n, (int)threadIdx.x * per), b = min(n, a + per);
+  int s = 0;
+  for (int i = a; i < b; ++i) s += hist[i];
+  sums[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {   // Hillis-Steele inclusive scan of the 1024 segment sums
+    const int v = threadIdx.x >= (unsigned)off ? sums[threadIdx.x - off] : 0;
+    __syncthreads();
+    sums[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int run = threadIdx.x ? sums[threadIdx.x - 1] : 0;
+  for (int i = a; i < b; ++i) {
+    const int c = hist[i];
+    hist[i] = run;
+    run += c;
+  }
+  if (next_hist)
+    for (int i = threadIdx.x; i < n; i += 1024) next_hist[i] = 0;
+}
+
+__global__ __launch_bounds__(256) void sort_scatter_kernel(const int64_t* __restrict__ ids, const int32_t* __restrict__ kin,
+                                                           const int32_t* __restrict__ vin, int32_t* __restrict__ kout,
+                                                           int32_t* __restrict__ vout, const int* __restrict__ start,
+                                                           int* __restrict__ next_hist, int T, int shift, int ntiles) {
+  __shared__ int bcnt[16][256];   // [batch][digit]: rows of the digit in the batch, then their exclusive prefix
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < 16 * 256; i += 256) (&bcnt[0][0])[i] = 0;
+  __syncthreads();
+  const int t0 = blockIdx.x * kSortTile;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  int key[4], val[4], dig[4], rank[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = wave * 4 + j;            // batch q covers tile rows q·64 … q·64 + 63 (tile order)
+    const int i = t0 + q * 64 + lane;
+    const bool ok = i < T;
+    key[j] = ok ? (kin ? kin[i] : (int)ids[i]) : 0;
+    val[j] = ok ? (vin ? vin[i] : i) : 0;
+    dig[j] = (key[j] >> shift) & 255;
+    uint64_t peers = __ballot(ok);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const bool on = (dig[j] >> bit) & 1;
+      const uint64_t m = __ballot(on);
+      peers &= on ? m : ~m;
+    }
+    rank[j] = __popcll(peers & lt);
+    if (ok && rank[j] == 0) bcnt[q][dig[j]] = __popcll(peers);   // the digit's first lane writes the batch count
+    if (!ok) rank[j] = -1;
+  }
+  __syncthreads();
+  {   // per digit (one per thread): exclusive prefix over the 16 batches, in batch order
+    int run = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int c = bcnt[q][tid];
+      bcnt[q][tid] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (rank[j] < 0) continue;
+    const int q = wave * 4 + j;
+    const int pos = start[dig[j] * ntiles + blockIdx.x] + bcnt[q][dig[j]] + rank[j];
+    HQ_DASSERT(pos >= 0 && pos < T);
+    kout[pos] = key[j];
+    vout[pos] = val[j];
+    if (next_hist) atomicAdd(&next_hist[((key[j] >> (shift + 8)) & 255) * ntiles + pos / kSortTile], 1);
+  }
 }
 
 // Word gradients over the id-sorted rows.  Wave c owns sorted positions [c·kEmbCH, …); the run of one id is
@@ -687,7 +784,7 @@ __global__ __launch_bounds__(256) void embed_word_kernel(
     const uint16_t* __restrict__ ww, const uint16_t* __restrict__ wp, const uint16_t* __restrict__ wt,
     const float* __restrict__ gamma, const float* __restrict__ mean, const float* __restrict__ rstd,
     float* __restrict__ g_word, float* __restrict__ carry, int T, int H, int pad_word, int accumulate, HqDropKey kd_,
-    uint32_t thr, float kscale) {
+    uint32_t thr, float kscale, int V) {
   const uint32_t key = kd_.get();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int c = blockIdx.x * kWaves + wave;
@@ -705,6 +802,8 @@ __global__ __launch_bounds__(256) void embed_word_kernel(
   const int after = j1 < T ? __builtin_amdgcn_readfirstlane(skeys[j1]) : -1;
   auto flush = [&](int id, int kind) {   // kind 0: carry slot 0, 1: carry slot 1, 2: the gradient row
     if (id != pad_word) {
+      // a gradient row of a real id, or carry slot (c, kind) of the [chunks][2][H] carry buffer
+      HQ_DASSERT(kind == 2 ? (id >= 0 && id < V) : (kind >= 0 && kind < 2 && c * kEmbCH < T));
       float* dst = kind == 2 ? g_word + (size_t)id * H : carry + ((size_t)c * 2 + kind) * H;
 #pragma unroll
       for (int q = 0; q < NCH; ++q) {
@@ -738,6 +837,7 @@ __global__ __launch_bounds__(256) void embed_word_kernel(
     if (j + 1 < j1)
       emb_load_k<NCH>(nxt, meta, j + 1 - j0, (size_t)__builtin_amdgcn_readlane(myrow, j + 1 - j0), dy, ww, wp, wt, H, lane);
     const int id = (int)cur.id;
+    HQ_DASSERT(id >= 0 && id < V && row < (size_t)T);
     if (id != seg) {
       flush(seg, seg_first && head_cont ? 0 : 2);
       seg = id;
@@ -759,7 +859,7 @@ __global__ __launch_bounds__(256) void embed_word_kernel(
 template <int NCH>
 __global__ __launch_bounds__(256) void embed_carry_kernel(const int32_t* __restrict__ skeys, const float* __restrict__ carry,
                                                           float* __restrict__ g_word, int T, int H, int pad_word,
-                                                          int accumulate) {
+                                                          int accumulate, int V) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int c = blockIdx.x * kWaves + wave;
   const int j0 = c * kEmbCH;
@@ -780,6 +880,7 @@ __global__ __launch_bounds__(256) void embed_carry_kernel(const int32_t* __restr
     hi = min(hi, lo + step);
   }
   const int ce = (hi - 1) / kEmbCH;   // the last chunk holding rows of the run: pieces of chunks c+1 … ce
+  HQ_DASSERT(last >= 0 && last < V && hi <= T && ce * kEmbCH < T && ce > c);
   float acc[NCH][4];
 #pragma unroll
   for (int q = 0; q < NCH; ++q) {
@@ -1045,17 +1146,42 @@ void hq_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, 
   });
 }
 
-static void emb_sort_check(hipError_t e) {
-  if (e != hipSuccess) { fprintf(stderr, "hq_embed_bwd: id sort failed: %s\n", hipGetErrorString(e)); abort(); }
-}
 static int emb_sort_bits(int V) { return V > 1 ? 32 - __builtin_clz((unsigned)(V - 1)) : 1; }
+static int emb_sort_passes(int V) { return (emb_sort_bits(V) + 7) / 8; }
+static int emb_sort_tiles(int T) { return (T + kSortTile - 1) / kSortTile; }
+
+size_t hq_sort_ids_bytes(int T, int V) { return (size_t)emb_sort_passes(V) * 256 * emb_sort_tiles(T) * sizeof(int); }
+
+// Stable sort of (ids[t], t) by id (sort_*_kernel): sorted ids -> skeys, their rows -> srows; keys / rows are the
+// ping-pong buffers of the odd passes (all [T]); hist: hq_sort_ids_bytes(T, V) bytes.  Passes alternate so that
+// the last one lands in (skeys, srows).
+void hq_sort_ids(const int64_t* ids, int T, int V, int32_t* keys, int32_t* rows, int32_t* skeys, int32_t* srows,
+                 void* hist_buf, size_t hist_bytes, hipStream_t s) {
+  const int np = emb_sort_passes(V), nt = emb_sort_tiles(T);
+  if (T <= 0) return;
+  if (hist_bytes < hq_sort_ids_bytes(T, V)) {
+    fprintf(stderr, "hq_sort_ids: histogram scratch too small (%zu < %zu)\n", hist_bytes, hq_sort_ids_bytes(T, V));
+    abort();
+  }
+  int* hist = reinterpret_cast<int*>(hist_buf);
+  hipLaunchKernelGGL(sort_hist_kernel, dim3(nt), dim3(256), 0, s, ids, T, hist, nt);
+  const int32_t *kin = nullptr, *vin = nullptr;
+  for (int p = 0; p < np; ++p) {
+    int* h = hist + (size_t)p * 256 * nt;
+    int* hn = p + 1 < np ? h + 256 * nt : nullptr;
+    const bool to_final = (np - 1 - p) % 2 == 0;
+    int32_t* kout = to_final ? skeys : keys;
+    int32_t* vout = to_final ? srows : rows;
+    hipLaunchKernelGGL(sort_scan_kernel, dim3(1), dim3(1024), 0, s, h, 256 * nt, hn);
+    hipLaunchKernelGGL(sort_scatter_kernel, dim3(nt), dim3(256), 0, s, ids, kin, vin, kout, vout, h, hn, T, 8 * p, nt);
+    kin = kout;
+    vin = vout;
+  }
+}
 
 HqEmbScratchSizes hq_embed_bwd_scratch(int T, int V, int L, int P) {
   HqEmbScratchSizes z{};
-  size_t bytes = 0;
-  emb_sort_check(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
-                                                    (const int32_t*)nullptr, (int32_t*)nullptr, T, 0, emb_sort_bits(V)));
-  z.sort_bytes = bytes;
+  z.sort_bytes = hq_sort_ids_bytes(T, V);   // one [256][tiles] digit histogram per radix pass
   z.chunks = (T + kEmbCH - 1) / kEmbCH;
   if (L <= 0 || T % L) L = T;
   // partial rows exist for the positions l < min(L, P) only: a row whose pid == l needs l < P
@@ -1078,11 +1204,8 @@ void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, c
   const HqEmbScratchSizes z = hq_embed_bwd_scratch(T, V, L, P);
   const int PL = std::min(L, P);   // position-partial rows per batch slice
   float* ppart = z.pos_rows > 0 ? sc.ppart : nullptr;
-  // (id, row) sort: stable, so every id's rows stay in token order
-  hipLaunchKernelGGL(embed_keys_kernel, dim3((T + 255) / 256), dim3(256), 0, s, ids, sc.keys, sc.rows, T);
-  size_t bytes = sc.sort_bytes;
-  emb_sort_check(hipcub::DeviceRadixSort::SortPairs(sc.sort_tmp, bytes, sc.keys, sc.skeys, sc.rows, sc.srows, T, 0,
-                                                    emb_sort_bits(V), s));
+  // (id, row) sort: the own stable radix sort, so every id's rows stay in token order
+  hq_sort_ids(ids, T, V, sc.keys, sc.rows, sc.skeys, sc.srows, sc.sort_tmp, sc.sort_bytes, s);
   const int nwb = (z.chunks + kWaves - 1) / kWaves;
   dispatch_nch(H, [&](auto nch) {
     constexpr int C = decltype(nch)::value;
@@ -1090,15 +1213,37 @@ void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, c
                        gamma, mean, rstd, g_pos, g_type, ppart, part, T, H, n_types, pad_pos, key, thr, ks, V, P, B, L,
                        PL);
     hipLaunchKernelGGL(embed_word_kernel<C>, dim3(nwb), dim3(256), 0, s, sc.skeys, sc.srows, dy, ids, pids, tids, ww,
-                       wp, wt, gamma, mean, rstd, g_word, sc.carry, T, H, pad_word, accumulate ? 1 : 0, key, thr, ks);
+                       wp, wt, gamma, mean, rstd, g_word, sc.carry, T, H, pad_word, accumulate ? 1 : 0, key, thr, ks, V);
     hipLaunchKernelGGL(embed_carry_kernel<C>, dim3(nwb), dim3(256), 0, s, sc.skeys, sc.carry, g_word, T, H, pad_word,
-                       accumulate ? 1 : 0);
+                       accumulate ? 1 : 0, V);
   });
   // outs: gamma, beta, type0, type1 (type rows only when n_types <= 2)
   colsum(part, nb, 4 * H, outs, H, accumulate, s);
   // position partials [B / kEmbNB][min(L, P)][H] -> rows 0 … min(L, P)-1 of g_pos, on top of its zeroed (or
   // accumulated) rows and the atomic flushes of non-default position ids
   if (ppart) colsum(ppart, (B + kEmbNB - 1) / kEmbNB, PL * H, HqOuts{{g_pos, nullptr, nullptr, nullptr}}, PL * H, true, s);
+}
+
+// LayerNorm-from-y guard (models/bert.py _ln_flags): LayerNorm i may recompute x̂ from its bf16 output iff every
+// column has γ != 0 and |β| <= ratio·|γ|.  One block per LayerNorm over the fp32 master arena (γ at goff[i], β at
+// boff[i]); flags[i] = 1 / 0.  Replaces a stack / abs / compare / and / all chain of ATen kernels.
+__global__ __launch_bounds__(256) void ln_guard_kernel(const float* __restrict__ master, const int64_t* __restrict__ goff,
+                                                       const int64_t* __restrict__ boff, int H, float ratio,
+                                                       uint8_t* __restrict__ flags) {
+  const float* g = master + goff[blockIdx.x];
+  const float* b = master + boff[blockIdx.x];
+  int bad = 0;
+  for (int c = threadIdx.x; c < H; c += 256) {
+    const float ag = fabsf(g[c]), ab = fabsf(b[c]);
+    bad |= !(ag > 0.f && ab <= ratio * ag);
+  }
+  bad = __syncthreads_or(bad);
+  if (threadIdx.x == 0) flags[blockIdx.x] = bad ? 0 : 1;
+}
+
+void hq_ln_guard(const float* master, const int64_t* goff, const int64_t* boff, int n, int H, float ratio, uint8_t* flags,
+                 hipStream_t s) {
+  if (n > 0) hipLaunchKernelGGL(ln_guard_kernel, dim3(n), dim3(256), 0, s, master, goff, boff, H, ratio, flags);
 }
 
 void hq_gelu_fwd(const uint16_t* pre, uint16_t* out, size_t n, hipStream_t s) {

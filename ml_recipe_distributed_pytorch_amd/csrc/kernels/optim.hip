@@ -219,9 +219,35 @@ __global__ __launch_bounds__(256) void cast_bf16_f32_kernel(const uint16_t* __re
     for (int64_t i = n4 * 4 + threadIdx.x; i < n; i += blockDim.x) dst[i] = hq_bf2f(src[i]) * scale;
 }
 
+// Exact replica fingerprint of an fp32 arena: part p covers [p·n/P, (p+1)·n/P) and holds
+//   Σ_i bits(x_i) · (2i + 1)   (mod 2^64, i = global element index)
+// — integer wrap-around adds are associative, so the value does not depend on the summation order and equals the
+// host-side numpy fingerprint (parallel/reducer.py) bit for bit.  Any flipped bit, sign, or swapped pair of words
+// changes it.  Used after the timed region only (bench / trainer cross-rank weight equality check).
+__global__ __launch_bounds__(256) void fingerprint_kernel(const uint32_t* __restrict__ x, int64_t n, int nparts,
+                                                          uint64_t* __restrict__ out) {
+  __shared__ uint64_t red[256];
+  const int64_t lo = n * blockIdx.x / nparts, hi = n * (blockIdx.x + 1) / nparts;
+  HQ_DASSERT(lo <= hi && hi <= n);
+  uint64_t s = 0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += 256) s += (uint64_t)x[i] * (2ull * (uint64_t)i + 1ull);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[blockIdx.x] = red[0];
+}
+
 int grid_for(int64_t n4) { return (int)std::max<int64_t>(1, std::min<int64_t>((n4 + 255) / 256, 2048)); }
 
 }  // namespace
+
+void hq_fingerprint(const float* x, int64_t n, int nparts, uint64_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(fingerprint_kernel, dim3(nparts), dim3(256), 0, s, reinterpret_cast<const uint32_t*>(x), n, nparts,
+                     out);
+}
 
 void hq_sq_norm_partials(const float* g, int64_t n, float* partials, int nparts, hipStream_t s) {
   hipLaunchKernelGGL(sq_norm_kernel, dim3(nparts), dim3(256), 0, s, g, n, partials);

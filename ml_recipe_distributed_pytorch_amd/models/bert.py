@@ -601,6 +601,21 @@ class BertForQuestionAnswering(nn.Module):
 
     def _ln_flags(self) -> torch.Tensor:
         names = self._ln_names()
+        m = self.store.master
+        if m.is_cuda:   # one own kernel (norm.hip ln_guard_kernel) over the master arena, no ATen chain
+            offs = getattr(self, "_ln_guard_offs", None)
+            if offs is None or offs[0].device != m.device:
+                H = self.config.hidden_size
+                def off(n):
+                    v = self.store.view(n, "master")
+                    o = (v.data_ptr() - m.data_ptr()) // m.element_size()
+                    assert v.is_contiguous() and v.numel() == H and 0 <= o and o + H <= m.numel(), n
+                    return o
+                offs = self._ln_guard_offs = (
+                    torch.tensor([off(n + ".weight") for n in names], dtype=torch.int64, device=m.device),
+                    torch.tensor([off(n + ".bias") for n in names], dtype=torch.int64, device=m.device))
+            from .._native import kernels
+            return kernels().ln_guard(m, offs[0], offs[1], self.config.hidden_size, self.LN_FROM_Y_MAX_RATIO)
         g = torch.stack([self.store.view(n + ".weight", "master") for n in names]).abs()
         b = torch.stack([self.store.view(n + ".bias", "master") for n in names]).abs()
         return ((g > 0) & (b <= self.LN_FROM_Y_MAX_RATIO * g)).all(1)
@@ -614,17 +629,17 @@ class BertForQuestionAnswering(nn.Module):
         return changed
 
     def poll_ln_modes(self) -> bool:
-        """Asynchronous form of ``refresh_ln_modes`` for the training loop (no host sync, ever): applies the
-        flags of the check launched at the previous call if its copy has landed, then launches the next check
-        (a few tiny kernels + a non-blocking copy into pinned memory behind an event) on the current stream.
-        A γ / β update that leaves the guard's region is picked up one to two optimizer steps later.
-        Returns True when a LayerNorm changed mode."""
+        """Asynchronous form of ``refresh_ln_modes`` for the training loop: applies the flags of the check launched
+        at the previous call, then launches the next check (a few tiny kernels + a non-blocking copy into pinned
+        memory behind an event) on the current stream.  The previous check was launched ``ln_check_every`` optimizer
+        steps ago, so waiting for its event costs nothing in practice — and waiting (rather than polling) makes
+        every data-parallel rank apply a mode change at the SAME optimizer step, so replicas stay bitwise
+        reproducible and release / recapture their graphs together.  Returns True when a LayerNorm changed mode."""
         changed = False
         pend = getattr(self, "_ln_pending", None)
         if pend is not None:
             host, ev = pend
-            if not ev.query():
-                return False          # still in flight: keep it, launch nothing new
+            ev.synchronize()
             changed = self._apply_ln_flags(host.tolist())
         flags = self._ln_flags()
         host = torch.empty(flags.shape, dtype=torch.bool, pin_memory=True)

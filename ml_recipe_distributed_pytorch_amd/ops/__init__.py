@@ -276,11 +276,16 @@ def gelud_code():
 
 
 def gelud_encode(g: torch.Tensor) -> torch.Tensor:
-    """gelu' → the 8-bit code, as the fp8 FFN1 epilogue writes it (hq_gd_encode8: fp32 g·(1/step) − lo/step, round
-    to nearest, clamp 0…255)."""
-    lo, step = gelud_code()
-    inv = torch.tensor(255.0 / 1.2578125, dtype=torch.float32)
-    q = torch.round(g.float() * inv.to(g.device) - inv.to(g.device) * lo)
+    """gelu' → the 8-bit code, as the fp8 FFN1 epilogue writes it (hq_gd_encode8: ONE fp32 fma g·inv + off with
+    inv = 1/step, off = −lo/step, round to nearest even, clamp 0…255).  On the GPU this is the device encoder
+    itself (``gelud_encode8`` kernel), so both paths write identical bytes; the host form mirrors it with the
+    constants taken from ``gelud_code()``."""
+    if g.is_cuda:
+        return _k().gelud_encode8(g.to(torch.bfloat16).contiguous())
+    inv, off = _k().gelud_code_enc()
+    inv = torch.tensor(inv, dtype=torch.float32)
+    off = torch.tensor(off, dtype=torch.float32)
+    q = torch.round(torch.addcmul(off.expand(g.shape), g.float(), inv.expand(g.shape)))
     return q.clamp_(0, 255).to(torch.uint8)
 
 
@@ -291,18 +296,19 @@ def gelud_decode(q: torch.Tensor, dtype=torch.bfloat16) -> torch.Tensor:
 
 def linear_gelu_fwd_fp8(x, w8s, b32, in_state: Fp8DelayedState, out_state: Fp8DelayedState, x8=None,
                         need_act: bool = True):
-    """FFN1 in fp8 on the own block-scaled MFMA kernel (gemm_fp8.hip): returns (gelu'(pre) as the 8-bit code of
-    ``gelud_code()``, act, act8) — act in bf16 (for a bf16 FFN2 weight gradient; ``need_act=False`` skips it and
-    returns None when the fp8 weight gradient will read act8) and in e4m3 under ``out_state``'s delayed scale for
-    the FFN2 fp8 GEMM; None when the shape does not tile (caller falls back).  ``x8``: the input already in e4m3
-    under ``in_state`` (LN forward's fp8 output), else it is quantised here."""
+    """FFN1 in fp8 on the own block-scaled MFMA kernel (gemm_fp8.hip): returns (gelu'(pre), act, act8) — act in
+    bf16 and in e4m3 under ``out_state``'s delayed scale for the FFN2 fp8 GEMM; None when the shape does not tile
+    (caller falls back).  ``need_act=False`` (the caller knows the backward will run the FFN2 dgrad and weight
+    gradient in fp8) skips the bf16 act (returned as None) and stores gelu' as the 8-bit code of ``gelud_code()``
+    that the fp8 dgrad reads; otherwise gelu' is stored in bf16 for the bf16 dgrad (no code, no decode error).
+    ``x8``: the input already in e4m3 under ``in_state`` (LN forward's fp8 output), else it is quantised here."""
     M, K, N = x.shape[0], x.shape[1], w8s[0].shape[0]
     if not _k().gemm_fp8_supported(M, N, K):
         return None
     if x8 is None:
         x8 = in_state.quantize(x)
     w8, sw = w8s
-    gd = torch.empty(M, N, dtype=torch.uint8, device=x.device)
+    gd = torch.empty(M, N, dtype=torch.bfloat16 if need_act else torch.uint8, device=x.device)
     act8 = torch.empty(M, N, dtype=torch.float8_e4m3fn, device=x.device)
     act = _k().gemm_fp8(x8, w8, _EPI_GELUD, b32, in_state.scale, sw.reshape(1).float(), pre=gd, out8=act8,
                         state=out_state.buf, phase=out_state.next_phase(), write_out=bool(need_act))
@@ -386,7 +392,7 @@ def linear_dgrad_gelu_d(dy, w, saved, is_deriv, g_bias, accumulate, wt=None):
     M, N = dy.shape[0], w.shape[1]
     assert wt is not None, "stored-derivative GELU backward needs the Wᵀ working copy"
     _check_nt(M, N, dy.shape[1], "linear_dgrad_gelu_d")
-    if saved.dtype == torch.uint8:   # the fp8 forward's gelu' code, while the fp8 dgrad is still uncalibrated
+    if saved.dtype == torch.uint8:   # the fp8 forward's gelu' code (written only when the fp8 dgrad was expected)
         saved = gelud_decode(saved)
     part = _part(M, N, dy.shape[1], dy.device)
     dpre = _k().gemm_nt(dy, wt, _EPI_DMUL, pre=saved, part=part)

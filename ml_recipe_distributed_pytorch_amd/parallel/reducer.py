@@ -50,6 +50,36 @@ logger = logging.getLogger(__name__)
 _uid_counter = itertools.count()
 
 
+def _part_bounds(n: int, parts: int):
+    return [(n * p // parts, n * (p + 1) // parts) for p in range(parts)]
+
+
+def fingerprint(x: torch.Tensor, parts: int = 256) -> torch.Tensor:
+    """Exact fingerprint of an fp32 tensor: ``parts`` int64 words, word p = Σ bits(x_i)·(2i+1) mod 2^64 over the
+    p-th contiguous slice (i = global index).  Integer wrap-around sums do not depend on summation order, so the
+    GPU kernel (``optim.hip`` ``fingerprint_kernel``) and this host path give the same bits; any changed bit,
+    sign or swapped pair of words changes the word of its slice."""
+    x = x.detach().contiguous().view(-1)
+    assert x.dtype == torch.float32
+    if x.is_cuda:
+        return kernels().fingerprint(x, parts)
+    import numpy as np
+    a = x.view(torch.int32).numpy().view(np.uint32)
+    out = np.zeros(parts, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        for p, (lo, hi) in enumerate(_part_bounds(a.size, parts)):
+            i = np.arange(lo, hi, dtype=np.uint64)
+            out[p] = np.sum(a[lo:hi].astype(np.uint64) * (np.uint64(2) * i + np.uint64(1)), dtype=np.uint64)
+    return torch.from_numpy(out.view(np.int64))
+
+
+def sq_partials(x: torch.Tensor, parts: int = 256) -> torch.Tensor:
+    """Σx² per contiguous slice (the same slices as ``fingerprint``), float64 on the host: the magnitude of a
+    replica mismatch (the fingerprint says only whether the bits differ)."""
+    x = x.detach().contiguous().view(-1).double().cpu()
+    return torch.stack([x[lo:hi].square().sum() for lo, hi in _part_bounds(x.numel(), parts)])
+
+
 class Bucket:
     __slots__ = ("index", "start", "end", "groups", "pending", "launched", "work", "dtype")
 
@@ -87,6 +117,11 @@ class GradReducer:
         self.broadcast_done = False
         self.stats = {"buckets_launched": 0, "bytes": 0}
         self._seq_hash = 0       # running hash of the (bucket, numel) launch sequence (SURVEY §5.2 checker)
+        # replica check: with ``snapshot_grads`` set, the engine fingerprints the REDUCED gradient arena of the next
+        # optimizer step (after finalize, before zero_grad) — bench.py sets it for one untimed step after the clock
+        self.snapshot_grads = False
+        self._grad_fp: Optional[torch.Tensor] = None
+        self._grad_sq: Optional[torch.Tensor] = None
         on_gpu = self.store.device.type == "cuda"
         backend = dist.get_backend(group) if dist.is_initialized() else None
         if native is None:
@@ -187,7 +222,10 @@ class GradReducer:
         for g, s, e in self.store.group_ranges():
             if not group_has_trainable.get(g):
                 continue
-            if buckets and (buckets[-1][1] == s) and (e - buckets[-1][0]) * elem <= self.bucket_cap:
+            # emb_bf16: the embeddings group always travels in a bucket of its own, so no other group is ever
+            # all-reduced in bf16 with it, whatever --bucket_cap_mb is
+            alone = self.allreduce_dtype == "emb_bf16" and (g == "embeddings" or (buckets and "embeddings" in buckets[-1][2]))
+            if buckets and not alone and (buckets[-1][1] == s) and (e - buckets[-1][0]) * elem <= self.bucket_cap:
                 bs, _, gs = buckets[-1]
                 buckets[-1] = (bs, e, gs + [g])
             else:
@@ -370,6 +408,60 @@ class GradReducer:
         if len(set(vals)) != 1:
             raise RuntimeError(f"gradient collective sequence diverged across ranks: {vals}")
         return True
+
+    _FP_PARTS = 256
+
+    def take_grad_snapshot(self):
+        """Fingerprint of the reduced gradient arena (called by the engine after ``finalize``, before the optimizer
+        zeroes it, when ``snapshot_grads`` is set)."""
+        g = self.store.grad
+        self._grad_fp = fingerprint(g, self._FP_PARTS)
+        self._grad_sq = sq_partials(g, self._FP_PARTS)
+        self.snapshot_grads = False
+
+    def replica_check(self) -> Dict[str, object]:
+        """Data-parallel correctness self-check (a collective: every rank calls it at the same point): all-gathers an
+        exact fingerprint of the fp32 master arena — and of the last snapshotted reduced gradient — and compares every
+        rank with rank 0.  After a correct DDP step every replica holds bitwise the same weights and gradients; a
+        reducer bug (a wrong bucket offset, a bf16 cast-back race, a missed fence) breaks that even when the step
+        is fast.  Returns the bench/trainer fields; ``ok`` is False on any mismatch or when the RCCL communicator
+        does not span the job."""
+        P = self._FP_PARTS
+        m = self.store.master
+        fm = fingerprint(m, P).cpu()
+        sm = sq_partials(m, P)
+        has_g = self._grad_fp is not None
+        fg = self._grad_fp.cpu() if has_g else torch.zeros(P, dtype=torch.int64)
+        sg = self._grad_sq if has_g else torch.zeros(P, dtype=torch.float64)
+        local = torch.stack([fm, fg, sm.view(torch.int64), sg.view(torch.int64)])   # [4, P] int64 (f64 bits)
+        if dist.is_initialized():
+            dev = self.store.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+            t = local.to(dev)
+            every = [torch.empty_like(t) for _ in range(self.world)]
+            dist.all_gather(every, t, group=self.group)
+            every = [e.cpu() for e in every]
+        else:
+            every = [local]
+        ref = every[0]
+        w_bad = sum(int((e[0] != ref[0]).sum()) for e in every[1:])
+        g_bad = sum(int((e[1] != ref[1]).sum()) for e in every[1:])
+
+        def rel(row):
+            r0 = ref[row].view(torch.float64)
+            den = float(r0.abs().max()) or 1.0
+            return max([float((e[row].view(torch.float64) - r0).abs().max()) / den for e in every[1:]] or [0.0])
+        comm_ok = self._native is None or self.comm_ranks == self.world
+        out = {"weights_equal_across_ranks": w_bad == 0,
+               "grads_equal_across_ranks": (g_bad == 0) if has_g else None,
+               "replica_mismatch_parts": w_bad + g_bad,
+               "max_weight_partial_mismatch": rel(2),
+               "max_grad_partial_mismatch": rel(3) if has_g else None,
+               "rccl_comm_ranks_ok": comm_ok,
+               "replicas_checked": len(every)}
+        out["ok"] = bool(w_bad == 0 and g_bad == 0 and comm_ok)
+        if not out["ok"]:
+            logger.error(f"data-parallel replica check FAILED (rank {self.rank}): {out}")
+        return out
 
     def close(self):
         if self._native is not None:

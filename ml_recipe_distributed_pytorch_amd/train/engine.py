@@ -328,6 +328,8 @@ class TrainEngine:
             torch.cuda.current_stream().wait_stream(side)
         if self.reducer is not None:
             self.reducer.finalize()
+            if self.reducer.snapshot_grads:   # replica check: fingerprint the reduced gradients (untimed steps only)
+                self.reducer.take_grad_snapshot()
         timer.mark("comm_wait")
         parts = self.reducer.norm_partials() if self.reducer is not None else None
         norm, coef = grad_norm_and_clip(self.model.store, self.max_grad_norm, partials=parts)

@@ -268,6 +268,9 @@ class Trainer:
             self.epoch_complete = True
             if self.reducer is not None:
                 self.reducer.verify_sequence()
+                rep = self.reducer.replica_check()   # every replica must hold bitwise rank 0's weights
+                if not rep["ok"]:
+                    raise RuntimeError(f"data-parallel replicas diverged at the end of epoch {epoch_i}: {rep}")
             for func in after_epoch_funcs:
                 func(epoch_i)
 

@@ -93,6 +93,41 @@ def test_gemm_fp8_gelud_delayed_q8(cuda, variant):
 
 
 @pytest.mark.gpu
+def test_gemm_fp8_gelud_bf16_gelu_prime_with_q8(cuda, variant):
+    """The fp8 FFN1 when the FFN2 dgrad will run in bf16: the e4m3 act AND gelu' in bf16 (no 8-bit code, so the
+    bf16 dgrad reads gelu' at bf16 precision) — same act / act8 bytes as the code-writing form."""
+    k = _native.kernels()
+    M, N, K = 512, 768, 256
+    g = torch.Generator(device=cuda).manual_seed(4)
+    A8, sa = _q(torch.randn(M, K, device=cuda, generator=g).bfloat16())
+    B8, sb = _q((torch.randn(N, K, device=cuda, generator=g) * 0.05).bfloat16())
+    bias = torch.randn(N, device=cuda, generator=g) * 0.1
+    x = ((A8.float() * sa) @ (B8.float() * sb).t() + bias).bfloat16().float().requires_grad_(True)
+    torch.nn.functional.gelu(x).backward(torch.ones(M, N, device=cuda))
+    s1, s2 = torch.zeros(4, device=cuda), torch.zeros(4, device=cuda)
+    gd16 = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    gd8 = torch.empty(M, N, device=cuda, dtype=torch.uint8)
+    a8_16 = torch.empty(M, N, device=cuda, dtype=torch.float8_e4m3fn)
+    a8_8 = torch.empty_like(a8_16)
+    act16 = k.gemm_fp8(A8, B8, EPI_GELUD, bias, sa, sb, pre=gd16, out8=a8_16, state=s1, phase=0)
+    act8 = k.gemm_fp8(A8, B8, EPI_GELUD, bias, sa, sb, pre=gd8, out8=a8_8, state=s2, phase=0)
+    assert torch.equal(act16, act8) and torch.equal(a8_16.view(torch.uint8), a8_8.view(torch.uint8))
+    assert torch.equal(s1, s2)
+    torch.testing.assert_close(gd16.float(), x.grad, atol=1e-2, rtol=1e-2)
+    # the device encoder of a bf16 gelu' = the host mirror (one fma; a rounding tie may differ by one code)
+    from ml_recipe_distributed_pytorch_amd import ops
+    dev = ops.gelud_encode(gd16)
+    host = ops.gelud_encode(gd16.cpu())
+    d = (dev.cpu().int() - host.int()).abs()
+    assert d.max().item() <= 1 and (d > 0).float().mean().item() < 1e-4
+    # and within half a step of the code the epilogue wrote from the fp32 gelu'
+    d2 = (dev.int() - gd8.int()).abs()
+    assert d2.max().item() <= 2, d2.max().item()
+    with pytest.raises(RuntimeError, match="write_out"):
+        k.gemm_fp8(A8, B8, EPI_GELUD, bias, sa, sb, pre=gd16, out8=a8_16, state=s1, phase=1, write_out=False)
+
+
+@pytest.mark.gpu
 def test_fp8_quant_delayed(cuda):
     k = _native.kernels()
     x = (torch.randn(1024, 768, device=cuda) * 3).bfloat16()

@@ -163,6 +163,23 @@ def test_embedding(cuda, H, ntypes, p, layout):
     assert out[0][0].abs().max().item() == 0.0, "padding row must get no gradient"
 
 
+@pytest.mark.parametrize("V,T", [(200, 1000), (30522, 98304 + 17), (30522, 1), (70000, 5000), (1000, 4096)])
+def test_sort_ids_is_a_stable_sort(cuda, V, T):
+    """The embedding backward's own LSD radix sort (norm.hip sort_*_kernel, 1 / 2 / 3 passes of 8 bits) equals a
+    stable sort: ids ascending, rows of one id in token order — and the same permutation every run."""
+    k = _native.kernels()
+    g = torch.Generator().manual_seed(V + T)
+    ids = torch.randint(0, V, (T,), generator=g)
+    if T > 100:
+        ids[torch.randperm(T, generator=g)[: T // 10]] = V // 2    # one long run
+    skeys, srows = k.sort_ids(ids.to(cuda), V)
+    want_k, want_r = torch.sort(ids, stable=True)
+    assert torch.equal(skeys.cpu().long(), want_k)
+    assert torch.equal(srows.cpu().long(), want_r)
+    k2, r2 = k.sort_ids(ids.to(cuda), V)
+    assert torch.equal(k2, skeys) and torch.equal(r2, srows)
+
+
 @pytest.mark.parametrize("accumulate", [False, True])
 def test_embedding_bwd_sorted_runs(cuda, accumulate):
     """The id-sorted word-gradient pass: runs of one id that stay inside a 16-row chunk, end exactly on a chunk

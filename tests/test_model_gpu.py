@@ -146,3 +146,22 @@ def test_memory_model_matches_measured_slope(cuda):
     est = estimate(cfg, L)
     modelled = est.act_bytes_per_sample + est.transient_bytes_per_sample
     assert measured == pytest.approx(modelled, rel=0.2), (measured, modelled)
+
+
+def test_ln_guard_kernel_matches_cpu_rule(cuda):
+    """The LayerNorm-from-y guard on the GPU is one own kernel (norm.hip ln_guard_kernel, no ATen chain) and gives
+    the CPU rule's flags: γ = 0, |β| > 8·|γ| and a border case |β| = 8·|γ| (allowed)."""
+    cfg = get_config("bert-tiny-test")
+    m = BertForQuestionAnswering(cfg, precision="bf16", seed=1).to(cuda)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    sd["transformer.encoder.layer.1.attention.output.LayerNorm.weight"][7] = 1e-3
+    sd["transformer.encoder.layer.1.attention.output.LayerNorm.bias"][7] = 0.5
+    sd["transformer.encoder.layer.0.output.LayerNorm.weight"][3] = 0.0
+    sd["transformer.encoder.layer.1.output.LayerNorm.weight"][5] = 0.25
+    sd["transformer.encoder.layer.1.output.LayerNorm.bias"][5] = -2.0
+    m.load_state_dict(sd)
+    flags = m._ln_flags()
+    assert flags.is_cuda and flags.dtype == torch.bool
+    cpu = BertForQuestionAnswering(cfg, precision="fp32", seed=1)
+    cpu.load_state_dict({k: v.cpu() for k, v in sd.items()})
+    assert flags.cpu().tolist() == cpu._ln_flags().tolist() == [True, False, False, True]

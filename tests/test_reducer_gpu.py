@@ -144,6 +144,17 @@ def test_torchrun_world1_runs_the_n_rank_path(cuda, tmp_path):
     assert rec["uid_via_store"] is True and rec["broadcast_done"] is True, rec
     assert "not the headline config" in rec["metric"], rec
     assert rec["value"] > 0 and rec["final_loss"] == rec["final_loss"], rec
+    # the N > 1 correctness self-check runs on the same path (a 1-replica gather here)
+    assert rec["weights_equal_across_ranks"] is True and rec["grads_equal_across_ranks"] is True, rec
+    assert rec["replica_mismatch_parts"] == 0 and rec["rccl_comm_ranks_ok"] is True, rec
+
+
+def test_fingerprint_kernel_equals_host(cuda):
+    """The device fingerprint kernel gives the host (numpy) fingerprint bit for bit, on an odd-sized arena."""
+    from ml_recipe_distributed_pytorch_amd.parallel.reducer import fingerprint
+    x = torch.randn(3_000_017, generator=torch.Generator().manual_seed(3))
+    for parts in (1, 7, 256):
+        assert torch.equal(fingerprint(x.to(cuda), parts).cpu(), fingerprint(x, parts)), parts
 
 
 def test_bench_refuses_more_gpus_than_visible(cuda):

@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """Build a second kernel library for same-box A/B: the in-tree sources, except the listed kernel files taken
 from git revision REV, linked into tools/ab_so/_hq_kernels<ext> (load it with HQ_KERNELS_DIR=tools/ab_so;
-AB_DIR=tools/<name> picks another directory).
+AB_DIR=tools/<name> picks another directory; HQ_KERNEL_CFLAGS="-DHQ_EPI_DIAG=1 ..." adds lab defines to THIS build
+only — the production build never reads it).
 
     python tools/build_ab_lib.py HEAD ml_recipe_distributed_pytorch_amd/csrc/kernels/gemm.hip
 """
@@ -29,7 +30,8 @@ def main():
     here, pkg = b.HERE, b.PKG
     try:
         b.HERE, b.PKG = tmp, out_dir
-        out = b.build_kernels(8)
+        lab = [f for f in os.environ.get("HQ_KERNEL_CFLAGS", "").split() if f.startswith("-D")]
+        out = b.build_kernels(8, lab_defines=lab)
     finally:
         b.HERE, b.PKG = here, pkg
     print(out)
