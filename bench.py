@@ -58,9 +58,10 @@ def parse():
     ap.add_argument("--allreduce_dtype", default="fp32", choices=["fp32", "bf16", "emb_bf16"],
                     help="gradient all-reduce wire dtype: every bucket fp32 / bf16, or only the embeddings bucket (the "
                          "step's exposed comm tail) in bf16")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"],
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8", "fp32"],
                     help="compute precision; fp8 = OCP e4m3 forward projections and e5m2-gradient dgrads "
-                         "(BASELINE config #5)")
+                         "(BASELINE config #5); fp32 = the reference's Apex-off mode (exact-f32 MFMA GEMMs, fp32 "
+                         "flash attention and row kernels)")
     ap.add_argument("--fp8_dgrad", type=int, default=1, choices=[0, 1],
                     help="with --precision fp8: 0 keeps the backward dgrads in bf16 (A/B of the fp8 backward)")
     ap.add_argument("--bucket_cap_mb", type=float, default=32.0)

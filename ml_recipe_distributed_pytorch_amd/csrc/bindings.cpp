@@ -805,6 +805,138 @@ Tensor qa_heads_bwd(Tensor seq, int64_t L, Tensor dlog, Tensor dheads, c10::opti
 
 }  // namespace
 
+// ---------------------------------------------------------------- --precision fp32 (f32_ops.hip)
+static void f32_rows(const Tensor& t, const char* n) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == F32 && t.is_contiguous(), n, " must be a contiguous fp32 GPU tensor");
+}
+
+std::vector<Tensor> f32_embed_fwd(Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tensor wp, Tensor wt, Tensor gamma,
+                                  Tensor beta, double eps, double p, int64_t seed, int64_t opid) {
+  check(ids, I64, "ids"); check(pids, I64, "pos_ids"); check(tids, I64, "type_ids");
+  f32_rows(ww, "w_word"); f32_rows(wp, "w_pos"); f32_rows(wt, "w_type"); f32_rows(gamma, "gamma"); f32_rows(beta, "beta");
+  const int64_t T = ids.numel(), H = ww.size(1);
+  TORCH_CHECK(pids.numel() == T && tids.numel() == T && wp.size(1) == H && wt.size(1) == H && gamma.numel() == H, "shapes");
+  c10::DeviceGuard g(ww.device());
+  auto y = at::empty({T, H}, ww.options());
+  auto mean = at::empty({T}, ww.options());
+  auto rstd = at::empty({T}, ww.options());
+  hq_f32_embed_fwd(ptr<int64_t>(ids), ptr<int64_t>(pids), ptr<int64_t>(tids), ptr<float>(ww), ptr<float>(wp), ptr<float>(wt),
+                   ptr<float>(gamma), ptr<float>(beta), ptr<float>(y), ptr<float>(mean), ptr<float>(rstd), (int)T, (int)H,
+                   (float)eps, (float)p, u32(seed), u32(opid), (int)ww.size(0), (int)wp.size(0), (int)wt.size(0),
+                   cur_stream());
+  return {y, mean, rstd};
+}
+
+void f32_embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tensor wp, Tensor wt, Tensor gamma, Tensor mean,
+                   Tensor rstd, double p, int64_t seed, int64_t opid, Tensor g_word, Tensor g_pos, Tensor g_type,
+                   Tensor g_gamma, Tensor g_beta, bool accumulate, int64_t pad_word, int64_t pad_pos) {
+  check(ids, I64, "ids"); check(pids, I64, "pos_ids"); check(tids, I64, "type_ids");
+  for (auto* t : {&dy, &ww, &wp, &wt, &gamma, &mean, &rstd, &g_word, &g_pos, &g_type, &g_gamma, &g_beta}) f32_rows(*t, "f32 operand");
+  const int64_t T = ids.numel(), H = ww.size(1);
+  TORCH_CHECK(dy.size(0) == T && dy.size(1) == H, "dy shape");
+  TORCH_CHECK(g_word.sizes() == ww.sizes() && g_pos.sizes() == wp.sizes() && g_type.sizes() == wt.sizes(), "grad shapes");
+  c10::DeviceGuard g(dy.device());
+  auto s = cur_stream();
+  if (!accumulate) {
+    (void)hipMemsetAsync(g_word.data_ptr(), 0, g_word.numel() * 4, s);
+    (void)hipMemsetAsync(g_pos.data_ptr(), 0, g_pos.numel() * 4, s);
+    (void)hipMemsetAsync(g_type.data_ptr(), 0, g_type.numel() * 4, s);
+  }
+  auto part = at::empty({hq_f32_row_partials((int)T), 2 * H}, dy.options());
+  hq_f32_embed_bwd(ptr<float>(dy), ptr<int64_t>(ids), ptr<int64_t>(pids), ptr<int64_t>(tids), ptr<float>(ww), ptr<float>(wp),
+                   ptr<float>(wt), ptr<float>(gamma), ptr<float>(mean), ptr<float>(rstd), ptr<float>(g_word),
+                   ptr<float>(g_pos), ptr<float>(g_type), ptr<float>(part), outs4(ptr<float>(g_gamma), ptr<float>(g_beta)),
+                   (int)T, (int)H, (int)pad_word, (int)pad_pos, (float)p, u32(seed), u32(opid), accumulate,
+                   (int)ww.size(0), (int)wp.size(0), (int)wt.size(0), s);
+}
+
+std::vector<Tensor> f32_ln_fwd(Tensor a, Tensor resid, Tensor gamma, Tensor beta, double eps, double p, int64_t seed,
+                               int64_t opid) {
+  f32_rows(a, "a"); f32_rows(resid, "resid"); f32_rows(gamma, "gamma"); f32_rows(beta, "beta");
+  TORCH_CHECK(a.dim() == 2 && a.sizes() == resid.sizes() && gamma.numel() == a.size(1), "ln shapes");
+  c10::DeviceGuard g(a.device());
+  const int64_t T = a.size(0), H = a.size(1);
+  auto y = at::empty_like(a), z = at::empty_like(a);
+  auto mean = at::empty({T}, a.options()), rstd = at::empty({T}, a.options());
+  hq_f32_ln_fwd(ptr<float>(a), ptr<float>(resid), ptr<float>(gamma), ptr<float>(beta), ptr<float>(y), ptr<float>(z),
+                ptr<float>(mean), ptr<float>(rstd), (int)T, (int)H, (float)eps, (float)p, u32(seed), u32(opid), cur_stream());
+  return {y, z, mean, rstd};
+}
+
+std::vector<Tensor> f32_ln_bwd(Tensor dy, c10::optional<Tensor> dy2, Tensor z, Tensor gamma, Tensor mean, Tensor rstd,
+                               double p, int64_t seed, int64_t opid, c10::optional<Tensor> g_gamma,
+                               c10::optional<Tensor> g_beta, c10::optional<Tensor> g_bias, bool accumulate,
+                               c10::optional<Tensor> beta) {
+  f32_rows(dy, "dy"); f32_rows(z, "z"); f32_rows(gamma, "gamma"); f32_rows(mean, "mean"); f32_rows(rstd, "rstd");
+  if (dy2.has_value() && dy2->defined()) { f32_rows(*dy2, "dy2"); TORCH_CHECK(dy2->sizes() == dy.sizes(), "dy2 shape"); }
+  if (beta.has_value() && beta->defined()) f32_rows(*beta, "beta");
+  TORCH_CHECK(dy.sizes() == z.sizes() && gamma.numel() == dy.size(1), "ln_bwd shapes");
+  c10::DeviceGuard g(dy.device());
+  const int64_t T = dy.size(0), H = dy.size(1);
+  auto dz = at::empty_like(dy), da = at::empty_like(dy);
+  auto part = at::empty({hq_f32_row_partials((int)T), 3 * H}, dy.options());
+  hq_f32_ln_bwd(ptr<float>(dy), optr<float>(dy2), ptr<float>(z), ptr<float>(gamma), optr<float>(beta), ptr<float>(mean),
+                ptr<float>(rstd), ptr<float>(dz), ptr<float>(da), ptr<float>(part),
+                outs4(optr<float>(g_gamma), optr<float>(g_beta), optr<float>(g_bias)), (int)T, (int)H, (float)p, u32(seed),
+                u32(opid), accumulate, cur_stream());
+  return {dz, da};
+}
+
+Tensor f32_gelu_fwd(Tensor x) {
+  f32_rows(x, "x");
+  c10::DeviceGuard g(x.device());
+  auto y = at::empty_like(x);
+  hq_f32_gelu_fwd(ptr<float>(x), ptr<float>(y), x.numel(), cur_stream());
+  return y;
+}
+
+Tensor f32_gelu_bwd(Tensor dout, Tensor x, c10::optional<Tensor> g_bias, bool accumulate) {
+  f32_rows(dout, "dout"); f32_rows(x, "pre");
+  TORCH_CHECK(dout.sizes() == x.sizes() && dout.dim() == 2, "gelu_bwd shapes");
+  c10::DeviceGuard g(x.device());
+  const int64_t T = x.size(0), N = x.size(1);
+  auto d = at::empty_like(x);
+  auto part = at::empty({hq_f32_row_partials((int)T), N}, x.options());
+  hq_f32_gelu_bwd(ptr<float>(dout), ptr<float>(x), ptr<float>(d), ptr<float>(part), optr<float>(g_bias), (int)T, (int)N,
+                  accumulate, cur_stream());
+  return d;
+}
+
+void f32_colsum(Tensor x, Tensor out, bool accumulate) {
+  f32_rows(x, "x"); f32_rows(out, "out");
+  TORCH_CHECK(x.dim() == 2 && out.numel() == x.size(1), "colsum shapes");
+  c10::DeviceGuard g(x.device());
+  auto part = at::empty({hq_f32_row_partials((int)x.size(0)), x.size(1)}, x.options());
+  hq_f32_colsum(ptr<float>(x), ptr<float>(part), ptr<float>(out), (int)x.size(0), (int)x.size(1), accumulate, cur_stream());
+}
+
+std::vector<Tensor> f32_attn_fwd(Tensor qkv, Tensor key_bias, int64_t B, int64_t L, int64_t nh, double p, int64_t seed,
+                                 int64_t opid, double scale) {
+  f32_rows(qkv, "qkv"); f32_rows(key_bias, "key_bias");
+  TORCH_CHECK(qkv.size(0) == B * L && qkv.size(1) == 3 * nh * 64 && key_bias.numel() == B * L, "f32 attention: head_dim 64");
+  TORCH_CHECK(B * nh * L * L < (int64_t(1) << 32), "f32 attention: dropout element index must fit 32 bits");
+  c10::DeviceGuard g(qkv.device());
+  auto ctx = at::empty({B * L, nh * 64}, qkv.options());
+  auto lse = at::empty({B, nh, L}, qkv.options());
+  hq_f32_attn_fwd(ptr<float>(qkv), ptr<float>(key_bias), ptr<float>(ctx), ptr<float>(lse), (int)B, (int)L, (int)nh, (float)p,
+                  u32(seed), u32(opid), (float)scale, cur_stream());
+  return {ctx, lse};
+}
+
+Tensor f32_attn_bwd(Tensor dctx, Tensor qkv, Tensor ctx, Tensor lse, Tensor key_bias, int64_t B, int64_t L, int64_t nh,
+                    double p, int64_t seed, int64_t opid, double scale) {
+  f32_rows(dctx, "dctx"); f32_rows(qkv, "qkv"); f32_rows(ctx, "ctx"); f32_rows(lse, "lse"); f32_rows(key_bias, "key_bias");
+  TORCH_CHECK(qkv.size(0) == B * L && qkv.size(1) == 3 * nh * 64 && dctx.sizes() == ctx.sizes() &&
+              ctx.size(0) == B * L && ctx.size(1) == nh * 64 && lse.numel() == B * nh * L && key_bias.numel() == B * L,
+              "f32 attention backward shapes");
+  c10::DeviceGuard g(qkv.device());
+  auto dqkv = at::empty_like(qkv);
+  auto delta = at::empty({B, nh, L}, qkv.options());
+  hq_f32_attn_bwd(ptr<float>(dctx), ptr<float>(qkv), ptr<float>(ctx), ptr<float>(lse), ptr<float>(key_bias), ptr<float>(dqkv),
+                  ptr<float>(delta), (int)B, (int)L, (int)nh, (float)p, u32(seed), u32(opid), (float)scale, cur_stream());
+  return dqkv;
+}
+
 PYBIND11_MODULE(_hq_kernels, m) {
   m.doc() = "gfx950 HIP kernels + RCCL reducer for ml_recipe_distributed_pytorch_amd";
   m.def("embed_fwd", &embed_fwd);
@@ -842,6 +974,25 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("transpose_tiles", &transpose_tiles);
   m.def("transpose_tiles8", &transpose_tiles8);
   m.def("colsum_into", &colsum_into);
+  m.def("f32_embed_fwd", &f32_embed_fwd);
+  m.def("f32_embed_bwd", &f32_embed_bwd);
+  m.def("f32_ln_fwd", &f32_ln_fwd);
+  m.def("f32_ln_bwd", &f32_ln_bwd, py::arg("dy"), py::arg("dy2"), py::arg("z"), py::arg("gamma"), py::arg("mean"),
+        py::arg("rstd"), py::arg("p"), py::arg("seed"), py::arg("opid"), py::arg("g_gamma"), py::arg("g_beta"),
+        py::arg("g_bias"), py::arg("accumulate"), py::arg("beta") = py::none());
+  m.def("f32_gelu_fwd", &f32_gelu_fwd);
+  m.def("f32_gelu_bwd", &f32_gelu_bwd);
+  m.def("f32_colsum", &f32_colsum);
+  m.def("f32_attn_fwd", &f32_attn_fwd);
+  m.def("f32_attn_bwd", &f32_attn_bwd);
+  m.def("key_bias", [](Tensor mask) {   // bool / uint8 attention mask -> fp32 additive key bias, same shape
+    TORCH_CHECK(mask.is_cuda() && mask.is_contiguous() && mask.element_size() == 1 &&
+                (mask.scalar_type() == at::kBool || mask.scalar_type() == at::kByte), "key_bias: bool / uint8 GPU mask");
+    c10::DeviceGuard g(mask.device());
+    auto kb = at::empty(mask.sizes(), mask.options().dtype(at::kFloat));
+    hq_key_bias(reinterpret_cast<const uint8_t*>(mask.data_ptr()), ptr<float>(kb), (int)mask.numel(), cur_stream());
+    return kb;
+  });
   m.def("ln_guard", [](Tensor master, Tensor goff, Tensor boff, int64_t H, double ratio) {
     check(master, F32, "master");
     TORCH_CHECK(goff.is_cuda() && boff.is_cuda() && goff.scalar_type() == at::kLong && boff.scalar_type() == at::kLong &&

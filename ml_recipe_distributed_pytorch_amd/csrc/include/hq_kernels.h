@@ -66,6 +66,32 @@ void hq_embed_bwd(const uint16_t* dy, const int64_t* ids, const int64_t* pids, c
 // partial-sum rows embed_bwd needs for T tokens laid out as [T / L][L] (L <= 0: one sequence)
 int hq_embed_bwd_partials(int T, int L);
 void hq_gelu_fwd(const uint16_t* pre, uint16_t* out, size_t n, hipStream_t s);
+void hq_key_bias(const uint8_t* mask, float* kb, int n, hipStream_t s);
+
+// ---- f32_ops.hip: --precision fp32 row-wise ops and flash attention ----------------------------------------------
+int hq_f32_row_partials(int T);   // partial rows of the column-partial kernels for T rows
+void hq_f32_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, const float* ww, const float* wp,
+                      const float* wt, const float* gamma, const float* beta, float* y, float* mean, float* rstd, int T, int H,
+                      float eps, float p, uint32_t seed, uint32_t opid, int V, int P, int NTY, hipStream_t s);
+void hq_f32_embed_bwd(const float* dy, const int64_t* ids, const int64_t* pids, const int64_t* tids, const float* ww,
+                      const float* wp, const float* wt, const float* gamma, const float* mean, const float* rstd,
+                      float* g_word, float* g_pos, float* g_type, float* part, HqOuts outs, int T, int H, int pad_word,
+                      int pad_pos, float p, uint32_t seed, uint32_t opid, bool accumulate, int V, int P, int NTY,
+                      hipStream_t s);
+void hq_f32_ln_fwd(const float* a, const float* resid, const float* gamma, const float* beta, float* y, float* z, float* mean,
+                   float* rstd, int T, int H, float eps, float p, uint32_t seed, uint32_t opid, hipStream_t s);
+void hq_f32_ln_bwd(const float* dy, const float* dy2, const float* z, const float* gamma, const float* beta, const float* mean,
+                   const float* rstd, float* dz, float* da, float* part, HqOuts outs, int T, int H, float p, uint32_t seed,
+                   uint32_t opid, bool accumulate, hipStream_t s);
+void hq_f32_gelu_fwd(const float* x, float* y, size_t n, hipStream_t s);
+void hq_f32_gelu_bwd(const float* dout, const float* x, float* d, float* part, float* g_bias, int T, int N, bool accumulate,
+                     hipStream_t s);
+void hq_f32_colsum(const float* x, float* part, float* out, int T, int N, bool accumulate, hipStream_t s);
+void hq_f32_attn_fwd(const float* qkv, const float* key_bias, float* ctx, float* lse, int B, int L, int nh, float p,
+                     uint32_t seed, uint32_t opid, float scale, hipStream_t s);
+void hq_f32_attn_bwd(const float* dctx, const float* qkv, const float* ctx, const float* lse, const float* key_bias,
+                     float* dqkv, float* delta, int B, int L, int nh, float p, uint32_t seed, uint32_t opid, float scale,
+                     hipStream_t s);
 void hq_ln_guard(const float* master, const int64_t* goff, const int64_t* boff, int n, int H, float ratio, uint8_t* flags,
                  hipStream_t s);
 void hq_gelu_bwd(const uint16_t* dout, const uint16_t* pre, uint16_t* dpre, float* part, HqOuts outs, int T, int N,

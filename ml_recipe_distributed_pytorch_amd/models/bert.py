@@ -665,6 +665,18 @@ class BertForQuestionAnswering(nn.Module):
             return torch.cumsum(mask, dim=1) * mask + self.config.pad_token_id
         return self.transformer.embeddings.position_ids[:, :L].expand(B, L)
 
+    def _default_positions(self, B: int, L: int, dev) -> torch.Tensor:
+        """BERT's default position ids (0 … L-1 for every row) flattened to [B·L] int64, cached per shape: the
+        forward used to expand + copy them every step."""
+        cache = self.__dict__.setdefault("_pos_cache", {})
+        key = (B, L, str(dev))
+        t = cache.get(key)
+        if t is None:
+            if len(cache) >= 8:
+                cache.clear()
+            t = cache[key] = self.transformer.embeddings.position_ids[0, :L].to(dev, torch.int64).repeat(B).contiguous()
+        return t
+
     def encode(self, input_ids, attention_mask=None, token_type_ids=None, position_ids=None):
         return self._encode(input_ids, attention_mask, token_type_ids, position_ids)[0]
 
@@ -695,9 +707,15 @@ class BertForQuestionAnswering(nn.Module):
         dev = self.store.device
         ids = input_ids.reshape(-1).to(dev, torch.int64)
         tt = (token_type_ids if token_type_ids is not None else torch.zeros_like(input_ids)).reshape(-1).to(dev, torch.int64)
-        pos = self._position_ids(input_ids, position_ids).reshape(-1).to(dev, torch.int64)
+        if position_ids is None and self.config.family != "roberta" and dev.type == "cuda":
+            pos = self._default_positions(B, L, dev)   # cached [B·L] arange rows: no per-step expand copy
+        else:
+            pos = self._position_ids(input_ids, position_ids).reshape(-1).to(dev, torch.int64)
         if attention_mask is None:
             key_bias = torch.zeros(B, L, dtype=torch.float32, device=dev)
+        elif dev.type == "cuda" and attention_mask.dtype in (torch.bool, torch.uint8):
+            from .._native import kernels   # one own kernel (norm.hip key_bias_kernel)
+            key_bias = kernels().key_bias(attention_mask.to(dev).contiguous())
         else:
             key_bias = (1.0 - attention_mask.to(dev, torch.float32)) * -10000.0
         # per-module train/eval as the reference's finetune mode sets it (model.eval() + .train() on the trainable

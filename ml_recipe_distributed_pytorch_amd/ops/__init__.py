@@ -6,7 +6,8 @@
   No vendor BLAS: an untileable shape raises.
 * CPU tensors → ``ops.reference`` (pure PyTorch, fp32), which is also the numerics oracle.
 * fp32 GPU tensors (``--precision fp32``, the reference's Apex-off mode) → ``ops.f32``: every GEMM-shaped product
-  on the own exact-f32 MFMA kernel (``gemm_f32.hip``), the row-wise / elementwise parts as the fp32 oracle ops.
+  on the own exact-f32 MFMA kernel (``gemm_f32.hip``), the row-wise / elementwise parts and the flash attention on
+  the own fp32 kernels (``f32_ops.hip``).
 """
 from __future__ import annotations
 
@@ -35,6 +36,8 @@ def embed_fwd(ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, beta, eps, p
     if _hip(w_word):
         return tuple(_k().embed_fwd(ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, beta,
                                     float(eps), float(p), int(seed), int(opid)))
+    if f32.active(w_word):
+        return f32.embed_fwd(ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, beta, eps, p, seed, opid)
     return ref.embed_fwd(ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, beta, eps, p, seed, opid, out_dtype)
 
 
@@ -46,6 +49,9 @@ def embed_bwd(dy, ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, mean, rs
         return _k().embed_bwd(dy, ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, mean, rstd, float(p),
                               int(seed), int(opid), g_word, g_pos, g_type, g_gamma, g_beta, bool(accumulate),
                               int(pad_word), int(pad_pos), int(seq_len))
+    if f32.active(dy):
+        return f32.embed_bwd(dy, ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, mean, rstd, p, seed, opid,
+                             g_word, g_pos, g_type, g_gamma, g_beta, accumulate, pad_word, pad_pos)
     return ref.embed_bwd(dy, ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, mean, rstd, p, seed, opid,
                          g_word, g_pos, g_type, g_gamma, g_beta, accumulate, pad_word, pad_pos)
 
@@ -65,6 +71,8 @@ def ln_fwd(a, resid, gamma, beta, eps, p, seed, opid, store_z: bool = True):
     if _hip(a):
         return _z_or_none(_k().ln_fwd(a, resid, gamma, beta, float(eps), float(p), int(seed), int(opid),
                                       store_z=bool(store_z)))
+    if f32.active(a):
+        return f32.ln_fwd(a, resid, gamma, beta, eps, p, seed, opid)
     return ref.ln_fwd(a, resid, gamma, beta, eps, p, seed, opid)
 
 
@@ -80,6 +88,8 @@ def ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias
     if _hip(dy):
         return tuple(_k().ln_bwd(dy, dy2, z, gamma, mean, rstd, float(p), int(seed), int(opid),
                                  g_gamma, g_beta, g_bias, bool(accumulate), beta=beta))
+    if f32.active(dy):
+        return f32.ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate, beta=beta)
     return ref.ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate, beta=beta)
 
 
@@ -98,12 +108,16 @@ def ln_bwd_q8(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_b
 def gelu_fwd(pre):
     if _hip(pre):
         return _k().gelu_fwd(pre)
+    if f32.active(pre):
+        return _k().f32_gelu_fwd(pre.contiguous())
     return ref.gelu_fwd(pre)
 
 
 def gelu_bwd(dout, pre, g_bias, accumulate):
     if _hip(dout):
         return _k().gelu_bwd(dout, pre, g_bias, bool(accumulate))
+    if f32.active(dout):
+        return _k().f32_gelu_bwd(dout.contiguous(), pre.contiguous(), g_bias, bool(accumulate))
     return ref.gelu_bwd(dout, pre, g_bias, accumulate)
 
 
@@ -427,7 +441,7 @@ def linear_dgrad_gelu(dy, w, pre, g_bias, accumulate, wt=None):
     """dpre = (dy·W) ⊙ gelu'(pre) and g_bias (+)= Σ_rows dpre — the dgrad of the layer after GELU
     fused with the GELU backward and the bias gradient of the layer before it."""
     if f32.active(dy):
-        return ref.gelu_bwd(f32.linear_dgrad(dy, w), pre, g_bias, accumulate)
+        return gelu_bwd(f32.linear_dgrad(dy, w), pre, g_bias, accumulate)
     if dy.is_cuda:
         assert wt is not None, "GPU dgrad needs the Wᵀ working copy"
         M, N = dy.shape[0], w.shape[1]

@@ -4,17 +4,17 @@ fp32, ``/root/reference/modules/model/trainer/trainer.py:23-32,128-133,200-204``
 
 Every GEMM-shaped FLOP runs on the own exact-f32 MFMA kernel (``csrc/kernels/gemm_f32.hip``,
 ``v_mfma_f32_32x32x2_f32``: a k-ordered fp32 fma chain, no reduced-precision inputs): the encoder projections
-(forward, dgrad and weight gradient, addressed as strided views — no transposed copies) and the attention's
-batched QKᵀ, PV and their four backward products.  The row-wise / elementwise parts (embedding gathers, LayerNorm,
-softmax, GELU, dropout masks from ``ops.rng``) are the fp32 oracle ops of ``ops.reference`` on the device — this
-mode exists for numerical parity with the reference's fp32 training, not for speed; the bf16 / fp8 paths are the
-fused kernels.
+(forward, dgrad and weight gradient, addressed as strided views — no transposed copies).  The attention is a
+flash-style fp32 kernel (``csrc/kernels/f32_ops.hip``: scores recomputed per 32-key tile in registers, online
+softmax forward, LSE backward — no [B, nh, L, L] tensor at any length), and the row-wise / elementwise parts
+(embedding gathers + LayerNorm, residual + dropout + LayerNorm, GELU, the bias-gradient column sums) are own fp32
+kernels too, with the dropout masks of ``ops.rng`` — so the fp32 GPU model reproduces the CPU oracle op for op.
+This mode exists for numerical parity with the reference's fp32 training; the bf16 / fp8 paths are the fast ones.
 """
 from __future__ import annotations
 
 import torch
 
-from . import reference as ref
 from .._native import kernels
 
 
@@ -59,63 +59,48 @@ def linear_wgrad(dy, x, g_w, g_b, accumulate: bool):
     assert g_w.is_contiguous() and g_w.shape == (N, K)
     _gemm(dy, x, g_w, N, K, T, (1, N, 0, 0), (1, K, 0, 0), (K, 0, 0), R=g_w if accumulate else None, ldr=K)
     if g_b is not None:
-        ref._acc(g_b, dy.sum(0), accumulate)
+        kernels().f32_colsum(dy, g_b, bool(accumulate))
+
+
+# ------------------------------------------------------------------------------------ row-wise ops (f32_ops.hip)
+def embed_fwd(ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, beta, eps, p, seed, opid):
+    return tuple(kernels().f32_embed_fwd(ids.contiguous(), pos_ids.contiguous(), type_ids.contiguous(),
+                                         w_word.contiguous(), w_pos.contiguous(), w_type.contiguous(), gamma.contiguous(),
+                                         beta.contiguous(), float(eps), float(p), int(seed), int(opid)))
+
+
+def embed_bwd(dy, ids, pos_ids, type_ids, w_word, w_pos, w_type, gamma, mean, rstd, p, seed, opid,
+              g_word, g_pos, g_type, g_gamma, g_beta, accumulate, pad_word=-1, pad_pos=-1):
+    kernels().f32_embed_bwd(dy.contiguous(), ids.contiguous(), pos_ids.contiguous(), type_ids.contiguous(),
+                            w_word.contiguous(), w_pos.contiguous(), w_type.contiguous(), gamma.contiguous(), mean, rstd,
+                            float(p), int(seed), int(opid), g_word, g_pos, g_type, g_gamma, g_beta, bool(accumulate),
+                            int(pad_word), int(pad_pos))
+
+
+def ln_fwd(a, resid, gamma, beta, eps, p, seed, opid):
+    """z = dropout(a) + resid, y = LN(z): (y, z, mean, rstd)."""
+    return tuple(kernels().f32_ln_fwd(a.contiguous(), resid.contiguous(), gamma.contiguous(), beta.contiguous(),
+                                      float(eps), float(p), int(seed), int(opid)))
+
+
+def ln_bwd(dy, dy2, z, gamma, mean, rstd, p, seed, opid, g_gamma, g_beta, g_bias, accumulate, beta=None):
+    return tuple(kernels().f32_ln_bwd(dy.contiguous(), None if dy2 is None else dy2.contiguous(), z.contiguous(),
+                                      gamma.contiguous(), mean, rstd, float(p), int(seed), int(opid), g_gamma, g_beta,
+                                      g_bias, bool(accumulate), beta=None if beta is None else beta.contiguous()))
 
 
 # ---------------------------------------------------------------------------------------------- attention
 # qkv [T = B·L, 3H] holds q | k | v, head h in columns h·dh … of each third; batch index z = b·nh + h.
 def attn_fwd(qkv, key_bias, B, L, nh, p, seed, opid, scale):
-    qkv = qkv.contiguous()
-    T, H3 = qkv.shape
-    H = H3 // 3
-    dh = H // nh
-    dev = qkv.device
-    s = torch.empty(B, nh, L, L, dtype=torch.float32, device=dev)
-    # S = scale·Q·Kᵀ: A(i = query, k = d) = qkv[(bL + i)·3H + h·dh + d], B(j = key, k = d) = qkv[… + H + …]
-    _gemm(qkv, qkv[:, H:], s, L, L, dh, (H3, 1, L * H3, dh), (H3, 1, L * H3, dh), (L, nh * L * L, L * L),
-          batch=B * nh, nb_in=nh, alpha=scale)
-    s += key_bias.float()[:, None, None, :]
-    lse = torch.logsumexp(s, -1)
-    P = torch.exp(s - lse[..., None])
-    keep = ref._attn_keep(B, nh, L, seed, opid, p, dev)
-    if keep is not None:
-        P = P * keep
-    ctx = torch.empty(T, H, dtype=torch.float32, device=dev)
-    # O = P·V: A(i, k = key) = P[z][i·L + k], B(j = d, k = key) = qkv[(bL + k)·3H + 2H + h·dh + d]
-    _gemm(P, qkv[:, 2 * H:], ctx, L, dh, L, (L, 1, nh * L * L, L * L), (1, H3, L * H3, dh), (H, L * H, dh),
-          batch=B * nh, nb_in=nh)
+    """(ctx [T, H], lse [B, nh, L]) from the flash fp32 kernel (head_dim 64)."""
+    ctx, lse = kernels().f32_attn_fwd(qkv.contiguous(), key_bias.float().contiguous(), int(B), int(L), int(nh), float(p),
+                                      int(seed), int(opid), float(scale))
     return ctx, lse
 
 
 def attn_bwd(dctx, qkv, ctx, lse, key_bias, B, L, nh, p, seed, opid, scale):
-    qkv, dctx, ctx = qkv.contiguous(), dctx.contiguous(), ctx.contiguous()
-    T, H3 = qkv.shape
-    H = H3 // 3
-    dh = H // nh
-    dev = qkv.device
-    bat = dict(batch=B * nh, nb_in=nh)
-    sq = (nh * L * L, L * L)                     # batch strides of a [B, nh, L, L] tensor
-    s = torch.empty(B, nh, L, L, dtype=torch.float32, device=dev)
-    _gemm(qkv, qkv[:, H:], s, L, L, dh, (H3, 1, L * H3, dh), (H3, 1, L * H3, dh), (L,) + sq, alpha=scale, **bat)
-    s += key_bias.float()[:, None, None, :]
-    P = torch.exp(s - lse[..., None])
-    del s
-    keep = ref._attn_keep(B, nh, L, seed, opid, p, dev)
-    Pd = P * keep if keep is not None else P
-    dqkv = torch.empty(T, H3, dtype=torch.float32, device=dev)
-    # dV[k, d] = Σ_q Pd[q, k]·dO[q, d]: A(i = k, kk = q) = Pd[q·L + k] (i-contiguous), B(j = d, kk = q) = dO
-    _gemm(Pd, dctx, dqkv[:, 2 * H:], L, dh, L, (1, L) + sq, (1, H, L * H, dh), (H3, L * H3, dh), **bat)
-    del Pd
-    # dP[q, k] = Σ_d dO[q, d]·V[k, d]
-    dP = torch.empty(B, nh, L, L, dtype=torch.float32, device=dev)
-    _gemm(dctx, qkv[:, 2 * H:], dP, L, L, dh, (H, 1, L * H, dh), (H3, 1, L * H3, dh), (L,) + sq, **bat)
-    if keep is not None:
-        dP = dP * keep
-    delta = (dctx.view(B, L, nh, dh) * ctx.view(B, L, nh, dh)).sum(-1).permute(0, 2, 1)   # [B, nh, L]
-    dS = P * (dP - delta[..., None])
-    del dP, P
-    # dQ = scale·dS·K: A = dS (k-contiguous), B(j = d, kk = key) = K[(bL + key)·3H + H + h·dh + d]
-    _gemm(dS, qkv[:, H:], dqkv, L, dh, L, (L, 1) + sq, (1, H3, L * H3, dh), (H3, L * H3, dh), alpha=scale, **bat)
-    # dK = scale·dSᵀ·Q: A(i = key, kk = q) = dS[q·L + key] (i-contiguous), B(j = d, kk = q) = Q
-    _gemm(dS, qkv, dqkv[:, H:], L, dh, L, (1, L) + sq, (1, H3, L * H3, dh), (H3, L * H3, dh), alpha=scale, **bat)
-    return dqkv
+    """dQKV [T, 3H]: a dQ kernel (which also writes δ = rowsum(dO ∘ O)) and a dK / dV kernel, both recomputing P
+    from the forward's LSE and the dropout keep bits from the hash."""
+    return kernels().f32_attn_bwd(dctx.contiguous(), qkv.contiguous(), ctx.contiguous(), lse.contiguous(),
+                                  key_bias.float().contiguous(), int(B), int(L), int(nh), float(p), int(seed), int(opid),
+                                  float(scale))

@@ -203,7 +203,7 @@ class TrainEngine:
         rng = torch.get_rng_state()   # the capture's forward draws a (unused) host seed: keep the stream aligned
         with torch.cuda.graph(g, stream=side, pool=self._graph_pool):
             loss = self.loss_fn(m(**static_in), static_lab)
-            (loss / self.batch_split).backward()
+            self._backward(loss)
             if sync:
                 self.reducer.finalize()   # the comm stream joins the capturing stream inside the graph
         torch.set_rng_state(rng)
@@ -312,7 +312,7 @@ class TrainEngine:
         preds = self.model(**inputs)
         loss = self.loss_fn(preds, labels)
         timer.mark("fwd")
-        (loss / self.batch_split).backward()
+        self._backward(loss)
         if self.reducer is not None and not boundary and not self.no_sync_accum:
             self.reducer.finalize()
         timer.mark("bwd")
@@ -320,6 +320,17 @@ class TrainEngine:
         if not boundary:
             return None
         return self._apply()
+
+    def _backward(self, loss):
+        """(loss / batch_split).backward() without the two scalar kernels and the ones-fill autograd would launch:
+        the seed gradient d(loss/S)/d(loss) = 1/S is a cached device scalar (computed once as fp32 1/S — the same
+        value DivBackward produces)."""
+        seed = getattr(self, "_grad_seed", None)
+        if (seed is None or seed.device != loss.device or seed.dtype != loss.dtype
+                or getattr(self, "_grad_seed_split", None) != self.batch_split):
+            seed = (torch.ones((), dtype=torch.float32) / self.batch_split).to(loss.dtype).to(loss.device)
+            self._grad_seed, self._grad_seed_split = seed, self.batch_split
+        torch.autograd.backward(loss, grad_tensors=seed)
 
     def _apply(self) -> StepResult:
         timer = self._timer
