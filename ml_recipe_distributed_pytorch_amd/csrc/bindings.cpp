@@ -710,7 +710,8 @@ HqHeadWeights head_weights(const std::vector<Tensor>& w, int64_t H, int64_t NL) 
 }
 
 void check_heads_shape(const Tensor& seq, int64_t L, int64_t NL) {
-  check(seq, BF16, "seq");
+  TORCH_CHECK(seq.is_cuda() && seq.is_contiguous() && (seq.scalar_type() == BF16 || seq.scalar_type() == F32),
+              "seq must be a contiguous bf16 or fp32 GPU tensor");
   const int64_t H = seq.size(-1), T = seq.numel() / H;
   TORCH_CHECK(L > 0 && T % L == 0, "seq rows must be B*L");
   TORCH_CHECK(H % 64 == 0 && H <= 2048, "fused heads need hidden % 64 == 0 and <= 2048, got ", H);
@@ -731,9 +732,9 @@ std::vector<Tensor> qa_heads_fwd(Tensor seq, int64_t L, std::vector<Tensor> w, d
   auto cls = at::empty({B, NL}, f);
   auto reg = at::empty({B, 2}, f);
   auto hpart = at::empty({(int64_t)hq_qa_heads_fwd_scratch((int)B, (int)H)}, f);
-  hq_qa_heads_fwd(ptr<uint16_t>(seq), hw, ptr<float>(logits), ptr<float>(pooled), ptr<float>(cls), ptr<float>(reg),
+  hq_qa_heads_fwd(seq.data_ptr(), hw, ptr<float>(logits), ptr<float>(pooled), ptr<float>(cls), ptr<float>(reg),
                   ptr<float>(hpart), ticket(seq, 0), (int)B, (int)L, (int)H, (int)NL, (float)p, u32(seed), u32(opid),
-                  cur_stream());
+                  cur_stream(), seq.scalar_type() == F32);
   return {logits, pooled, cls, reg};
 }
 
@@ -797,9 +798,9 @@ Tensor qa_heads_bwd(Tensor seq, int64_t L, Tensor dlog, Tensor dheads, c10::opti
   c10::DeviceGuard g(seq.device());
   auto dseq = at::empty_like(seq);
   auto part = at::empty({(int64_t)hq_qa_heads_bwd_span_blocks((int)T), 2 * H + 2}, pooled.options());
-  hq_qa_heads_bwd(ptr<uint16_t>(seq), ptr<float>(dlog), ptr<float>(dheads), optr<float>(gscale), ptr<float>(pooled),
-                  ptr<float>(reg), hw, gg, ptr<uint16_t>(dseq), ptr<float>(part), (int)B, (int)L, (int)H, (int)NL,
-                  accumulate, (float)p, u32(seed), u32(opid), cur_stream());
+  hq_qa_heads_bwd(seq.data_ptr(), ptr<float>(dlog), ptr<float>(dheads), optr<float>(gscale), ptr<float>(pooled),
+                  ptr<float>(reg), hw, gg, dseq.data_ptr(), ptr<float>(part), (int)B, (int)L, (int)H, (int)NL,
+                  accumulate, (float)p, u32(seed), u32(opid), cur_stream(), seq.scalar_type() == F32);
   return dseq;
 }
 
@@ -837,15 +838,18 @@ void f32_embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, T
   TORCH_CHECK(g_word.sizes() == ww.sizes() && g_pos.sizes() == wp.sizes() && g_type.sizes() == wt.sizes(), "grad shapes");
   c10::DeviceGuard g(dy.device());
   auto s = cur_stream();
+  const int n_types = (int)wt.size(0);
   if (!accumulate) {
     (void)hipMemsetAsync(g_word.data_ptr(), 0, g_word.numel() * 4, s);
     (void)hipMemsetAsync(g_pos.data_ptr(), 0, g_pos.numel() * 4, s);
-    (void)hipMemsetAsync(g_type.data_ptr(), 0, g_type.numel() * 4, s);
+    if (n_types > 2) (void)hipMemsetAsync(g_type.data_ptr(), 0, g_type.numel() * 4, s);   // else folded from partials
   }
-  auto part = at::empty({hq_f32_row_partials((int)T), 2 * H}, dy.options());
+  auto part = at::empty({hq_f32_part_rows((int)T), 4 * H}, dy.options());
+  float* t0 = ptr<float>(g_type);
   hq_f32_embed_bwd(ptr<float>(dy), ptr<int64_t>(ids), ptr<int64_t>(pids), ptr<int64_t>(tids), ptr<float>(ww), ptr<float>(wp),
                    ptr<float>(wt), ptr<float>(gamma), ptr<float>(mean), ptr<float>(rstd), ptr<float>(g_word),
-                   ptr<float>(g_pos), ptr<float>(g_type), ptr<float>(part), outs4(ptr<float>(g_gamma), ptr<float>(g_beta)),
+                   ptr<float>(g_pos), t0, ptr<float>(part),
+                   outs4(ptr<float>(g_gamma), ptr<float>(g_beta), n_types <= 2 ? t0 : nullptr, n_types == 2 ? t0 + H : nullptr),
                    (int)T, (int)H, (int)pad_word, (int)pad_pos, (float)p, u32(seed), u32(opid), accumulate,
                    (int)ww.size(0), (int)wp.size(0), (int)wt.size(0), s);
 }
@@ -874,7 +878,7 @@ std::vector<Tensor> f32_ln_bwd(Tensor dy, c10::optional<Tensor> dy2, Tensor z, T
   c10::DeviceGuard g(dy.device());
   const int64_t T = dy.size(0), H = dy.size(1);
   auto dz = at::empty_like(dy), da = at::empty_like(dy);
-  auto part = at::empty({hq_f32_row_partials((int)T), 3 * H}, dy.options());
+  auto part = at::empty({hq_f32_part_rows((int)T), 3 * H}, dy.options());
   hq_f32_ln_bwd(ptr<float>(dy), optr<float>(dy2), ptr<float>(z), ptr<float>(gamma), optr<float>(beta), ptr<float>(mean),
                 ptr<float>(rstd), ptr<float>(dz), ptr<float>(da), ptr<float>(part),
                 outs4(optr<float>(g_gamma), optr<float>(g_beta), optr<float>(g_bias)), (int)T, (int)H, (float)p, u32(seed),
@@ -896,7 +900,7 @@ Tensor f32_gelu_bwd(Tensor dout, Tensor x, c10::optional<Tensor> g_bias, bool ac
   c10::DeviceGuard g(x.device());
   const int64_t T = x.size(0), N = x.size(1);
   auto d = at::empty_like(x);
-  auto part = at::empty({hq_f32_row_partials((int)T), N}, x.options());
+  auto part = at::empty({hq_f32_part_rows((int)T), N}, x.options());
   hq_f32_gelu_bwd(ptr<float>(dout), ptr<float>(x), ptr<float>(d), ptr<float>(part), optr<float>(g_bias), (int)T, (int)N,
                   accumulate, cur_stream());
   return d;
@@ -906,7 +910,7 @@ void f32_colsum(Tensor x, Tensor out, bool accumulate) {
   f32_rows(x, "x"); f32_rows(out, "out");
   TORCH_CHECK(x.dim() == 2 && out.numel() == x.size(1), "colsum shapes");
   c10::DeviceGuard g(x.device());
-  auto part = at::empty({hq_f32_row_partials((int)x.size(0)), x.size(1)}, x.options());
+  auto part = at::empty({hq_f32_part_rows((int)x.size(0)), x.size(1)}, x.options());
   hq_f32_colsum(ptr<float>(x), ptr<float>(part), ptr<float>(out), (int)x.size(0), (int)x.size(1), accumulate, cur_stream());
 }
 

@@ -70,6 +70,7 @@ void hq_key_bias(const uint8_t* mask, float* kb, int n, hipStream_t s);
 
 // ---- f32_ops.hip: --precision fp32 row-wise ops and flash attention ----------------------------------------------
 int hq_f32_row_partials(int T);   // partial rows of the column-partial kernels for T rows
+int hq_f32_part_rows(int T);      // rows to allocate for their `part` scratch (partials + the fold's level 1)
 void hq_f32_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, const float* ww, const float* wp,
                       const float* wt, const float* gamma, const float* beta, float* y, float* mean, float* rstd, int T, int H,
                       float eps, float p, uint32_t seed, uint32_t opid, int V, int P, int NTY, hipStream_t s);
@@ -250,9 +251,10 @@ struct HqLossCfg {
 };
 size_t hq_qa_heads_fwd_scratch(int B, int H);   // floats of the fwd head-partial scratch
 // logits [B·L, 2], pooled [B, H], cls [B, NL], reg [B, 2] (sigmoid); cnt: a zeroed device word, one per stream
-void hq_qa_heads_fwd(const uint16_t* seq, const HqHeadWeights& w, float* logits, float* pooled, float* cls, float* reg,
+// seq / dseq: bf16 (seq_f32 = false) or fp32 [B·L, H]
+void hq_qa_heads_fwd(const void* seq, const HqHeadWeights& w, float* logits, float* pooled, float* cls, float* reg,
                      float* hpart, unsigned* cnt, int B, int L, int H, int NL, float p, uint32_t seed, uint32_t opid,
-                     hipStream_t s);
+                     hipStream_t s, bool seq_f32 = false);
 int hq_qa_loss_partials(int B);                 // rows of the [rows][4] loss scratch
 // losses[6] = start, end, start_reg, end_reg, cls, total; dlog [B·L, 2] and dheads [B, 16] = d total / d preds
 void hq_qa_loss(const float* logits, const float* cls, const float* reg, const int64_t* t_start, const int64_t* t_end,
@@ -260,6 +262,7 @@ void hq_qa_loss(const float* logits, const float* cls, const float* reg, const i
                 float* losses, float* part, unsigned* cnt, int B, int L, int NL, const HqLossCfg& cfg, const int* seg_len,
                 int nseg, hipStream_t s);   // nseg equal segments (seg_len [nseg] span lengths, or null = L)
 int hq_qa_heads_bwd_span_blocks(int T);         // rows of the [rows][2H + 2] span partial scratch
-void hq_qa_heads_bwd(const uint16_t* seq, const float* dlog, const float* dheads, const float* gscale, const float* pooled,
-                     const float* reg, const HqHeadWeights& w, const HqHeadGrads& g, uint16_t* dseq, float* span_part,
-                     int B, int L, int H, int NL, bool accumulate, float p, uint32_t seed, uint32_t opid, hipStream_t s);
+void hq_qa_heads_bwd(const void* seq, const float* dlog, const float* dheads, const float* gscale, const float* pooled,
+                     const float* reg, const HqHeadWeights& w, const HqHeadGrads& g, void* dseq, float* span_part,
+                     int B, int L, int H, int NL, bool accumulate, float p, uint32_t seed, uint32_t opid, hipStream_t s,
+                     bool seq_f32 = false);

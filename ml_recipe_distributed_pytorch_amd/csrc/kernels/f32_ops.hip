@@ -83,13 +83,16 @@ __global__ __launch_bounds__(256) void f32_embed_bwd_kernel(const float* __restr
                                                             float* __restrict__ g_type, float* __restrict__ part, int T, int H,
                                                             int pad_word, int pad_pos, int V, int P, int NTY, HqDropKey kd,
                                                             uint32_t thr, float ks) {
-  __shared__ float red[kW][2][NC * 64];
+  // γ | β | type-0 | type-1 partials per block (the type rows as partials when NTY <= 2: every row of the batch
+  // hits one of two rows, which f32 atomics serialise)
+  __shared__ float red[kW][4][NC * 64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t key = kd.get();
-  float ag[NC], ab[NC], gam[NC];
+  const bool tpart = NTY <= 2;
+  float ag[NC], ab[NC], at0[NC], at1[NC], gam[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
-    ag[c] = ab[c] = 0.f;
+    ag[c] = ab[c] = at0[c] = at1[c] = 0.f;
     gam[c] = c * 64 + lane < H ? gamma[c * 64 + lane] : 0.f;
   }
   const int r0 = blockIdx.x * kRowsPerBlock, r1 = min(T, r0 + kRowsPerBlock);
@@ -123,16 +126,23 @@ __global__ __launch_bounds__(256) void f32_embed_bwd_kernel(const float* __restr
         const float dx = rs * (g[c] * gam[c] - s1 - xh[c] * s2);
         if (id != pad_word) atomicAdd(g_word + id * H + col, dx);
         if (pid != pad_pos) atomicAdd(g_pos + pid * H + col, dx);
-        atomicAdd(g_type + tid * H + col, dx);
+        if (!tpart) atomicAdd(g_type + tid * H + col, dx);
+        at0[c] += tid == 0 ? dx : 0.f;
+        at1[c] += tid == 1 ? dx : 0.f;
       }
     }
   }
 #pragma unroll
-  for (int c = 0; c < NC; ++c) { red[wave][0][c * 64 + lane] = ag[c]; red[wave][1][c * 64 + lane] = ab[c]; }
+  for (int c = 0; c < NC; ++c) {
+    red[wave][0][c * 64 + lane] = ag[c];
+    red[wave][1][c * 64 + lane] = ab[c];
+    red[wave][2][c * 64 + lane] = at0[c];
+    red[wave][3][c * 64 + lane] = at1[c];
+  }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * H; i += 256) {
+  for (int i = threadIdx.x; i < 4 * H; i += 256) {
     const int w = i / H, col = i - w * H;
-    part[(size_t)blockIdx.x * 2 * H + i] = (red[0][w][col] + red[1][w][col]) + (red[2][w][col] + red[3][w][col]);
+    part[(size_t)blockIdx.x * 4 * H + i] = (red[0][w][col] + red[1][w][col]) + (red[2][w][col] + red[3][w][col]);
   }
 }
 
@@ -279,13 +289,31 @@ __global__ __launch_bounds__(256) void f32_colpart_kernel(const float* __restric
   part[(size_t)blockIdx.y * N + col] = s;
 }
 
-// out[c] (+)= Σ_b part[b][c] in block order (deterministic); up to 3 destinations for consecutive W-column slices
-__global__ __launch_bounds__(256) void f32_fold_kernel(const float* __restrict__ part, int nb, int W, int width, HqOuts outs,
-                                                       int accumulate) {
+// Deterministic two-level fold of column partials part[nb][W] (nb ~ T / 64 rows, W up to 3·H): a single
+// column-per-thread pass had W / 256 blocks (9 at W = 2304) each walking ~400 rows serially — 97 µs per fold.
+// Level 1: blocks of (64 columns × one of kFoldS row slices), 4 waves each summing every 4th row of the slice,
+// combined in LDS in a fixed order -> p2[kFoldS][W]; level 2: out[c] (+)= Σ_s p2[s][c] in slice order.
+constexpr int kFoldS = 16;
+__global__ __launch_bounds__(256) void f32_fold1_kernel(const float* __restrict__ part, int nb, int W,
+                                                        float* __restrict__ p2) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane, sl = blockIdx.y;
+  const int b0 = nb * sl / kFoldS, b1 = nb * (sl + 1) / kFoldS;
+  float s = 0.f;
+  if (c < W)
+    for (int b = b0 + wave; b < b1; b += 4) s += part[(size_t)b * W + c];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && c < W) p2[(size_t)sl * W + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+__global__ __launch_bounds__(256) void f32_fold2_kernel(const float* __restrict__ p2, int W, int width, HqOuts outs,
+                                                        int accumulate) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= W) return;
   float s = 0.f;
-  for (int b = 0; b < nb; ++b) s += part[(size_t)b * W + i];
+#pragma unroll
+  for (int k = 0; k < kFoldS; ++k) s += p2[(size_t)k * W + i];
   float* dst = outs.p[i / width];
   if (dst == nullptr) return;
   const int c = i % width;
@@ -514,14 +542,18 @@ void dispatch_nc(int H, F&& f) {
   else { fprintf(stderr, "f32 row kernels: hidden size %d > 1024 unsupported\n", H); abort(); }
 }
 
-void fold(const float* part, int nb, int width, int nout, HqOuts outs, bool accumulate, hipStream_t s) {
+// part must have room for kFoldS more rows past its nb partial rows (the level-1 result lives there)
+void fold(float* part, int nb, int width, int nout, HqOuts outs, bool accumulate, hipStream_t s) {
   const int W = width * nout;
-  hipLaunchKernelGGL(f32_fold_kernel, dim3((W + 255) / 256), dim3(256), 0, s, part, nb, W, width, outs, accumulate ? 1 : 0);
+  float* p2 = part + (size_t)nb * W;
+  hipLaunchKernelGGL(f32_fold1_kernel, dim3((W + 63) / 64, kFoldS), dim3(256), 0, s, part, nb, W, p2);
+  hipLaunchKernelGGL(f32_fold2_kernel, dim3((W + 255) / 256), dim3(256), 0, s, p2, W, width, outs, accumulate ? 1 : 0);
 }
 
 }  // namespace
 
 int hq_f32_row_partials(int T) { return (T + kRowsPerBlock - 1) / kRowsPerBlock; }
+int hq_f32_part_rows(int T) { return hq_f32_row_partials(T) + kFoldS; }
 
 void hq_f32_embed_fwd(const int64_t* ids, const int64_t* pids, const int64_t* tids, const float* ww, const float* wp,
                       const float* wt, const float* gamma, const float* beta, float* y, float* mean, float* rstd, int T, int H,
@@ -547,7 +579,7 @@ void hq_f32_embed_bwd(const float* dy, const int64_t* ids, const int64_t* pids, 
                        gamma, mean, rstd, g_word, g_pos, g_type, part, T, H, pad_word, pad_pos, V, P, NTY, kd, thr,
                        hq_keep_scale(thr));
   });
-  fold(part, nb, H, 2, outs, accumulate, s);
+  fold(part, nb, H, 4, outs, accumulate, s);
 }
 
 void hq_f32_ln_fwd(const float* a, const float* resid, const float* gamma, const float* beta, float* y, float* z, float* mean,

@@ -70,9 +70,47 @@ __device__ bool last_arriver(unsigned* cnt, unsigned nblocks, int* flag) {
   return *flag != 0;
 }
 
+// The sequence (encoder output) and its gradient are bf16 (the bf16 / fp8 step) or fp32 (--precision fp32): TS is
+// the element type; every load widens to fp32 and the head math is fp32 either way.
+template <typename TS> struct SeqRaw4 { using type = uint2; };    // 4 elements as loaded
+template <> struct SeqRaw4<float> { using type = float4; };
+template <typename TS>
+__device__ __forceinline__ typename SeqRaw4<TS>::type ld_raw4(const void* base, size_t off) {
+  return *reinterpret_cast<const typename SeqRaw4<TS>::type*>(static_cast<const TS*>(base) + off);
+}
+__device__ __forceinline__ void raw_to_f4(const uint2& r, float* x) { hq_unpack4(r, x); }
+__device__ __forceinline__ void raw_to_f4(const float4& r, float* x) { x[0] = r.x; x[1] = r.y; x[2] = r.z; x[3] = r.w; }
+template <typename TS>
+__device__ __forceinline__ void ld8f(const void* base, size_t off, float* f) {
+  if constexpr (std::is_same<TS, float>::value) {
+    const float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(base) + off);
+    const float4 b = *reinterpret_cast<const float4*>(static_cast<const float*>(base) + off + 4);
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  } else {
+    hq_unpack8(*reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(base) + off), f);
+  }
+}
+template <typename TS>
+__device__ __forceinline__ float ld1f(const void* base, size_t off) {
+  if constexpr (std::is_same<TS, float>::value) return static_cast<const float*>(base)[off];
+  else return hq_bf2f(static_cast<const uint16_t*>(base)[off]);
+}
+template <typename TS>
+__device__ __forceinline__ void st1f(void* base, size_t off, float v) {
+  if constexpr (std::is_same<TS, float>::value) static_cast<float*>(base)[off] = v;
+  else static_cast<uint16_t*>(base)[off] = hq_f2bf(v);
+}
+template <typename TS>
+__device__ __forceinline__ void st4f(void* base, size_t off, const float* d) {
+  if constexpr (std::is_same<TS, float>::value)
+    *reinterpret_cast<float4*>(static_cast<float*>(base) + off) = make_float4(d[0], d[1], d[2], d[3]);
+  else
+    *reinterpret_cast<uint2*>(static_cast<uint16_t*>(base) + off) = hq_pack4(d);
+}
+
 // =============================================================================================== fwd
 struct FwdArgs {
-  const uint16_t* seq;
+  const void* seq;
   const float *wp, *bp, *wc, *bc, *wrs, *brs, *wre, *bre, *wsp, *bsp;
   float *logits, *pooled, *cls, *reg, *hpart;  // hpart [H/64][B][kHS] scratch
   unsigned* cnt;
@@ -82,7 +120,7 @@ struct FwdArgs {
   float ks;
 };
 
-template <int NCH>
+template <int NCH, typename TS>
 __global__ __launch_bounds__(256) void qa_heads_fwd_kernel(FwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const uint32_t key = a.kd.get();
@@ -91,14 +129,14 @@ __global__ __launch_bounds__(256) void qa_heads_fwd_kernel(FwdArgs a) {
   if ((int)blockIdx.x >= a.npool) {  // ---------------------------------------------- span rows
     const int row0 = (((int)blockIdx.x - a.npool) * 4 + wv) * kSpanFwdRPW;
     if (row0 >= a.T) return;
-    uint2 raw[kSpanFwdRPW][NCH];
+    typename SeqRaw4<TS>::type raw[kSpanFwdRPW][NCH];
 #pragma unroll
     for (int r = 0; r < kSpanFwdRPW; ++r)
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         const int col = c * 256 + lane * 4;
-        raw[r][c] = row0 + r < a.T && col < H ? *reinterpret_cast<const uint2*>(a.seq + (size_t)(row0 + r) * H + col)
-                                              : make_uint2(0u, 0u);
+        raw[r][c] = row0 + r < a.T && col < H ? ld_raw4<TS>(a.seq, (size_t)(row0 + r) * H + col)
+                                              : typename SeqRaw4<TS>::type{};
       }
     float4 u[NCH], v[NCH];
 #pragma unroll
@@ -113,7 +151,7 @@ __global__ __launch_bounds__(256) void qa_heads_fwd_kernel(FwdArgs a) {
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         float x[4];
-        hq_unpack4(raw[r][c], x);
+        raw_to_f4(raw[r][c], x);
         s0 += x[0] * u[c].x + x[1] * u[c].y + x[2] * u[c].z + x[3] * u[c].w;
         s1 += x[0] * v[c].x + x[1] * v[c].y + x[2] * v[c].z + x[3] * v[c].w;
       }
@@ -136,7 +174,7 @@ __global__ __launch_bounds__(256) void qa_heads_fwd_kernel(FwdArgs a) {
     {
       const int s = tid >> 3, kk = (tid & 7) * 8, b = sb * 32 + s;
       float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (b < a.B) hq_unpack8(*reinterpret_cast<const uint4*>(a.seq + (size_t)b * a.L * H + k0 + kk), f);
+      if (b < a.B) ld8f<TS>(a.seq, (size_t)b * a.L * H + k0 + kk, f);
       *reinterpret_cast<float4*>(xs + s * 64 + kk) = make_float4(f[0], f[1], f[2], f[3]);
       *reinterpret_cast<float4*>(xs + s * 64 + kk + 4) = make_float4(f[4], f[5], f[6], f[7]);
     }
@@ -404,10 +442,10 @@ __global__ __launch_bounds__(256) void qa_loss_kernel(LossArgs a) {
 
 // =============================================================================================== bwd
 struct BwdArgs {
-  const uint16_t* seq;
+  const void* seq;
   const float *dlog, *dheads, *gscale, *pooled, *reg;
   const float *wp, *wc, *wrs, *wre, *wsp;
-  uint16_t* dseq;
+  void* dseq;
   float* span_part;  // [nspan][2H + 2]
   float *gwp, *gbp, *gwc, *gbc, *gwrs, *gbrs, *gwre, *gbre;
   int B, L, H, NL, T, acc;
@@ -439,7 +477,7 @@ __device__ __forceinline__ float dpre_at(const BwdArgs& a, uint32_t key, int b, 
 
 __device__ __forceinline__ void put(float* p, float v, int acc) { *p = acc ? *p + v : v; }
 
-template <int NCH>
+template <int NCH, typename TS>
 __global__ __launch_bounds__(256) void qa_heads_bwd_kernel(BwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const uint32_t key = a.kd.get();
@@ -493,7 +531,7 @@ __global__ __launch_bounds__(256) void qa_heads_bwd_kernel(BwdArgs a) {
       if (b >= B) break;
       const size_t row = (size_t)b * a.L;
       const float2 g = *reinterpret_cast<const float2*>(a.dlog + 2 * row);
-      a.dseq[row * H + i] = hq_f2bf(acc[s] + gs * (g.x * u0 + g.y * u1));
+      st1f<TS>(a.dseq, row * H + i, acc[s] + gs * (g.x * u0 + g.y * u1));
     }
     return;
   }
@@ -517,7 +555,7 @@ __global__ __launch_bounds__(256) void qa_heads_bwd_kernel(BwdArgs a) {
       for (int q = 0; q < 8; ++q) {
         const int s = wv + 4 * q, b = b0 + s;
         dp[s * 64 + lane] = b < B ? dpre_at(a, key, b, kb * 64 + lane, scs + s * kHS) : 0.f;
-        xs[s * 64 + lane] = b < B ? hq_bf2f(a.seq[(size_t)b * a.L * H + ib * 64 + lane]) : 0.f;
+        xs[s * 64 + lane] = b < B ? ld1f<TS>(a.seq, (size_t)b * a.L * H + ib * 64 + lane) : 0.f;
       }
       __syncthreads();
 #pragma unroll 4
@@ -636,14 +674,14 @@ __global__ __launch_bounds__(256) void qa_heads_bwd_kernel(BwdArgs a) {
       const int col = c * 256 + lane * 4;
       if (col < H) {
         float x[4], d[4];
-        hq_unpack4(*reinterpret_cast<const uint2*>(a.seq + (size_t)row * H + col), x);
+        raw_to_f4(ld_raw4<TS>(a.seq, (size_t)row * H + col), x);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           acc[0][c][i] = fmaf(g.x, x[i], acc[0][c][i]);
           acc[1][c][i] = fmaf(g.y, x[i], acc[1][c][i]);
           d[i] = g.x * w0[c][i] + g.y * w1[c][i];
         }
-        if (!cls_row) *reinterpret_cast<uint2*>(a.dseq + (size_t)row * H + col) = hq_pack4(d);
+        if (!cls_row) st4f<TS>(a.dseq, (size_t)row * H + col, d);
       }
     }
   }
@@ -683,9 +721,9 @@ void dispatch_nch(int H, F&& f) {
 // ================================================================================== launchers
 size_t hq_qa_heads_fwd_scratch(int B, int H) { return (size_t)(H / 64) * B * kHS; }
 
-void hq_qa_heads_fwd(const uint16_t* seq, const HqHeadWeights& w, float* logits, float* pooled, float* cls, float* reg,
+void hq_qa_heads_fwd(const void* seq, const HqHeadWeights& w, float* logits, float* pooled, float* cls, float* reg,
                      float* hpart, unsigned* cnt, int B, int L, int H, int NL, float p, uint32_t seed, uint32_t opid,
-                     hipStream_t s) {
+                     hipStream_t s, bool seq_f32) {
   FwdArgs a;
   a.seq = seq;
   a.wp = w.wp; a.bp = w.bp; a.wc = w.wc; a.bc = w.bc; a.wrs = w.wrs; a.brs = w.brs; a.wre = w.wre; a.bre = w.bre;
@@ -699,7 +737,11 @@ void hq_qa_heads_fwd(const uint16_t* seq, const HqHeadWeights& w, float* logits,
   const int nspan = (a.T + 4 * kSpanFwdRPW - 1) / (4 * kSpanFwdRPW);
   const size_t lds = (32 * 64 + 64 * 65) * sizeof(float);
   dispatch_nch(H, [&](auto nch) {
-    hipLaunchKernelGGL(qa_heads_fwd_kernel<decltype(nch)::value>, dim3(a.npool + nspan), dim3(256), lds, s, a);
+    if (seq_f32)
+      hipLaunchKernelGGL((qa_heads_fwd_kernel<decltype(nch)::value, float>), dim3(a.npool + nspan), dim3(256), lds, s, a);
+    else
+      hipLaunchKernelGGL((qa_heads_fwd_kernel<decltype(nch)::value, uint16_t>), dim3(a.npool + nspan), dim3(256), lds, s,
+                         a);
   });
 }
 
@@ -724,9 +766,10 @@ void hq_qa_loss(const float* logits, const float* cls, const float* reg, const i
 
 int hq_qa_heads_bwd_span_blocks(int T) { return (T + 4 * kSpanRPW - 1) / (4 * kSpanRPW); }
 
-void hq_qa_heads_bwd(const uint16_t* seq, const float* dlog, const float* dheads, const float* gscale, const float* pooled,
-                     const float* reg, const HqHeadWeights& w, const HqHeadGrads& g, uint16_t* dseq, float* span_part,
-                     int B, int L, int H, int NL, bool accumulate, float p, uint32_t seed, uint32_t opid, hipStream_t s) {
+void hq_qa_heads_bwd(const void* seq, const float* dlog, const float* dheads, const float* gscale, const float* pooled,
+                     const float* reg, const HqHeadWeights& w, const HqHeadGrads& g, void* dseq, float* span_part,
+                     int B, int L, int H, int NL, bool accumulate, float p, uint32_t seed, uint32_t opid, hipStream_t s,
+                     bool seq_f32) {
   BwdArgs a;
   a.seq = seq; a.dlog = dlog; a.dheads = dheads; a.gscale = gscale; a.pooled = pooled; a.reg = reg;
   a.wp = w.wp; a.wc = w.wc; a.wrs = w.wrs; a.wre = w.wre; a.wsp = w.wsp;
@@ -746,8 +789,12 @@ void hq_qa_heads_bwd(const uint16_t* seq, const float* dlog, const float* dheads
   lds = std::max(lds, (size_t)4 * 64 * (kMaxNL + 3) * sizeof(float));              // R3
   lds = std::max(lds, (size_t)4 * (2 * H + 2) * sizeof(float));                    // R4
   dispatch_nch(H, [&](auto nch) {
-    hipLaunchKernelGGL(qa_heads_bwd_kernel<decltype(nch)::value>, dim3(a.nA + a.nW + a.nS + nspan), dim3(256), lds, s,
-                       a);
+    if (seq_f32)
+      hipLaunchKernelGGL((qa_heads_bwd_kernel<decltype(nch)::value, float>), dim3(a.nA + a.nW + a.nS + nspan), dim3(256),
+                         lds, s, a);
+    else
+      hipLaunchKernelGGL((qa_heads_bwd_kernel<decltype(nch)::value, uint16_t>), dim3(a.nA + a.nW + a.nS + nspan),
+                         dim3(256), lds, s, a);
   });
   hq_colsum_outs(span_part, nspan, 2 * H + 2, HqOuts{{g.gwsp, g.gwsp ? g.gwsp + H : nullptr, g.gbsp, nullptr}}, H,
                  accumulate, s);

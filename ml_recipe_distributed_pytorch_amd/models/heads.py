@@ -68,7 +68,7 @@ def head_views(store, which: str) -> List[torch.Tensor]:
 
 
 def fused_heads_possible(model) -> bool:
-    """The model's forward will take the fused head kernels on a bf16 GPU sequence (config / flags only).
+    """The model's forward will take the fused head kernels on a bf16 / fp32 GPU sequence (config / flags only).
     Frozen head parameters (``--finetune_*``, reference D16) are fine: the backward kernel's gradients for them
     are cleared again, so they never reach the grad norm, the reducer or the optimizer."""
     cfg = model.config
@@ -78,7 +78,8 @@ def fused_heads_possible(model) -> bool:
 
 
 def fused_heads_available(model, seq: torch.Tensor) -> bool:
-    return seq.is_cuda and seq.dtype == torch.bfloat16 and fused_heads_possible(model)
+    """bf16 (bf16 / fp8 step) or fp32 (--precision fp32) GPU sequences: heads.hip widens either to fp32."""
+    return seq.is_cuda and seq.dtype in (torch.bfloat16, torch.float32) and fused_heads_possible(model)
 
 
 class _FusedHeadsFn(torch.autograd.Function):

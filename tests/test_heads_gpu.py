@@ -93,6 +93,25 @@ def test_fused_heads_and_loss_match_reference(cuda, kind, lw, B, L, H):
     _close(df, dr, "dseq", rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("kind,B,L,H", [("smooth", 37, 50, 768), ("ce", 16, 128, 1024)])
+def test_fused_heads_fp32_sequence(cuda, kind, B, L, H):
+    """--precision fp32: the fused head / loss kernels read an fp32 sequence and write an fp32 d seq (no ATen /
+    vendor-BLAS head GEMMs in the fp32 step) — vs the reference heads on the same fp32 sequence."""
+    NL = 5
+    m = _model(cuda, H=H, NL=NL)
+    seq = torch.randn(B, L, H, device=cuda) * 0.8
+    t = _targets(cuda, B, L, NL)
+    of, lf, gf, df = _run(m, seq, t, _loss(kind, NL), fused=True)
+    orf, lr, gr, dr = _run(m, seq, t, _loss(kind, NL), fused=False)
+    for k in KEYS:
+        _close(of[k], orf[k], "pred " + k)
+    for k in lr:
+        assert lf[k] == pytest.approx(lr[k], rel=2e-4, abs=1e-6), (k, lf[k], lr[k])
+    for k in gr:
+        _close(gf[k], gr[k], "grad " + k, rtol=1e-3, atol=1e-4)
+    _close(df, dr, "dseq", rtol=1e-4, atol=1e-5)   # fp32 d seq: no bf16 rounding now
+
+
 @pytest.mark.parametrize("kind,lw,S,b,L", [("ce", True, 4, 8, 96), ("focal", False, 3, 11, 64),
                                            ("smooth", False, 128, 2, 512), ("ce", False, 2, 5, 40)])
 def test_fused_loss_segments_match_reference(cuda, kind, lw, S, b, L):

@@ -447,5 +447,12 @@ def test_ln_grid_scale_vs_fp32_oracle(cuda, p):
     dzr, dar = ref.ln_bwd(dy, dy2, z, gamma, m, rs, p, 4321, 3, ggr[0], ggr[1], ggr[2], False)
     _close(dz, dzr, 3e-2, 2e-2, "dz")
     _close(da, dar, 3e-2, 2e-2, "da")
+    # column sums over 98304 rows of the SAME bf16 inputs: the two sides differ only by fp32 summation order, so
+    # the bound is relative to each column's Σ|term| (fp32 order error ~ sqrt(T)·2^-24 of it), not an absolute 2.0
+    g = dy.float() + dy2.float()
+    xh = (z.float() - m[:, None]) * rs[:, None]
+    abs_sums = [(g * xh).abs().sum(0), g.abs().sum(0), dar.float().abs().sum(0)]
     for i, n in enumerate(["dgamma", "dbeta", "dbias"]):
-        torch.testing.assert_close(gg[i], ggr[i], atol=2.0, rtol=2e-3, msg=n)
+        err = (gg[i] - ggr[i]).abs()
+        bound = 1e-4 * abs_sums[i] + 1e-4
+        assert bool((err <= bound).all()), f"{n}: max err/bound {float((err / bound).max()):.3f}"
