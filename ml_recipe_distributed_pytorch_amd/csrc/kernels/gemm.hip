@@ -635,7 +635,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bf[ks][j] = frag(pb, nh * 128 + wn * 32 + j * 16 + fr, ks * 4 + fq);
+      for (int j = 0; j < 2; ++j) bf[ks][j] = frag(pb, wn * 64 + nh * 32 + j * 16 + fr, ks * 4 + fq);
   };
   auto mma = [&](int mh, int nh, const bf16x8_t (&bf)[2][2]) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -715,7 +715,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
   constexpr int NIT = 128 / ROWS_PER_IT;        // 16 row-coalesced pieces per lane
   constexpr bool kReadsAux = EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR;
   const int seg = lane % SEGS, rsub = lane / SEGS;
-  const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;   // 4 pieces per 32-col chunk
+  const int gcol = n0 + wn * 64 + seg * 8;   // full 128-B lines per store (see gemm_nt3_kernel)
   auto grow_of = [&](int it) {
     const int lr = it * ROWS_PER_IT + rsub;
     return m0 + (lr >> 6) * 128 + wm * 64 + (lr & 63);
@@ -727,7 +727,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt2_kernel(const uint16_t* _
     const int nh = J >> 1, j = J & 1;
     const int lc = nh * 32 + j * 16 + fq * 4;
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
+    if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + wn * 64 + nh * 32 + j * 16 + fq * 4);
 #pragma unroll
     for (int I = 0; I < 8; ++I) {
       float v[4] = {acc[I][J][0], acc[I][J][1], acc[I][J][2], acc[I][J][3]};
@@ -976,7 +976,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bf[ks][j] = frag(pb, nh * 128 + wn * 32 + j * 16 + fr, ks * 4 + fq);
+      for (int j = 0; j < 2; ++j) bf[ks][j] = frag(pb, wn * 64 + nh * 32 + j * 16 + fr, ks * 4 + fq);
   };
   auto mma = [&](int mh, int nh, const bf16x8_t (&bf)[2][2]) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1148,7 +1148,11 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     constexpr bool kReadsAux = EPI == HQ_EPI_DGELU || EPI == HQ_EPI_DMUL || EPI == HQ_EPI_RESID || EPI == HQ_EPI_BDR;
     constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELU || EPI == HQ_EPI_GELUD || EPI == HQ_EPI_BDR;
     const int seg = lane % SEGS, rsub = lane / SEGS;
-    const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;
+    // wave column wn owns the 64 contiguous tile columns wn·64 … +63 (B fragments nh·32 + j·16 inside it), so each
+    // store instruction writes 8 rows × one full 128-B line — the earlier wn·32 + {0, 128} map wrote two 64-B half
+    // lines per row, each line split between two waves: −2…−3 % on every K = 768 GEMM, +1.45 % step
+    // (profiles/r6_lines)
+    const int gcol = n0 + wn * 64 + seg * 8;
     const uint32_t wreg_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)wreg;
     // round q: rows (q >> 1)·128 + wm·64 + (q & 1)·32 + it·8 + rsub of the tile (it: 0..3 within the round)
     auto goff_of = [&](int q, int it) {
@@ -1196,12 +1200,12 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
       constexpr bool kAll = kReadsAux && EPI != HQ_EPI_BDR;
       f32x4_t bvs[4] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f},
                         f32x4_t{0.f, 0.f, 0.f, 0.f}};
-      if constexpr (kBias) {   // J = 0..3 at byte offsets 0, 64, 512, 576 (cols +0, +16, +128, +144); one statement
+      if constexpr (kBias) {   // J = 0..3 at byte offsets 0, 64, 128, 192 (cols +0, +16, +32, +48); one statement
         const uint32_t bias_lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)(smem + BIASL);
-        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:512\n\t"
-                     "ds_read_b128 %3, %4 offset:576\n\ts_waitcnt lgkmcnt(0)"
+        asm volatile("ds_read_b128 %0, %4\n\tds_read_b128 %1, %4 offset:64\n\tds_read_b128 %2, %4 offset:128\n\t"
+                     "ds_read_b128 %3, %4 offset:192\n\ts_waitcnt lgkmcnt(0)"
                      : "=&v"(bvs[0]), "=&v"(bvs[1]), "=&v"(bvs[2]), "=&v"(bvs[3])
-                     : "v"(bias_lds + (uint32_t)((wn * 32 + fq * 4) * 4))
+                     : "v"(bias_lds + (uint32_t)((wn * 64 + fq * 4) * 4))
                      : "memory");
       }
       const __amdgpu_buffer_rsrc_t rC = rsrc_of(C);

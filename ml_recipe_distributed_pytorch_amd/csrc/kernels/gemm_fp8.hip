@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
   auto readB = [&](int t, int nh, i32x8 (&bf)[2]) {
     const uint32_t pb = lds0 + (t & 1) * STAGE + PANEL;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) bf[j] = frag32(pb, nh * 128 + wn * 32 + j * 16 + fr, fq);
+    for (int j = 0; j < 2; ++j) bf[j] = frag32(pb, wn * 64 + nh * 32 + j * 16 + fr, fq);
   };
   auto mma = [&](int mh, int nh, const i32x8 (&bf)[2]) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
     const int nh = J >> 1, j = J & 1;
     const int lc = nh * 32 + j * 16 + fq * 4;
     float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
+    if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + wn * 64 + nh * 32 + j * 16 + fq * 4);
 #pragma unroll
     for (int I = 0; I < 8; ++I) {
       float v[4] = {fmaf(acc[I][J][0], dq, bv.x), fmaf(acc[I][J][1], dq, bv.y), fmaf(acc[I][J][2], dq, bv.z),
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
   }
   constexpr int SEGS = WN / 8, ROWS_PER_IT = 64 / SEGS, NIT = 128 / ROWS_PER_IT;
   const int seg = lane % SEGS, rsub = lane / SEGS;
-  const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;
+  const int gcol = n0 + wn * 64 + seg * 8;   // full 128-B lines per store (gemm.hip gemm_nt3_kernel)
   auto grow_of = [&](int it) {
     const int lr = it * ROWS_PER_IT + rsub;
     return m0 + (lr >> 6) * 128 + wm * 64 + (lr & 63);
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* _
   auto readB = [&](int buf, int nh, i32x8 (&bf)[2]) {
     const uint32_t pb = lds0 + buf * STAGE + PANEL;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) bf[j] = frag32(pb, nh * 128 + wn * 32 + j * 16 + fr, fq);
+    for (int j = 0; j < 2; ++j) bf[j] = frag32(pb, wn * 64 + nh * 32 + j * 16 + fr, fq);
   };
   auto mma = [&](int mh, int nh, const i32x8 (&bf)[2]) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -508,7 +508,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* _
     constexpr int SEGS = WN / 8, ROWS_PER_IT = 64 / SEGS;
     constexpr bool kBias = EPI == HQ_EPI_BIAS || EPI == HQ_EPI_GELUD;
     const int seg = lane % SEGS, rsub = lane / SEGS;
-    const int gcol = n0 + (seg >> 2) * 128 + wn * 32 + (seg & 3) * 8;
+    const int gcol = n0 + wn * 64 + seg * 8;   // full 128-B lines per store (gemm.hip gemm_nt3_kernel)
     float csum[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) csum[e] = 0.f;
@@ -519,7 +519,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* _
         const int nh = J >> 1, j = J & 1;
         const int lc = nh * 32 + j * 16 + fq * 4;
         float4 bv = make_float4(0.f, 0.f, 0.f, 0.f);
-        if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + nh * 128 + wn * 32 + j * 16 + fq * 4);
+        if constexpr (kBias) bv = *reinterpret_cast<const float4*>(bias + n0 + wn * 64 + nh * 32 + j * 16 + fq * 4);
 #pragma unroll
         for (int I = 0; I < 4; ++I) {
           const f32x4_t& a = acc[rnd * 4 + I][J];
