@@ -120,6 +120,8 @@ class _Ctx:
         self.B, self.L, self.seed, self.training, self.model = B, L, seed, training, model
         self.x8 = {}   # fp8 path: layer index -> its QKV input in e4m3 (written by the previous layer's LN)
         self.head_mask = None   # [layers, H] per-column multipliers (each head's mask over its dh columns), or None
+        # grad mode of the CALLER: inside an autograd.Function's forward torch.is_grad_enabled() is always False
+        self.grad = torch.is_grad_enabled()
 
 
 class _EmbeddingFn(torch.autograd.Function):
@@ -226,7 +228,7 @@ class _LayerFn(torch.autograd.Function):
         act8 = None
         # bf16 act is only read by a bf16 FFN2 weight gradient: skipped (604 MB of stores at b256) when the
         # backward will run that weight gradient in fp8 from act8 (its gradient state calibrated by then)
-        need_act = not (fp8 and torch.is_grad_enabled() and m.fp8_backward_ok(x.shape[0])
+        need_act = not (fp8 and info.grad and m.fp8_backward_ok(x.shape[0])
                         and s8["dffn2"].step >= 1)
         r8 = (ops.linear_gelu_fwd_fp8(h1, W8("intermediate.dense"), Bm("intermediate.dense.bias"), s8["ffn1"],
                                       s8["ffn2"], x8=h1_8, need_act=need_act) if fp8 else None)
