@@ -145,6 +145,33 @@ __device__ __forceinline__ void store_row64(uint16_t* out, const f32x16_t (&a)[2
     }
 }
 
+// A wave's 32 output rows × 64 bf16 (the same two transposed accumulators as store_row64, × mul per lane) as
+// FULL 128-B lines: lane (q, hh) holds a[d][4G + j] of row q, column d·32 + 8G + 4hh + j; it writes those as
+// 8-B pieces into a private 4 KiB LDS region (row r's 16-B chunk c at c ^ (r & 7): conflict-free reads), reads
+// back 16 B of row (l >> 3) + 8i, chunk l & 7, and each store instruction writes 8 rows × one whole line.
+// store_row64's pieces cover a quarter line per row and instruction (the GEMMs measured half-line stores
+// 2-3 % slower than whole lines, profiles/r6_lines).  Rows >= nvalid are not stored.  `lds` must be free of
+// other waves' traffic; the region is reused at once by the same wave (its LDS operations run in order).
+__device__ __forceinline__ void store_tile64_lines(uint16_t* out0, size_t ld, int nvalid, const f32x16_t (&a)[2],
+                                                   float mul, int lane, char* lds) {
+  const int q = lane & 31, hh = lane >> 5;
+#pragma unroll
+  for (int d = 0; d < 2; ++d)
+#pragma unroll
+    for (int G = 0; G < 4; ++G) {
+      const float v[4] = {a[d][4 * G] * mul, a[d][4 * G + 1] * mul, a[d][4 * G + 2] * mul, a[d][4 * G + 3] * mul};
+      const int c = d * 4 + G;
+      *reinterpret_cast<uint2*>(lds + q * 128 + ((c ^ (q & 7)) << 4) + hh * 8) = hq_pack4(v);
+    }
+  const int c = lane & 7, r0 = lane >> 3;
+  uint4 w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = *reinterpret_cast<const uint4*>(lds + (r0 + 8 * i) * 128 + ((c ^ r0) << 4));
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (r0 + 8 * i < nvalid) *reinterpret_cast<uint4*>(out0 + (size_t)(r0 + 8 * i) * ld + c * 8) = w[i];
+}
+
 // store_row64 plus the same 8 bf16-rounded values per lane as e4m3 (x·inv8) at out8 (same element
 // offsets, one byte each); returns this lane's |max| for the delayed-scaling amax.
 __device__ __forceinline__ float store_row64_q8(uint16_t* out, uint8_t* out8, const f32x16_t (&a)[2], float mul,
@@ -437,7 +464,7 @@ __global__ __launch_bounds__(RW * 64, 4) void attn_fwd_ring_kernel(const uint16_
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
   constexpr int RNS = RAHEAD + 2;
-  static_assert(RAHEAD >= 1 && RAHEAD <= 4, "ring depth");
+  static_assert(RAHEAD >= 2 && RAHEAD <= 4, "ring depth (>= RW slots: per-wave slow-path / store regions)");
   char* ring = reinterpret_cast<char*>(smem);                       // [RNS][K 4 KB | V 4 KB]
   char* sQ = ring + RAHEAD * 2 * RTILE;                             // [RQ][64] bf16 = ring slots RAHEAD, +1
   uint2* sA = reinterpret_cast<uint2*>(ring + RNS * 2 * RTILE);     // [Lp]: (pk(b_hi, b_lo), pk(1, 0))
@@ -705,10 +732,11 @@ __global__ __launch_bounds__(RW * 64, 4) void attn_fwd_ring_kernel(const uint16_
     if (lane == 0) part8[blockIdx.x * RW + wave] = amax;
     return;
   }
-  if (qi < L) {  // lanes q and q+32 share qi: the permlane partners are active together
-    store_row64(ctx + ((size_t)b * L + qi) * H + h * D, o, inv, hh);
-    if (hh == 0) lse[(size_t)bh * L + qi] = (m_b + __builtin_amdgcn_logf(l_tot)) * LN2;  // v_log_f32 = log2
-  }
+  // ctx as whole 128-B lines through this wave's slow-path region of the ring (every tile was consumed before
+  // the vote's barrier, and no other wave touches this region)
+  store_tile64_lines(ctx + ((size_t)b * L + qs * 32) * H + h * D, H, L - qs * 32, o, inv, lane,
+                     ring + wave * 2 * RTILE);
+  if (qi < L && hh == 0) lse[(size_t)bh * L + qi] = (m_b + __builtin_amdgcn_logf(l_tot)) * LN2;  // v_log_f32 = log2
 }
 
 // ============================================================================ backward v3
@@ -884,6 +912,7 @@ __global__ __launch_bounds__(RW * 64, MODE == 0 && NT > 0 ? 4 : 3) void attn_bwd
     if constexpr (MODE == 2) colsum_row64(bpart + ((size_t)b * n32 + qs) * 3 * H + h * D, dq, scale, qok, lane, hh);
     return;
   }
+  // (dQ keeps the quarter-line store_row64: the staged whole-line form pushed this 128-VGPR loop into 43 spills)
   if (qok) store_row64(dqkv + orow_q, dq, scale, hh);
 }
 
@@ -900,6 +929,7 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // slot: Q' [32][64] 4 KB | dO [32][64] 4 KB | A' words [32] uint4 512 B | δ [32] f32 128 B | bits [RW][64] u16
   constexpr int SLOT = 2 * RTILE + 512 + 128 + RW * 128;
+  static_assert(2 * SLOT >= RW * 4096, "dK/dV store staging: 4 KiB per wave in the two slots");
   const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
   const int nblk = gridDim.x, ob = blockIdx.x, xcd = ob & 7, qq = nblk >> 3, rr = nblk & 7;
   const int lin = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (ob >> 3);
@@ -1138,11 +1168,15 @@ __global__ __launch_bounds__(RW * 64, 2) void attn_bwd_dkdv_ring_kernel(
     }
     return;
   }
-  if (active && kok) {
-    uint16_t* out = dqkv + orow_k;
-    store_row64(out + 2 * H, dv, ksc, hh);   // pd carried the mask only
-    store_row64(out + H, dk, LN2, hh);                   // Q' = c·Q with c = scale·log2e: dK = Σ dS·Q'/log2e
+  // dV, dK as whole 128-B lines: every wave is past its last slot read after this barrier; 4 KiB per wave
+  __syncthreads();
+  if (active) {
+    uint16_t* out = dqkv + ((size_t)b * L + ks_idx * 32) * ld + h * D;
+    char* reg = reinterpret_cast<char*>(smem) + wave * 4096;
+    store_tile64_lines(out + 2 * H, ld, L - ks_idx * 32, dv, ksc, lane, reg);   // pd carried the mask only
+    store_tile64_lines(out + H, ld, L - ks_idx * 32, dk, LN2, lane, reg);       // Q' = c·Q, c = scale·log2e
   }
+  (void)orow_k;
 }
 
 }  // namespace
