@@ -1168,7 +1168,13 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_nt3_kernel(const uint16_t* _
     const int vo_lane = ((wm * 64 + rsub) * ldc + gcol) * 2;
     auto so_of = [&](int q, int it) { return ((q >> 1) * 128 + (q & 1) * 32 + it * ROWS_PER_IT) * ldc * 2; };
     auto bload = [&](__amdgpu_buffer_rsrc_t r, int rnd, int it) {
+#if HQ_EPI_DIAG & 64
+      // bit 6 (timing lab only, results WRONG): every operand load reads the tile's first 8 rows (L2-resident):
+      // what the epilogue would cost if the operand never came from HBM
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, vo_lane & 0xFFFF, 0, 0);
+#else
       const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, vo_lane, so_of(rnd, it), 0);
+#endif
       return make_uint4(v.x, v.y, v.z, v.w);
     };
     // STORE-DATA HOLD.  A dwordx4 store can read its data VGPRs well after it issued when the wave has a
