@@ -874,6 +874,9 @@ __global__ __launch_bounds__(RW * 64, MODE == 0 && NT > 0 ? 4 : 3) void attn_bwd
     const uint16_t* tK = reinterpret_cast<const uint16_t*>(sK);
     const uint16_t* tV = reinterpret_cast<const uint16_t*>(sK + RTILE);
     const bf16x8_t ka = __builtin_bit_cast(bf16x8_t, u32x4{aug_src[kt * 32], 0x3F803F80u, 0x3F80u, 0u});
+    // without dropout the MFMA groups run at s_setprio 1 (backward −9 % at p = 0, profiles/r6_attn_prio_not_adopted;
+    // with dropout it gains nothing, and dK/dV and the forward lose with it)
+    if constexpr (!DROP) __builtin_amdgcn_s_setprio(1);
     f32x16_t s_acc = mfma32(row8(tK, 0, lo_, 0), qf[0], zero16);
 #pragma unroll
     for (int s = 1; s < 4; ++s) s_acc = mfma32(row8(tK, 0, lo_, s), qf[s], s_acc);
@@ -881,6 +884,7 @@ __global__ __launch_bounds__(RW * 64, MODE == 0 && NT > 0 ? 4 : 3) void attn_bwd
     f32x16_t p_acc = mfma32(row8(tV, 0, lo_, 0), of[0], zero16);
 #pragma unroll
     for (int s = 1; s < 4; ++s) p_acc = mfma32(row8(tV, 0, lo_, s), of[s], p_acc);
+    if constexpr (!DROP) __builtin_amdgcn_s_setprio(0);
     uint32_t bits = 0xFFFFu;
     f2_t ksc = {1.f, 1.f};
     if constexpr (DROP) {
@@ -899,8 +903,10 @@ __global__ __launch_bounds__(RW * 64, MODE == 0 && NT > 0 ? 4 : 3) void attn_bwd
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const bf16x8_t sb = pack_b(ds, s);
+      if constexpr (!DROP) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int d = 0; d < 2; ++d) dq[d] = mfma32(tr8(tK, 0, lo_, s, d), sb, dq[d]);
+      if constexpr (!DROP) __builtin_amdgcn_s_setprio(0);
     }
   }
   const size_t orow_q = ((size_t)b * L + qi) * ld + h * D;
