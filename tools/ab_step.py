@@ -4,7 +4,7 @@ per-step differences are not swamped by box-to-box variance.  Rounds alternate A
 median ms/step of each.
 
     python tools/ab_step.py --toggle gelu_deriv [--batch 256] [--rounds 4] [--steps 8]
-toggles: tn_lockstep (weight-gradient kernel: lockstep vs alternating rows), gemm_v1 (NT kernel v2 vs v1), halftail (GEMM half-tile tail on / off),
+toggles: fp8_persist (with --precision fp8), tn_lockstep (weight-gradient kernel: lockstep vs alternating rows), gemm_v1 (NT kernel v2 vs v1), halftail (GEMM half-tile tail on / off),
          input_pipeline (on: bench.py's per-step host synthesis + pinned H2D; off: one resident batch)
 """
 import argparse
@@ -51,6 +51,8 @@ def set_toggle(name, on):
         _native.kernels().gemm_set_store_policy(1 if on else 0)
     elif name == "store_nt_all":   # on: streamed epilogue stores at every K; off: only at K <= 768 (production)
         _native.kernels().gemm_set_store_policy(2 if on else 1)
+    elif name == "fp8_persist":   # on: every fp8 GEMM on the persistent kernel (3); off: auto (0, production)
+        _native.kernels().gemm_fp8_set_variant(3 if on else 0)
     elif name == "input_pipeline":
         pass
     else:
@@ -63,6 +65,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--seq", type=int, default=384)
     ap.add_argument("--model", default="bert-base-uncased")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--steps", type=int, default=8)
     ap.add_argument("--only", choices=["off", "on"], default=None,
@@ -70,7 +73,7 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     cfg = get_config(a.model)
-    model = BertForQuestionAnswering(cfg, seed=0).to(dev).train()
+    model = BertForQuestionAnswering(cfg, seed=0, precision=a.precision).to(dev).train()
     _MODEL["m"] = model
     lp = SimpleNamespace(loss="smooth", smooth_alpha=0.01, w_start=1, w_end=1, w_start_reg=1, w_end_reg=1, w_cls=1)
     opt = FusedAdamW(optimizer_groups(model.named_parameters(), 1e-4), model.store, lr=1e-5, correct_bias=False,
