@@ -671,12 +671,18 @@ class BertForQuestionAnswering(nn.Module):
         """BERT's default position ids (0 … L-1 for every row) flattened to [B·L] int64, cached per shape: the
         forward used to expand + copy them every step."""
         cache = self.__dict__.setdefault("_pos_cache", {})
+        # entries read inside a HIP-graph capture stay pinned: the captured kernels keep their address, so the
+        # tensor must outlive the graph (a cleared entry's memory would be handed to later allocations)
+        pinned = self.__dict__.setdefault("_pos_pinned", set())
         key = (B, L, str(dev))
         t = cache.get(key)
         if t is None:
             if len(cache) >= 8:
-                cache.clear()
+                for k in [k for k in cache if k not in pinned]:
+                    del cache[k]
             t = cache[key] = self.transformer.embeddings.position_ids[0, :L].to(dev, torch.int64).repeat(B).contiguous()
+        if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
+            pinned.add(key)
         return t
 
     def encode(self, input_ids, attention_mask=None, token_type_ids=None, position_ids=None):
