@@ -74,9 +74,9 @@ void embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, Tenso
   c10::DeviceGuard g(dy.device());
   auto s = cur_stream();
   if (!accumulate) {
-    hipMemsetAsync(g_word.data_ptr(), 0, g_word.numel() * 4, s);
-    hipMemsetAsync(g_pos.data_ptr(), 0, g_pos.numel() * 4, s);
-    if (n_types > 2) hipMemsetAsync(g_type.data_ptr(), 0, g_type.numel() * 4, s);
+    hq_zero_f32(ptr<float>(g_word), (size_t)g_word.numel(), s);
+    hq_zero_f32(ptr<float>(g_pos), (size_t)g_pos.numel(), s);
+    if (n_types > 2) hq_zero_f32(ptr<float>(g_type), (size_t)g_type.numel(), s);
   }
   const int nb = hq_embed_bwd_partials((int)T, (int)seq_len);
   auto part = at::empty({nb, 4 * H}, gamma.options());
@@ -840,9 +840,9 @@ void f32_embed_bwd(Tensor dy, Tensor ids, Tensor pids, Tensor tids, Tensor ww, T
   auto s = cur_stream();
   const int n_types = (int)wt.size(0);
   if (!accumulate) {
-    (void)hipMemsetAsync(g_word.data_ptr(), 0, g_word.numel() * 4, s);
-    (void)hipMemsetAsync(g_pos.data_ptr(), 0, g_pos.numel() * 4, s);
-    if (n_types > 2) (void)hipMemsetAsync(g_type.data_ptr(), 0, g_type.numel() * 4, s);   // else folded from partials
+    hq_zero_f32(ptr<float>(g_word), (size_t)g_word.numel(), s);
+    hq_zero_f32(ptr<float>(g_pos), (size_t)g_pos.numel(), s);
+    if (n_types > 2) hq_zero_f32(ptr<float>(g_type), (size_t)g_type.numel(), s);   // else folded from partials
   }
   auto part = at::empty({hq_f32_part_rows((int)T), 4 * H}, dy.options());
   float* t0 = ptr<float>(g_type);

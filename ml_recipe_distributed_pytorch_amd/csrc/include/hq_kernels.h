@@ -152,6 +152,7 @@ int hq_gemm_nt_part_rows(int M, int N, int K);
 // 0 = auto (128² tiles for M % 256 != 0 or < 80 % CU fill; else the persistent v3 kernel for K <= 2304,
 // v2 above), 1 = v1, 2 = v2, 3 = v3 (the 256-row kernels wherever M % 256 == 0), 4 = 128² tiles always
 void hq_gemm_set_variant(int v);
+void hq_zero_f32(float* p, size_t n, hipStream_t s);   // own zero-fill kernel (no runtime memset node in graphs)
 void hq_gemm_set_store_policy(int v);   // persistent-kernel epilogue stores: 0 default, 1 nt|sc1 at K <= 768, 2 always
 void hq_gemm_set_stagger(int v);   // v3 start offset of half the workgroups (units of s_sleep(127))
 // v3 tile scheduling: 1 = dynamic (a workgroup's third and later tiles come from per-XCD atomic ticket

@@ -72,7 +72,7 @@ void hq_gelud_encode8(const uint16_t* g, uint8_t* q, size_t n, hipStream_t s) {
 }
 
 void hq_amax_bf16(const uint16_t* x, size_t n, unsigned* amax, hipStream_t s) {
-  (void)hipMemsetAsync(amax, 0, sizeof(unsigned), s);
+  hq_zero_f32(reinterpret_cast<float*>(amax), 1, s);   // own kernel: no runtime memset node under graph capture
   const size_t n8 = n / 8;
   if (n8) hipLaunchKernelGGL(amax_kernel, dim3(grid_for(n8)), dim3(256), 0, s, x, n8, amax);
 }

@@ -1083,11 +1083,35 @@ void colsum(const float* part, int P, int N, HqOuts outs, int Hq, bool accumulat
 
 }  // namespace
 
+// Zero-fill of a gradient buffer (the embedding backward's fresh g_word / g_pos): an own grid-stride kernel with
+// 16-B stores instead of hipMemsetAsync, so the step's graph holds kernel nodes only (a runtime memset node
+// is the one kind of node the rest of the step never uses) and the step trace names every kernel.
+// p[0, head) and the last `tail` (< 4 each) are the unaligned ends, [head, head + 4·n4) the 16-B-aligned body
+__global__ __launch_bounds__(256) void zero_f32_kernel(float* __restrict__ p, int head, size_t n4, int tail) {
+  float4* body = reinterpret_cast<float4*>(p + head);
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) body[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (blockIdx.x == 0) {
+    if ((int)threadIdx.x < head) p[threadIdx.x] = 0.f;
+    if ((int)threadIdx.x < tail) p[head + 4 * n4 + threadIdx.x] = 0.f;
+  }
+}
+
 // ================================================================================== launchers
 namespace {
 const uint32_t* g_seed_ptr = nullptr;
 }
 void hq_set_dropout_seed_ptr(const uint32_t* p) { g_seed_ptr = p; }
+void hq_zero_f32(float* p, size_t n, hipStream_t s) {
+  if (n == 0) return;
+  const size_t mis = (reinterpret_cast<uintptr_t>(p) / sizeof(float)) % 4;   // p is 4-B aligned (f32 tensor)
+  const int head = (int)std::min<size_t>(n, mis ? 4 - mis : 0);
+  const size_t n4 = (n - head) / 4;
+  const int tail = (int)(n - head - 4 * n4);
+  const size_t blocks = (n4 + 255) / 256;
+  const int grid = (int)(blocks < 1 ? 1 : (blocks > 2048 ? 2048 : blocks));
+  hipLaunchKernelGGL(zero_f32_kernel, dim3(grid), dim3(256), 0, s, p, head, n4, tail);
+}
 HqDropKey hq_drop_key(uint32_t seed, uint32_t opid) { return HqDropKey{hq_op_key(seed, opid), opid, g_seed_ptr}; }
 
 void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, const float* beta, uint16_t* y, uint16_t* z,
