@@ -108,3 +108,15 @@ def test_graph_shape_cap_runs_other_lengths_eagerly(cuda):
     assert r1 == 3 and st["shapes"] == 2 and st["graphs"] == 2 and st["eager"] == 2, st
     assert len(st["pools"]) == 1, st
     _same(model, le, me, lg, mg)
+
+
+def test_graph_replay_matches_eager_under_per_op_sync(cuda, monkeypatch):
+    """Regression (profiles/r6_debug_asserts): with a device synchronisation after every kernel op (the debug
+    build's proxy, here over the release kernels), the replays diverged from eager at the third replay while a
+    runtime hipMemsetAsync (the embedding gradients' fresh zero-fill) sat inside the captured step as a memset
+    node.  The step graph now holds kernel nodes only; replay must equal eager bit for bit under any timing."""
+    monkeypatch.setenv("HQ_SYNC_PROXY", "1")
+    le, me, _, model, _ = _run(cuda, graph=False)
+    lg, mg, r1, _, _ = _run(cuda, graph=True)
+    assert r1 == 3
+    _same(model, le, me, lg, mg)
