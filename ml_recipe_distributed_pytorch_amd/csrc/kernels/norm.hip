@@ -1059,6 +1059,43 @@ __global__ __launch_bounds__(1024) void colsum_chunk_kernel(float* __restrict__ 
   }
 }
 
+// The same first pass with 16-B loads: block (x, c) = 4 waves over 256 columns (a float4 per lane) and rows
+// [c·P/C, (c+1)·P/C); each wave walks every 4th row with 4 loads in flight, the block folds its 4 waves in LDS in
+// wave order.  The 64-column form issued 4-B loads (256 B per wave instruction, one row at a time): 9.7 µs for a
+// 28 MB LayerNorm partial (2.9 TB/s).  Needs N % 4 == 0 and 16-B-aligned rows.
+__global__ __launch_bounds__(256) void colsum_chunk4_kernel(float* __restrict__ part, int P, int N, int C) {
+  __shared__ float4 red[4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c4 = blockIdx.x * 64 + lane;                       // float4 column index
+  const int n4 = N >> 2;
+  const int r0 = (int)((long)blockIdx.y * P / C), r1 = (int)((long)(blockIdx.y + 1) * P / C);
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  if (c4 < n4) {
+    int p = r0 + wave;
+    for (; p + 12 < r1; p += 16) {   // 4 rows in flight, two accumulators (fixed association per wave)
+      const float4 v0 = p4[(size_t)p * n4 + c4], v1 = p4[(size_t)(p + 4) * n4 + c4];
+      const float4 v2 = p4[(size_t)(p + 8) * n4 + c4], v3 = p4[(size_t)(p + 12) * n4 + c4];
+      a.x += v0.x; a.y += v0.y; a.z += v0.z; a.w += v0.w;
+      b.x += v1.x; b.y += v1.y; b.z += v1.z; b.w += v1.w;
+      a.x += v2.x; a.y += v2.y; a.z += v2.z; a.w += v2.w;
+      b.x += v3.x; b.y += v3.y; b.z += v3.z; b.w += v3.w;
+    }
+    for (; p < r1; p += 4) {
+      const float4 v = p4[(size_t)p * n4 + c4];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  red[wave][lane] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  __syncthreads();
+  if (wave == 0 && c4 < n4) {
+    float4 t = red[0][lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) { const float4 v = red[w][lane]; t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w; }
+    reinterpret_cast<float4*>(part)[(size_t)r0 * n4 + c4] = t;
+  }
+}
+
 template <typename F>
 void dispatch_nch(int H, F&& f) {
   const int nch = (H + 255) / 256;
@@ -1076,8 +1113,13 @@ void dispatch_nch(int H, F&& f) {
 
 void colsum(const float* part, int P, int N, HqOuts outs, int Hq, bool accumulate, hipStream_t s) {
   const int C = P >= 128 ? std::min(32, P / 32) : P;
-  if (C < P)
-    hipLaunchKernelGGL(colsum_chunk_kernel, dim3((N + 63) / 64, C), dim3(1024), 0, s, const_cast<float*>(part), P, N, C);
+  if (C < P) {
+    if (N % 4 == 0 && reinterpret_cast<uintptr_t>(part) % 16 == 0)
+      hipLaunchKernelGGL(colsum_chunk4_kernel, dim3((N / 4 + 63) / 64, C), dim3(256), 0, s, const_cast<float*>(part), P, N,
+                         C);
+    else
+      hipLaunchKernelGGL(colsum_chunk_kernel, dim3((N + 63) / 64, C), dim3(1024), 0, s, const_cast<float*>(part), P, N, C);
+  }
   hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64), dim3(1024), 0, s, part, C, N, outs, Hq, accumulate ? 1 : 0, P);
 }
 
