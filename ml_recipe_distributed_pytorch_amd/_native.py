@@ -41,9 +41,6 @@ def _load(name: str, directory: str = _PKG_DIR):
         return mod
 
 
-_KEEP = []
-
-
 class _SyncedKernels:
     """Debug-build proxy: every kernel entry point is followed by a device synchronisation, so an
     ``HQ_DASSERT`` trap or a memory fault is reported against the op that caused it.  Not while the current
@@ -60,8 +57,6 @@ class _SyncedKernels:
         def call(*args, **kwargs):
             import torch
             out = attr(*args, **kwargs)
-            if os.environ.get("HQ_PROXY_KEEP", "0") == "1":   # lab: no tensor an op touched is ever freed
-                _KEEP.append((args, kwargs, out))
             if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
                 return out
             if os.environ.get("HQ_DEBUG_NOSYNC", "0") == "1":   # lab: the debug kernels without the serialisation

@@ -17,7 +17,6 @@ gradient as G accumulated micro-steps (mean of per-micro-batch means), at merged
 """
 from __future__ import annotations
 
-import os
 import time
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional
@@ -36,9 +35,6 @@ def to_device(data, device, non_blocking=True):
     if torch.is_tensor(data):
         return data.to(device, non_blocking=non_blocking)
     return data
-
-
-_LAB_SYNC_BEFORE_REPLAY = os.environ.get("HQ_LAB_SYNC_BEFORE_REPLAY", "0") == "1"
 
 
 class PhaseTimer:
@@ -234,8 +230,6 @@ class TrainEngine:
                     dst[k].copy_(v, non_blocking=True)
         seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
         self.model.seed_device.fill_(seed)
-        if _LAB_SYNC_BEFORE_REPLAY:   # lab: input copies / seed word complete on the device before the launch
-            torch.cuda.synchronize()
         if fresh:
             self._timer.reset()
         self._timer.mark()
