@@ -194,6 +194,9 @@ def test_gloo_rehearsal_two_ranks_share_one_gpu(cuda, tmp_path):
     assert rec["process_group"] == "gloo" and rec["world_size"] == 2, rec
     assert rec["hw_queues"] == 4, rec   # not raised: the two ranks share cuda:0
     assert rec["value"] > 0, rec
+    # the data-parallel replica check ran across the two ranks and found bitwise-equal weights and gradients
+    assert rec["weights_equal_across_ranks"] is True and rec["grads_equal_across_ranks"] is True, rec
+    assert rec["replica_mismatch_parts"] == 0, rec
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "emb_bf16"])
