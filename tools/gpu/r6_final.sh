@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$(dirname "$0")/../.."
 export TMPDIR=/tmp
-O=gpurun_out/r6_final
+O=gpurun_out/${R6_OUT:-r6_final}
 mkdir -p "$O"
 timeout -k 10 900 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu tests > "$O/pytest_gpu.log" 2>&1 \
   || { tail -40 "$O/pytest_gpu.log"; exit 1; }
