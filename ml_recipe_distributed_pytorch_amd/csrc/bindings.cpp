@@ -1036,6 +1036,10 @@ PYBIND11_MODULE(_hq_kernels, m) {
   m.def("fp8_quantize", &fp8_quantize);
   m.def("fp8_quant_delayed", &fp8_quant_delayed);
   m.def("fp8_quant_delayed_multi", &fp8_quant_delayed_multi);
+  m.def("fp8_fold_defer", [](bool on) { return hq_fp8_fold_defer(on ? 1 : 0); },
+        "batch the delayed-scaling amax folds of the fp8 producers until fp8_fold_flush (False: flush, immediate folds)");
+  m.def("fp8_fold_flush", []() { hq_fp8_fold_flush(); });
+  m.def("fp8_fold_pending", []() { return hq_fp8_fold_pending(); });
   m.def("fp8_quant_multi_blocks", &fp8_quant_multi_blocks);
   m.def("gemm_fp8_supported", &gemm_fp8_supported);
   m.def("gemm_fp8_set_variant", [](int64_t v) { hq_gemm_fp8_set_variant((int)v); });

@@ -227,6 +227,12 @@ __device__ __forceinline__ float hq_fp8_delayed_scale(const float* st, int phase
   const float margin = fmax == kHqBf8Max ? kHqBf8Margin : kHqFp8Margin;
   return prev > 0.f ? prev * margin / fmax : 1.f;
 }
+// A producer publishes the dequant scale of its own fp8 output (state[3]) itself — one thread of block 0, at its
+// start — so that its amax fold (hq_fp8_amax_fold) may run later, batched with the other sites' folds
+// (hq_fp8_fold_defer); the fold writes the same value again.  Nothing in the producer reads state[3].
+__device__ __forceinline__ void hq_fp8_publish_scale(const float* st, int phase, float fmax = kHqFp8Max) {
+  if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) const_cast<float*>(st)[3] = hq_fp8_delayed_scale(st, phase, fmax);
+}
 // 4 values -> 4 e5m2 bytes (x·inv, saturated to ±57344)
 __device__ __forceinline__ uint32_t hq_pack_bf8x4(const float* f, float inv) {
   float g[4];

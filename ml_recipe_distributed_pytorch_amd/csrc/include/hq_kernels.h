@@ -212,9 +212,16 @@ void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* b
 void hq_fp8_quant_delayed(const uint16_t* x, uint8_t* y, size_t n, float* q8, int phase, hipStream_t s);
 long long hq_fp8_quant_multi_blocks(long long n8);   // blocks of one segment of n8 8-element groups
 // fp8 producers write per-wave amax partials into this device scratch (>= n floats, current device) and
-// hq_fp8_amax_fold folds them into the delayed-scaling state q8 (slot `phase`, clears (phase+1)%3, q8[3])
-float* hq_fp8_amax_parts(size_t n);
+// hq_fp8_amax_fold folds them into the delayed-scaling state q8 (slot `phase`, clears (phase+1)%3, q8[3]).
+// A producer also publishes q8[3] itself (hq_fp8_publish_scale), so under hq_fp8_fold_defer(1) a site's fold may
+// wait: the partials come from a per-device arena (pass the site's state q8 and stream s) and the folds of many
+// sites run as one batched launch at hq_fp8_fold_flush() — or earlier, automatically, when a site with a pending
+// fold produces again, a producer runs on another stream, or the arena is full.
+float* hq_fp8_amax_parts(size_t n, const float* q8 = nullptr, hipStream_t s = nullptr);
 void hq_fp8_amax_fold(const float* part, int n, float* q8, int phase, hipStream_t s, float fmax = 448.f);
+int hq_fp8_fold_defer(int on);   // on = 0 flushes the pending folds and returns to immediate folds
+void hq_fp8_fold_flush();
+int hq_fp8_fold_pending();
 void hq_fp8_quant_delayed_multi(const uint16_t* x, uint8_t* y, const long long* seg, int nseg, long long blocks,
                                 float* states, int phase, hipStream_t s);
 

@@ -461,6 +461,7 @@ __global__ __launch_bounds__(RW * 64, 4) void attn_fwd_ring_kernel(const uint16_
                                                                    const float* __restrict__ q8,
                                                                    float* __restrict__ part8, int phase) {
   const uint32_t key = kd_.get();
+  if (ctx8 != nullptr) hq_fp8_publish_scale(q8, phase);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
   constexpr int RNS = RAHEAD + 2;
@@ -766,6 +767,7 @@ __global__ __launch_bounds__(RW * 64, MODE == 0 && NT > 0 ? 4 : 3) void attn_bwd
     float kscale, uint8_t* __restrict__ dqkv8, const float* __restrict__ q8, float* __restrict__ part8, int phase,
     float* __restrict__ bpart) {
   constexpr bool Q8 = MODE > 0;
+  if constexpr (Q8) hq_fp8_publish_scale(q8, phase, kHqBf8Max);   // dQKV's state (dK/dV share it)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int RNS = RAHEAD + 2;
   const int Lp = NT > 0 ? NT * 32 : (L + 31) & ~31, n32 = Lp >> 5;
@@ -1214,7 +1216,7 @@ void hq_attn_fwd(const uint16_t* qkv, const float* key_bias, uint16_t* ctx, floa
     constexpr int ahead = 2;   // K/V tiles in flight (4-deep measured slower: profiles/r2_attn)
     const size_t lds = (size_t)4 * 2 * RTILE + Lp * sizeof(uint2);
     const int nparts = B * nh * n_qb * RW;
-    float* part8 = ctx8 ? hq_fp8_amax_parts((size_t)nparts) : nullptr;
+    float* part8 = ctx8 ? hq_fp8_amax_parts((size_t)nparts, q8, s) : nullptr;
     auto run = [&](auto cn) {
       constexpr int NT = decltype(cn)::value;
       auto launch1 = [&](auto kern) {
@@ -1266,7 +1268,7 @@ void hq_attn_bwd(const uint16_t* dctx, const uint16_t* qkv, const uint16_t* ctx,
     const size_t lds_kv = 2 * (size_t)(2 * RTILE + 512 + 128 + RW * 128);
     // dQ and dK/dV grids are the same size: partials [dQ waves | dK/dV waves], one fold after both
     const int nparts = B * nh * nb * RW;
-    float* part8 = dqkv8 ? hq_fp8_amax_parts((size_t)2 * nparts) : nullptr;
+    float* part8 = dqkv8 ? hq_fp8_amax_parts((size_t)2 * nparts, q8, s) : nullptr;
     auto run = [&](auto cn) {
       constexpr int NT = decltype(cn)::value;
       auto launch = [&](auto kdq, auto kkv) {

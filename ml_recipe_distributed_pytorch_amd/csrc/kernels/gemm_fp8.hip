@@ -171,6 +171,7 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8_kernel(const uint8_t* __
   const uint8_t* Ab = A + (size_t)m0 * lda;
   const uint8_t* Bb = B + (size_t)n0 * ldb;
   const int nt = K / BK;
+  if constexpr (Q8) hq_fp8_publish_scale(q8, phase, EPI == HQ_EPI_DMUL ? kHqBf8Max : kHqFp8Max);
 
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc((void*)Ab, (short)0, BM * lda, 0x00020000);
   const __amdgpu_buffer_rsrc_t rB = __builtin_amdgcn_make_buffer_rsrc((void*)Bb, (short)0, BN * ldb, 0x00020000);
@@ -435,7 +436,10 @@ __global__ __launch_bounds__(kThreads, 1) void gemm_fp8p_kernel(const uint8_t* _
 
   const float dq = sa[0] * sb[0];
   float inv8 = 1.f, amax = 0.f;
-  if constexpr (Q8) inv8 = 1.f / hq_fp8_delayed_scale(q8, phase, EPI == HQ_EPI_DMUL ? kHqBf8Max : kHqFp8Max);
+  if constexpr (Q8) {
+    hq_fp8_publish_scale(q8, phase, EPI == HQ_EPI_DMUL ? kHqBf8Max : kHqFp8Max);
+    inv8 = 1.f / hq_fp8_delayed_scale(q8, phase, EPI == HQ_EPI_DMUL ? kHqBf8Max : kHqFp8Max);
+  }
 
   int tile = id;
   HQ_DASSERT(tile < ntiles);   // the host launches min(tiles, CUs) workgroups
@@ -605,7 +609,7 @@ void launch(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, 
     }();
     const int tiles = (M / BM) * (N / BN);
     const int nwg = std::min(tiles, ncu);   // every workgroup has at least one tile
-    float* part8 = Q8 ? hq_fp8_amax_parts((size_t)nwg * (kThreads / 64)) : nullptr;
+    float* part8 = Q8 ? hq_fp8_amax_parts((size_t)nwg * (kThreads / 64), q8, s) : nullptr;
     hipLaunchKernelGGL((gemm_fp8p_kernel<EPI, Q8, WC, GD8>), dim3(nwg), dim3(kThreads), lds, s, A, B, C, bias, P, sa, sb, C8, q8,
                        part8, part, phase, M, N, K);
     if (Q8) hq_fp8_amax_fold(part8, nwg * (kThreads / 64), q8, phase, s, EPI == HQ_EPI_DMUL ? kHqBf8Max : kHqFp8Max);
@@ -618,7 +622,7 @@ void launch(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, 
   }();
   (void)init;
   const int grid = (M / BM) * (N / BN);
-  float* part8 = Q8 ? hq_fp8_amax_parts((size_t)grid * (kThreads / 64)) : nullptr;
+  float* part8 = Q8 ? hq_fp8_amax_parts((size_t)grid * (kThreads / 64), q8, s) : nullptr;
   hipLaunchKernelGGL((gemm_fp8_kernel<EPI, Q8, WC, GD8>), dim3(grid), dim3(kThreads), lds, s, A, B, C, bias, P, sa, sb,
                      C8, q8, part8, part, phase, M, N, K, K, K, N);
   if (Q8) hq_fp8_amax_fold(part8, grid * (kThreads / 64), q8, phase, s, EPI == HQ_EPI_DMUL ? kHqBf8Max : kHqFp8Max);
@@ -631,6 +635,7 @@ void launch(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* bias, 
 __global__ __launch_bounds__(256) void quant_delayed_kernel(const uint16_t* __restrict__ x, uint2* __restrict__ y, size_t n8,
                                                             const float* __restrict__ q8, float* __restrict__ part,
                                                             int phase) {
+  hq_fp8_publish_scale(q8, phase);
   const float s = delayed_scale(q8, phase);
   const float inv = 1.f / s;
   float m = 0.f;
@@ -698,16 +703,8 @@ __global__ __launch_bounds__(256) void quant_delayed_multi_kernel(const uint16_t
 // forward into 967 µs).  This single-block kernel then folds the partials into slot `phase`, clears slot
 // (phase+1)%3 and stores the scale the producer used in state[3] — segment g of a multi-segment call
 // (blockIdx.x = g) folds partials [4·blk[g], 4·blk[g+1]).
-__global__ __launch_bounds__(1024) void amax_fold_kernel(const float* __restrict__ part, const long long* __restrict__ seg,
-                                                         int nseg, long long nblk, int n, float* __restrict__ states,
-                                                         int phase, float fmax) {
-  const int g = blockIdx.x;
-  long long i0 = 0, i1 = n;
-  if (seg != nullptr) {
-    i0 = 4 * seg[4 * g + 3];
-    i1 = 4 * (g + 1 < nseg ? seg[4 * (g + 1) + 3] : nblk);
-  }
-  float* q8 = states + 4 * g;
+__device__ __forceinline__ void amax_fold_segment(const float* __restrict__ part, long long i0, long long i1,
+                                                  float* __restrict__ q8, int phase, float fmax) {
   // partial counts are multiples of 4 (4 or 8 waves per producer block): float4 loads, 4 in flight
   const float4* p4 = reinterpret_cast<const float4*>(part);
   const long long j0 = i0 >> 2, j1 = i1 >> 2;
@@ -740,6 +737,65 @@ __global__ __launch_bounds__(1024) void amax_fold_kernel(const float* __restrict
   }
 }
 
+__global__ __launch_bounds__(1024) void amax_fold_kernel(const float* __restrict__ part, const long long* __restrict__ seg,
+                                                         int nseg, long long nblk, int n, float* __restrict__ states,
+                                                         int phase, float fmax) {
+  const int g = blockIdx.x;
+  long long i0 = 0, i1 = n;
+  if (seg != nullptr) {
+    i0 = 4 * seg[4 * g + 3];
+    i1 = 4 * (g + 1 < nseg ? seg[4 * (g + 1) + 3] : nblk);
+  }
+  amax_fold_segment(part, i0, i1, states + 4 * g, phase, fmax);
+}
+
+// Deferred folds (hq_fp8_fold_defer): up to kFoldBatch sites' folds in ONE launch, block g = site g — the ~97
+// per-site single-block launches of an fp8 training step (~5 µs each, mostly launch and drain) become a handful.
+struct FoldSeg {
+  const float* part;
+  float* q8;
+  int n, phase;
+  float fmax;
+  int pad;
+};
+constexpr int kFoldBatch = 32;
+struct FoldBatch {
+  FoldSeg s[kFoldBatch];
+};
+__global__ __launch_bounds__(1024) void amax_fold_batch_kernel(FoldBatch b) {
+  const FoldSeg& g = b.s[blockIdx.x];
+  amax_fold_segment(g.part, 0, g.n, g.q8, g.phase, g.fmax);
+}
+
+// Per-device deferral state: partial slots come from one arena, bump-allocated and reset when the pending folds are
+// launched, so every pending site keeps its own partials until its fold has read them.
+struct FoldDefer {
+  bool on = false;
+  float* arena = nullptr;
+  size_t cap = 0, used = 0;
+  hipStream_t stream = nullptr;
+  std::vector<FoldSeg> pending;
+};
+constexpr size_t kFoldArena = size_t(8) << 20;   // floats (32 MiB): a BERT-large step's partials with room to spare
+FoldDefer& fold_defer() {
+  static std::vector<FoldDefer> st;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if ((int)st.size() <= dev) st.resize(dev + 1);
+  return st[dev];
+}
+
+void fold_flush(FoldDefer& d) {
+  for (size_t i = 0; i < d.pending.size(); i += kFoldBatch) {
+    FoldBatch b{};
+    const int n = (int)std::min<size_t>(kFoldBatch, d.pending.size() - i);
+    for (int j = 0; j < n; ++j) b.s[j] = d.pending[i + j];
+    hipLaunchKernelGGL(amax_fold_batch_kernel, dim3(n), dim3(1024), 0, d.stream, b);
+  }
+  d.pending.clear();
+  d.used = 0;   // stream order: the folds above read the arena before any later producer on d.stream writes it
+}
+
 }  // namespace
 
 long long hq_fp8_quant_multi_blocks(long long n8) { return (n8 + kQmBlk8 - 1) / kQmBlk8; }
@@ -753,9 +809,24 @@ void hq_fp8_quant_delayed_multi(const uint16_t* x, uint8_t* y, const long long* 
   hipLaunchKernelGGL(amax_fold_kernel, dim3(nseg), dim3(1024), 0, s, part, seg, nseg, blocks, 0, states, phase, kFp8Max);
 }
 
-float* hq_fp8_amax_parts(size_t n) {
-  // per-device scratch, grown on demand and never freed while kernels may still read it (the old block is
-  // kept: a grow happens a handful of times per process).  Producers and their fold share one stream.
+float* hq_fp8_amax_parts(size_t n, const float* q8, hipStream_t s) {
+  FoldDefer& d = fold_defer();
+  if (d.on && q8 != nullptr) {
+    // a site whose previous production still has a pending fold (its next scale reads that fold's slot), or a
+    // producer on another stream (unordered against the pending folds' partials): launch the pending folds first
+    bool flush = !d.pending.empty() && s != d.stream;
+    for (const FoldSeg& g : d.pending) flush = flush || g.q8 == q8;
+    const size_t n4 = (n + 3) & ~size_t(3);
+    if (flush || d.used + n4 > d.cap) fold_flush(d);
+    if (n4 <= d.cap) {
+      float* p = d.arena + d.used;
+      d.used += n4;
+      d.stream = s;
+      return p;
+    }
+  }
+  // immediate mode: per-device scratch, grown on demand and never freed while kernels may still read it (the old
+  // block is kept: a grow happens a handful of times per process).  Producers and their fold share one stream.
   static std::vector<std::pair<float*, size_t>> bufs;
   int dev = 0;
   (void)hipGetDevice(&dev);
@@ -772,8 +843,35 @@ float* hq_fp8_amax_parts(size_t n) {
 
 void hq_fp8_amax_fold(const float* part, int n, float* q8, int phase, hipStream_t s, float fmax) {
   if (n % 4 != 0) { fprintf(stderr, "hq_fp8_amax_fold: %d partials (must be a multiple of 4)\n", n); abort(); }
+  FoldDefer& d = fold_defer();
+  if (d.on && part >= d.arena && part < d.arena + d.cap && s == d.stream) {
+    d.pending.push_back(FoldSeg{part, q8, n, phase, fmax, 0});
+    return;
+  }
   hipLaunchKernelGGL(amax_fold_kernel, dim3(1), dim3(1024), 0, s, part, nullptr, 1, 0LL, n, q8, phase, fmax);
 }
+
+void hq_fp8_fold_flush() { fold_flush(fold_defer()); }
+
+int hq_fp8_fold_defer(int on) {
+  FoldDefer& d = fold_defer();
+  if (!on) {
+    fold_flush(d);
+    d.on = false;
+    return 0;
+  }
+  if (d.arena == nullptr) {   // allocated once, outside any graph capture (the first deferred step is eager)
+    if (hipMalloc(&d.arena, kFoldArena * sizeof(float)) != hipSuccess) {
+      fprintf(stderr, "hq_fp8_fold_defer: hipMalloc failed\n");
+      abort();
+    }
+    d.cap = kFoldArena;
+  }
+  d.on = true;
+  return 0;
+}
+
+int hq_fp8_fold_pending() { return (int)fold_defer().pending.size(); }
 
 void hq_gemm_fp8_set_variant(int v) { g_fp8_variant = v; }
 
@@ -807,7 +905,7 @@ void hq_gemm_fp8(const uint8_t* A, const uint8_t* B, uint16_t* C, const float* b
 void hq_fp8_quant_delayed(const uint16_t* x, uint8_t* y, size_t n, float* q8, int phase, hipStream_t s) {
   const size_t n8 = n / 8;
   const int grid = std::max(1, (int)std::min<size_t>((n8 + 255) / 256, 256 * 8));
-  float* part = hq_fp8_amax_parts((size_t)grid * 4);
+  float* part = hq_fp8_amax_parts((size_t)grid * 4, q8, s);
   hipLaunchKernelGGL(quant_delayed_kernel, dim3(grid), dim3(256), 0, s, x, reinterpret_cast<uint2*>(y), n8, q8, part,
                      phase);
   hq_fp8_amax_fold(part, grid * 4, q8, phase, s);

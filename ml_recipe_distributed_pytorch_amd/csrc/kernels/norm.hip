@@ -41,7 +41,10 @@ __global__ __launch_bounds__(256) void ln_fwd_rows_kernel(const uint16_t* __rest
                                                           float* __restrict__ part8, int phase) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float amax = 0.f, inv8 = 1.f;
-  if constexpr (Q8) inv8 = 1.f / hq_fp8_delayed_scale(q8, phase);
+  if constexpr (Q8) {
+    hq_fp8_publish_scale(q8, phase);
+    inv8 = 1.f / hq_fp8_delayed_scale(q8, phase);
+  }
   const int row0 = (blockIdx.x * kWaves + wave) * RPW;
   uint2 ra[RPW][NCH], rr[RES ? RPW : 1][NCH];
 #pragma unroll
@@ -193,7 +196,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
   // Q8 (--precision fp8 backward): da also as e5m2 under the delayed scale of the dgrad GEMM that consumes
   // it (state q8), so that GEMM runs on fp8 operands without a separate quantisation pass
   float inv8 = 1.f, amax8 = 0.f;
-  if constexpr (Q8) inv8 = 1.f / hq_fp8_delayed_scale(q8, phase, kHqBf8Max);
+  if constexpr (Q8) {
+    hq_fp8_publish_scale(q8, phase, kHqBf8Max);
+    inv8 = 1.f / hq_fp8_delayed_scale(q8, phase, kHqBf8Max);
+  }
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float acc[3][NCH][4];
@@ -1164,7 +1170,7 @@ void hq_ln_fwd(const uint16_t* a, const uint16_t* resid, const float* gamma, con
   const float ks = hq_keep_scale(thr);
   constexpr int rpw = 2;   // rows per wave (1 / 2 / 4 measured: profiles/r3_ln_rpw)
   const int grid = (T + kWaves * rpw - 1) / (kWaves * rpw);
-  float* part8 = y8 ? hq_fp8_amax_parts((size_t)grid * kWaves) : nullptr;
+  float* part8 = y8 ? hq_fp8_amax_parts((size_t)grid * kWaves, q8, s) : nullptr;
   dispatch_nch(H, [&](auto nch) {
     constexpr int C = decltype(nch)::value;
     auto go = [&](auto R, auto res, auto q) {
@@ -1203,7 +1209,7 @@ void hq_ln_bwd(const uint16_t* dy, const uint16_t* dy2, const uint16_t* z, const
   const HqDropKey key = hq_drop_key(seed, opid);
   const float ks = hq_keep_scale(thr);
   const int nb = hq_ln_bwd_partials(T);
-  float* part8 = da8 ? hq_fp8_amax_parts((size_t)nb * kWaves) : nullptr;
+  float* part8 = da8 ? hq_fp8_amax_parts((size_t)nb * kWaves, q8, s) : nullptr;
   dispatch_nch(H, [&](auto nch) {
     constexpr int C = decltype(nch)::value;
     auto go = [&](auto kern) {

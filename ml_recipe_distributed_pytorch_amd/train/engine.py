@@ -17,12 +17,14 @@ gradient as G accumulated micro-steps (mean of per-micro-batch means), at merged
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional
 
 import torch
 
+from .._native import kernels
 from ..models.losses import LossRecord
 from .optim import grad_norm_and_clip
 
@@ -136,6 +138,13 @@ class TrainEngine:
         self.ln_check_every = 10
         self._ln_version = getattr(model, "ln_mode_version", 0)
         self.graph_eager_steps = 0              # micro-steps of an uncaptured shape run eagerly beside the graphs
+        # --precision fp8: batch the ~97 per-site amax folds of a micro-step into a few launches at its end
+        # (HQ_FP8_FOLD_DEFER=0: one fold launch per producing site, the immediate form)
+        self.fp8_fold_defer = os.environ.get("HQ_FP8_FOLD_DEFER", "1") == "1"
+
+    def _fp8_defer_folds(self) -> bool:
+        return (self.fp8_fold_defer and getattr(self.model, "precision", "bf16") == "fp8"
+                and self.model.store.device.type == "cuda")
 
     @property
     def device(self):
@@ -309,10 +318,17 @@ class TrainEngine:
         boundary = (self.micro + 1) % self.batch_split == 0
         if self.reducer is not None:
             self.reducer.prepare(sync=boundary or not self.no_sync_accum)
-        preds = self.model(**inputs)
-        loss = self.loss_fn(preds, labels)
-        timer.mark("fwd")
-        self._backward(loss)
+        defer = self._fp8_defer_folds()
+        if defer:   # the fp8 sites' amax folds run batched at the end of the micro-step (gemm_fp8.hip, FoldDefer)
+            kernels().fp8_fold_defer(True)
+        try:
+            preds = self.model(**inputs)
+            loss = self.loss_fn(preds, labels)
+            timer.mark("fwd")
+            self._backward(loss)
+        finally:
+            if defer:
+                kernels().fp8_fold_defer(False)   # launches the pending folds
         if self.reducer is not None and not boundary and not self.no_sync_accum:
             self.reducer.finalize()
         timer.mark("bwd")

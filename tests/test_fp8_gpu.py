@@ -552,3 +552,44 @@ def test_gemm_fp8_persistent_matches_per_tile(cuda, epi, q8):
         if key in kw2:
             assert torch.equal(kw2[key].view(torch.uint8) if kw2[key].element_size() == 1 else kw2[key],
                                kw3[key].view(torch.uint8) if kw3[key].element_size() == 1 else kw3[key]), key
+
+
+@pytest.mark.gpu
+def test_fp8_deferred_amax_folds_match_immediate(cuda):
+    """TrainEngine under --precision fp8 with the sites' amax folds batched at the end of each micro-step
+    (gemm_fp8.hip FoldDefer; producers publish their dequant scale themselves) against one fold launch per site:
+    bitwise the same losses, weights and delayed-scaling states over steps that cross calibration, with a 2-way
+    accumulation (every state produced twice per optimizer step) and nothing left pending afterwards."""
+    from types import SimpleNamespace
+    from ml_recipe_distributed_pytorch_amd.data.dummy import SpecialIds, synth_batch_native
+    from ml_recipe_distributed_pytorch_amd.models.bert import BertForQuestionAnswering
+    from ml_recipe_distributed_pytorch_amd.models.config import get_config
+    from ml_recipe_distributed_pytorch_amd.models.losses import build_loss
+    from ml_recipe_distributed_pytorch_amd.train.engine import TrainEngine, to_device
+    from ml_recipe_distributed_pytorch_amd.train.optim import FusedAdamW
+    from ml_recipe_distributed_pytorch_amd.train.trainer import optimizer_groups
+    k = _native.kernels()
+    cfg = get_config("bert-base-uncased", num_hidden_layers=2)
+    lp = SimpleNamespace(loss="smooth", smooth_alpha=0.01, w_start=1, w_end=1, w_start_reg=1, w_end_reg=1, w_cls=1)
+    batches = [synth_batch_native(8, 256, 64, SpecialIds(), seed=s) for s in range(8)]
+    runs = {}
+    for defer in (False, True):
+        torch.manual_seed(0)
+        m = BertForQuestionAnswering(cfg, seed=0, precision="fp8").to(cuda).train()
+        opt = FusedAdamW(optimizer_groups(m.named_parameters(), 1e-4), m.store, lr=1e-4, correct_bias=False,
+                         zero_grad_fn=m.zero_grad)
+        eng = TrainEngine(m, build_loss(lp), opt, batch_split=2)
+        eng.fp8_fold_defer = defer
+        losses = []
+        for i in range(0, 8, 2):
+            mb = [(to_device(batches[j][0], cuda), to_device(batches[j][1], cuda)) for j in (i, i + 1)]
+            losses.append(eng.step(mb).losses.to_floats()["loss"])
+        torch.cuda.synchronize()
+        assert k.fp8_fold_pending() == 0
+        states = [s.buf.clone() for st in (m.fp8_states(l) for l in range(2)) for s in st.values()]
+        runs[defer] = (losses, m.store.master.clone(), states)
+    (l0, w0, s0), (l1, w1, s1) = runs[False], runs[True]
+    assert l0 == l1
+    assert torch.equal(w0, w1)
+    assert len(s0) == len(s1) > 0 and all(torch.equal(a, b) for a, b in zip(s0, s1))
+    assert any(a[:3].abs().sum().item() > 0 for a in s1)
