@@ -22,6 +22,9 @@ def main():
     ap.add_argument("--last", type=int, default=5)
     ap.add_argument("--top", type=int, default=40)
     ap.add_argument("--marker", default="adamw_kernel")
+    ap.add_argument("--gaps", type=int, default=0,
+                    help="also list the N largest idle gaps (previous kernel's end -> next kernel's start) of those "
+                         "steps, grouped by the kernel pair around them")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     ends = [i for i, r in enumerate(rows) if a.marker in r["Kernel_Name"]]
@@ -44,6 +47,22 @@ def main():
         print(f"{k[:60]:60s} {c // n:7d} {t / 1e3 / n:9.3f} {t / c:9.1f} {100 * t / busy:6.2f}")
     print(f"{'TOTAL (kernel time)':60s} {'':7s} {busy / 1e3 / n:9.3f}")
     print(f"{'SPAN (wall, first to last step end)':60s} {'':7s} {span / 1e3 / n:9.3f}")
+    if a.gaps:
+        # idle time between consecutive kernels (one stream's view: overlapping kernels give no gap)
+        gaps, end = {}, int(rows[lo - 1]["End_Timestamp"])
+        prev = short(rows[lo - 1]["Kernel_Name"])
+        for r in sel:
+            st, k = int(r["Start_Timestamp"]), short(r["Kernel_Name"])
+            g = (st - end) / 1e3
+            if g > 0:
+                t, c = gaps.get((prev, k), (0.0, 0))
+                gaps[(prev, k)] = (t + g, c + 1)
+            if int(r["End_Timestamp"]) > end:
+                end, prev = int(r["End_Timestamp"]), k
+        tot = sum(t for t, _ in gaps.values())
+        print(f"\nidle gaps: {tot / 1e3 / n:.3f} ms/step; largest (us/step, count/step): previous -> next kernel")
+        for (pk, nk), (t, c) in sorted(gaps.items(), key=lambda kv: -kv[1][0])[: a.gaps]:
+            print(f"{t / n:9.1f} {c / n:6.1f}  {pk[:45]} -> {nk[:45]}")
 
 
 if __name__ == "__main__":
