@@ -211,11 +211,14 @@ def main():
     for e in events:
         e.record()
     step_no = [0]
+    host_wait = [0.0]   # host time blocked on the slot events: ~0 means the host, not the GPU, paces the loop
 
     def next_batch():
         i = step_no[0]
         s = i % 2
+        t_w = time.perf_counter()
         events[s].synchronize()              # previous H2D out of this pinned slot has finished
+        host_wait[0] += time.perf_counter() - t_w
         inputs, labels = slots[s]
         from ml_recipe_distributed_pytorch_amd.data.dummy import _refill
         _refill(slots[s], sp, Q, seed=rank * 1_000_003 + 7919 * (i + 2))
@@ -242,12 +245,14 @@ def main():
         hqdist.barrier()
     torch.cuda.synchronize()
     bytes0 = reducer.stats["bytes"] if reducer is not None else 0
+    host_wait[0] = 0.0
     t0 = time.perf_counter()
     phase = {}
     for _ in range(args.steps):
         res = one_step()
         for k, v in res.timings.items():
             phase[k] = phase.get(k, 0.0) + v
+    t_host = time.perf_counter() - t0        # the host's own time to issue the K steps (before the final drain)
     torch.cuda.synchronize()
     if launched:
         hqdist.barrier()
@@ -311,6 +316,10 @@ def main():
                           if reducer is not None and comm.get("comm_span_ms") else None),
            "mfu_bf16_dense": round(value * flops_per_sample / (world * 2.5e15), 4),
            "max_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2),
+           # host pacing diagnostic (rank 0): per step, the host's issue time and its time blocked on the input slots'
+           # events; a blocked time near 0 means the host, not the GPU, sets the step time
+           "host_issue_ms": round(t_host / args.steps * 1e3, 3),
+           "host_blocked_ms": round(host_wait[0] / args.steps * 1e3, 3),
            "final_loss": round(final_loss, 4),
            # cross-rank replica check (null without a reducer): exact fingerprints of the fp32 master arena and of
            # an untimed extra step's reduced gradients, every rank vs rank 0
