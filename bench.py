@@ -207,24 +207,49 @@ def main():
                     "bert" if cfg.family == "bert" else "roberta")
     B, L, Q = args.batch, args.seq, 64
     slots = [synth_batch_native(B, L, Q, sp, seed=rank * 1_000_003 + i) for i in range(2)]
-    events = [torch.cuda.Event() for _ in slots]
+    from ml_recipe_distributed_pytorch_amd.data.dummy import _refill
+    from ml_recipe_distributed_pytorch_amd.train.engine import DevicePrefetcher, to_device
+    # batch i+1 is synthesised into its pinned slot and copied to the GPU on a copy stream while step i runs
+    # (DevicePrefetcher: a copy issued on the compute stream left the GPU idle at every step boundary)
+    prefetcher = DevicePrefetcher(device)
+    copy_done = [None, None]   # per pinned slot: the event of the last copy out of it
+    events = [torch.cuda.Event() for _ in slots]   # compute stream, per slot: keeps the host <= 2 steps ahead
     for e in events:
         e.record()
     step_no = [0]
+    pending = [None]
     host_wait = [0.0]   # host time blocked on the slot events: ~0 means the host, not the GPU, paces the loop
+
+    # HQ_BENCH_PREFETCH=0 (A/B only): each batch copied on the compute stream at its own step, the pre-prefetch form
+    early = os.environ.get("HQ_BENCH_PREFETCH", "1") == "1"
+
+    def issue(i):
+        s = i % 2
+        if copy_done[s] is not None:
+            copy_done[s].synchronize()       # the copy of batch i-2 out of this slot has finished
+        inputs, labels = slots[s]
+        _refill(slots[s], sp, Q, seed=rank * 1_000_003 + 7919 * (i + 2))
+        if not early:
+            dev = to_device((inputs, labels), device)
+            ev = torch.cuda.Event()
+            ev.record()
+            copy_done[s] = ev
+            return dev, None
+        item = prefetcher.issue((inputs, labels))
+        copy_done[s] = item[1]
+        return item
 
     def next_batch():
         i = step_no[0]
         s = i % 2
         t_w = time.perf_counter()
-        events[s].synchronize()              # previous H2D out of this pinned slot has finished
+        events[s].synchronize()              # the compute stream has reached step i-2
         host_wait[0] += time.perf_counter() - t_w
-        inputs, labels = slots[s]
-        from ml_recipe_distributed_pytorch_amd.data.dummy import _refill
-        _refill(slots[s], sp, Q, seed=rank * 1_000_003 + 7919 * (i + 2))
-        dev_in = {k: v.to(device, non_blocking=True) for k, v in inputs.items()}
-        dev_lb = {k: v.to(device, non_blocking=True) for k, v in labels.items()}
+        if pending[0] is None or not early:
+            pending[0] = issue(i)
+        dev_in, dev_lb = prefetcher.claim(pending[0])
         events[s].record()
+        pending[0] = issue(i + 1) if early else None   # overlaps step i on the copy stream
         step_no[0] += 1
         return dev_in, dev_lb
 

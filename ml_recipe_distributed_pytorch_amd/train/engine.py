@@ -39,6 +39,68 @@ def to_device(data, device, non_blocking=True):
     return data
 
 
+def _tensors(data):
+    if isinstance(data, (list, tuple)):
+        for d in data:
+            yield from _tensors(d)
+    elif isinstance(data, dict):
+        for d in data.values():
+            yield from _tensors(d)
+    elif torch.is_tensor(data):
+        yield data
+
+
+class DevicePrefetcher:
+    """Host → device copies of upcoming batches on a copy stream, one batch ahead of the compute stream.
+
+    A pinned-memory copy issued on the compute stream waited there behind the previous optimizer step: every step
+    boundary left the GPU idle ~0.25 ms between the AdamW kernel and the next batch's first kernel while the runtime
+    serviced the copies (``profiles/r6_s3/gaps_*.txt``, ``tools/trace_steps.py --gaps``).  Issued one batch early on
+    their own stream, the copies run under the previous step's kernels and the compute stream only waits on an event
+    that has long completed.  ``issue`` starts a copy, ``claim`` makes the current stream wait for it (and tells the
+    caching allocator that stream uses the tensors).  On CPU both are plain ``to_device``."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+
+    def issue(self, data):
+        if self.stream is None:
+            return to_device(data, self.device), None
+        # no wait on the compute stream: the copy must not queue behind the step it is meant to overlap (the
+        # device buffers come from this stream's own pool, and the pinned source is the caller's to keep intact)
+        with torch.cuda.stream(self.stream):
+            dev = to_device(data, self.device)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return dev, ev
+
+    def claim(self, item):
+        dev, ev = item
+        if ev is not None:
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_event(ev)
+            for t in _tensors(dev):
+                t.record_stream(cur)
+        return dev
+
+
+def prefetch_to_device(iterable, device):
+    """Yield the items of ``iterable`` already on ``device``, each one's copy issued while the previous item is in
+    use (``DevicePrefetcher``)."""
+    pf = DevicePrefetcher(device)
+    it = iter(iterable)
+    try:
+        nxt = pf.issue(next(it))
+    except StopIteration:
+        return
+    for data in it:
+        cur = pf.claim(nxt)
+        nxt = pf.issue(data)
+        yield cur
+    yield pf.claim(nxt)
+
+
 class PhaseTimer:
     """Per-phase step timer.  On GPU it records HIP events on the compute stream (no per-phase
     synchronisation; ``resolve`` waits for the last event once per step, profiling runs only);

@@ -38,7 +38,7 @@ from ..parallel.reducer import GradReducer
 from ..utils.tb import SummaryWriter
 from .callbacks import TestCallback
 from .amp import apex_to_precision, resolve_precision  # noqa: F401  (apex_to_precision re-exported)
-from .engine import TrainEngine, to_device
+from .engine import TrainEngine, prefetch_to_device, to_device
 from .meters import AverageMeter
 from .optim import get_linear_schedule_with_warmup
 
@@ -306,14 +306,14 @@ class Trainer:
             trace_mb = int(self.train_batch_size // self.batch_split)
         data = tqdm(loader, desc=f"Train (epoch #{epoch_i} / {self.n_epochs})",
                     disable=self.rank != 0 or not logger.isEnabledFor(logging.INFO))
-        for i, (inputs, labels) in enumerate(data):
+        # each micro-batch's host → device copy runs on a copy stream under the previous micro-step (DevicePrefetcher)
+        for i, (inputs, labels) in enumerate(prefetch_to_device(data, self.device)):
             if trace:
                 import json
                 with open(trace, "a") as f:
                     f.write(json.dumps({"epoch": epoch_i, "rank": self.rank,
                                         "idx": [int(x) for x in order[(skip + i) * trace_mb:(skip + i + 1) * trace_mb]]})
                             + "\n")
-            inputs, labels = self._to_device((inputs, labels))
             res = self.engine.micro_step(inputs, labels)
             if res is None:
                 continue

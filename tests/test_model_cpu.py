@@ -269,3 +269,15 @@ def test_engine_graph_key_includes_segment_lengths():
     b = TrainEngine._shape_key({"input_ids": ids}, {"segments": torch.tensor([16, 9]), "segment_lengths": (16, 9)})
     c = TrainEngine._shape_key({"input_ids": ids}, {"segments": torch.tensor([16, 9]), "segment_lengths": (16, 9)})
     assert a != b and b == c
+
+
+def test_prefetch_to_device_cpu_yields_items_in_order():
+    """The trainer's prefetcher on CPU: every item, in order, tensors equal to the source (plain to_device)."""
+    import torch
+    from ml_recipe_distributed_pytorch_amd.train.engine import prefetch_to_device
+    items = [({"a": torch.arange(4) + i}, {"b": torch.ones(2) * i}) for i in range(5)]
+    out = list(prefetch_to_device(items, "cpu"))
+    assert len(out) == 5
+    for i, (x, y) in enumerate(out):
+        assert torch.equal(x["a"], torch.arange(4) + i) and torch.equal(y["b"], torch.ones(2) * i)
+    assert list(prefetch_to_device([], "cpu")) == []
