@@ -170,22 +170,33 @@ __global__ __launch_bounds__(256) void qa_heads_fwd_kernel(FwdArgs a) {
   float acc[8];
 #pragma unroll
   for (int s = 0; s < 8; ++s) acc[s] = 0.f;
-  for (int k0 = 0; k0 < H; k0 += 64) {
-    {
-      const int s = tid >> 3, kk = (tid & 7) * 8, b = sb * 32 + s;
-      float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (b < a.B) ld8f<TS>(a.seq, (size_t)b * a.L * H + k0 + kk, f);
-      *reinterpret_cast<float4*>(xs + s * 64 + kk) = make_float4(f[0], f[1], f[2], f[3]);
-      *reinterpret_cast<float4*>(xs + s * 64 + kk + 4) = make_float4(f[4], f[5], f[6], f[7]);
-    }
+  // the next K chunk's global loads are issued before this chunk's FMAs (register double buffer); with the parallel
+  // partial fold below the kernel went 103.4 -> 86.6 µs at B = 256, L = 384 (profiles/r6_s3_heads)
+  const int xs_s = tid >> 3, xs_k = (tid & 7) * 8, xs_b = sb * 32 + xs_s;
+  float f[8];
+  float4 wq[4];
+  auto load_chunk = [&](int k0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = 0.f;
+    if (xs_b < a.B) ld8f<TS>(a.seq, (size_t)xs_b * a.L * H + k0 + xs_k, f);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int idx = tid + q * 256, r = idx >> 4, c4 = (idx & 15) * 4;
-      const float4 v = *reinterpret_cast<const float4*>(a.wp + (size_t)(jb * 64 + r) * H + k0 + c4);
+      wq[q] = *reinterpret_cast<const float4*>(a.wp + (size_t)(jb * 64 + r) * H + k0 + c4);
+    }
+  };
+  load_chunk(0);
+  for (int k0 = 0; k0 < H; k0 += 64) {
+    *reinterpret_cast<float4*>(xs + xs_s * 64 + xs_k) = make_float4(f[0], f[1], f[2], f[3]);
+    *reinterpret_cast<float4*>(xs + xs_s * 64 + xs_k + 4) = make_float4(f[4], f[5], f[6], f[7]);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int idx = tid + q * 256, r = idx >> 4, c4 = (idx & 15) * 4;
       float* d = ws + r * 65 + c4;
-      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+      d[0] = wq[q].x; d[1] = wq[q].y; d[2] = wq[q].z; d[3] = wq[q].w;
     }
     __syncthreads();
+    if (k0 + 64 < H) load_chunk(k0 + 64);
 #pragma unroll 4
     for (int kk = 0; kk < 64; kk += 4) {
       const float w0 = ws[lane * 65 + kk], w1 = ws[lane * 65 + kk + 1], w2 = ws[lane * 65 + kk + 2],
@@ -227,8 +238,15 @@ __global__ __launch_bounds__(256) void qa_heads_fwd_kernel(FwdArgs a) {
   for (int idx = tid; idx < a.B * nout; idx += 256) {
     const int b = idx / nout, c = idx % nout;
     const int col = c < a.NL ? c : 8 + (c - a.NL);
+    // every partial's load in flight at once (nj <= 4·NCH), then the sum in the same q order (bitwise the old result):
+    // the loop of dependent load → add steps was 12 L2 round trips per output, 7 outputs per thread, in ONE block
+    float v[4 * NCH];
+#pragma unroll
+    for (int q = 0; q < 4 * NCH; ++q) v[q] = q < nj ? a.hpart[((size_t)q * a.B + b) * kHS + col] : 0.f;
     float s = 0.f;
-    for (int q = 0; q < nj; ++q) s += a.hpart[((size_t)q * a.B + b) * kHS + col];
+#pragma unroll
+    for (int q = 0; q < 4 * NCH; ++q)
+      if (q < nj) s += v[q];
     if (c < a.NL) a.cls[(size_t)b * a.NL + c] = s + a.bc[c];
     else if (c == a.NL) a.reg[2 * b] = sigmoidf_(s + a.brs[0]);
     else a.reg[2 * b + 1] = sigmoidf_(s + a.bre[0]);
