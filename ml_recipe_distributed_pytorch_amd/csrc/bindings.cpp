@@ -798,9 +798,10 @@ Tensor qa_heads_bwd(Tensor seq, int64_t L, Tensor dlog, Tensor dheads, c10::opti
   c10::DeviceGuard g(seq.device());
   auto dseq = at::empty_like(seq);
   auto part = at::empty({(int64_t)hq_qa_heads_bwd_span_blocks((int)T), 2 * H + 2}, pooled.options());
+  auto dpre = at::empty({B, H}, pooled.options());
   hq_qa_heads_bwd(seq.data_ptr(), ptr<float>(dlog), ptr<float>(dheads), optr<float>(gscale), ptr<float>(pooled),
                   ptr<float>(reg), hw, gg, dseq.data_ptr(), ptr<float>(part), (int)B, (int)L, (int)H, (int)NL,
-                  accumulate, (float)p, u32(seed), u32(opid), cur_stream(), seq.scalar_type() == F32);
+                  accumulate, (float)p, u32(seed), u32(opid), cur_stream(), seq.scalar_type() == F32, ptr<float>(dpre));
   return dseq;
 }
 

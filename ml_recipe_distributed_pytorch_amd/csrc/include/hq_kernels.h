@@ -273,4 +273,4 @@ int hq_qa_heads_bwd_span_blocks(int T);         // rows of the [rows][2H + 2] sp
 void hq_qa_heads_bwd(const void* seq, const float* dlog, const float* dheads, const float* gscale, const float* pooled,
                      const float* reg, const HqHeadWeights& w, const HqHeadGrads& g, void* dseq, float* span_part,
                      int B, int L, int H, int NL, bool accumulate, float p, uint32_t seed, uint32_t opid, hipStream_t s,
-                     bool seq_f32 = false);
+                     bool seq_f32 = false, float* dpre = nullptr);   // dpre: [B][H] scratch (dL/d pooler pre-activation)

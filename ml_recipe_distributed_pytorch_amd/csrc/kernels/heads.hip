@@ -471,6 +471,7 @@ struct BwdArgs {
   HqDropKey kd;
   uint32_t thr;
   float ks;
+  float* dpre;   // [B][H] dL/d(pooler pre-activation), written by qa_dpre_kernel before the backward (or null: recomputed)
 };
 
 // per-sample backward scalars: [0, NL) gs·dcls, 8 / 9 = gs·dreg·σ'(pre) for start / end
@@ -494,6 +495,20 @@ __device__ __forceinline__ float dpre_at(const BwdArgs& a, uint32_t key, int b, 
 }
 
 __device__ __forceinline__ void put(float* p, float v, int acc) { *p = acc ? *p + v : v; }
+
+// dpre [B][H] once per backward: the dx tiles (R1, 12 column blocks per sample block) and the dWp tiles (R2, 12 row
+// blocks per k block) each recomputed it for every element they read — the same dpre_at call, so the same bits
+__global__ __launch_bounds__(256) void qa_dpre_kernel(BwdArgs a) {
+  const uint32_t key = a.kd.get();
+  const float gs = a.gscale ? *a.gscale : 1.f;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)a.B * a.H) return;
+  const int b = (int)(i / a.H), k = (int)(i % a.H);
+  float sc[kHS];
+#pragma unroll
+  for (int c = 0; c < kHS; ++c) sc[c] = sample_scalar(a, b, c, gs);
+  a.dpre[i] = dpre_at(a, key, b, k, sc);
+}
 
 template <int NCH, typename TS>
 __global__ __launch_bounds__(256) void qa_heads_bwd_kernel(BwdArgs a) {
@@ -520,7 +535,8 @@ __global__ __launch_bounds__(256) void qa_heads_bwd_kernel(BwdArgs a) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int s = wv + 4 * q, b = sb * 32 + s;
-        dp[s * 64 + lane] = b < B ? dpre_at(a, key, b, k0 + lane, scs + s * kHS) : 0.f;
+        dp[s * 64 + lane] = b >= B ? 0.f
+                            : a.dpre ? a.dpre[(size_t)b * H + k0 + lane] : dpre_at(a, key, b, k0 + lane, scs + s * kHS);
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -572,7 +588,9 @@ __global__ __launch_bounds__(256) void qa_heads_bwd_kernel(BwdArgs a) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int s = wv + 4 * q, b = b0 + s;
-        dp[s * 64 + lane] = b < B ? dpre_at(a, key, b, kb * 64 + lane, scs + s * kHS) : 0.f;
+        dp[s * 64 + lane] = b >= B ? 0.f
+                            : a.dpre ? a.dpre[(size_t)b * H + kb * 64 + lane]
+                                     : dpre_at(a, key, b, kb * 64 + lane, scs + s * kHS);
         xs[s * 64 + lane] = b < B ? ld1f<TS>(a.seq, (size_t)b * a.L * H + ib * 64 + lane) : 0.f;
       }
       __syncthreads();
@@ -787,8 +805,9 @@ int hq_qa_heads_bwd_span_blocks(int T) { return (T + 4 * kSpanRPW - 1) / (4 * kS
 void hq_qa_heads_bwd(const void* seq, const float* dlog, const float* dheads, const float* gscale, const float* pooled,
                      const float* reg, const HqHeadWeights& w, const HqHeadGrads& g, void* dseq, float* span_part,
                      int B, int L, int H, int NL, bool accumulate, float p, uint32_t seed, uint32_t opid, hipStream_t s,
-                     bool seq_f32) {
+                     bool seq_f32, float* dpre) {
   BwdArgs a;
+  a.dpre = dpre;
   a.seq = seq; a.dlog = dlog; a.dheads = dheads; a.gscale = gscale; a.pooled = pooled; a.reg = reg;
   a.wp = w.wp; a.wc = w.wc; a.wrs = w.wrs; a.wre = w.wre; a.wsp = w.wsp;
   a.dseq = dseq; a.span_part = span_part;
@@ -806,6 +825,7 @@ void hq_qa_heads_bwd(const void* seq, const float* dlog, const float* dheads, co
   size_t lds = (32 * kHS + 32 * 64 + 64 * 64) * sizeof(float);                     // R1
   lds = std::max(lds, (size_t)4 * 64 * (kMaxNL + 3) * sizeof(float));              // R3
   lds = std::max(lds, (size_t)4 * (2 * H + 2) * sizeof(float));                    // R4
+  if (dpre) hipLaunchKernelGGL(qa_dpre_kernel, dim3((unsigned)(((size_t)B * H + 255) / 256)), dim3(256), 0, s, a);
   dispatch_nch(H, [&](auto nch) {
     if (seq_f32)
       hipLaunchKernelGGL((qa_heads_bwd_kernel<decltype(nch)::value, float>), dim3(a.nA + a.nW + a.nS + nspan), dim3(256),
